@@ -1,0 +1,288 @@
+"""Golden-vector generator for the NPG / TRPO / DAPG update path.
+
+Runs the REFERENCE update code (bennevans/mjrl, mounted read-only at
+/root/reference) on synthetic, seeded `paths` and stores inputs plus every
+intermediate the parity tests check as small .npz fixtures next to this file.
+
+Build-container only: /root/reference does not exist on the GPU box; the GPU box
+only ever reads the committed .npz files.  Nothing from the reference is copied:
+the fixtures are data (inputs and the outputs the reference produced).
+
+Import recipe: `mjrl.algos.*` imports the samplers, which
+import gym; the update path never calls gym, so a stub module is installed
+before import.  torch runs single-threaded so a re-run reproduces the files.
+
+Captured per case (reference call sites in brackets):
+  returns / baseline / advantages   process_samples.compute_returns/_advantages
+                                    (utils/process_samples.py:3-35)
+  adv_whitened                      argument of the first CPI_surrogate call
+                                    (algos/npg_cg.py:91,113)
+  mean0 / ll0                       MLP.mean_LL at the initial params
+                                    (policies/gaussian_mlp.py:100-110)
+  surr_calls / kl_calls             every CPI_surrogate / kl_old_new result in order
+                                    (algos/batch_reinforce.py:37-49)
+  vpg_grad                          flat_vpg result (batch_reinforce.py:51-55)
+  hvp_v / hvp_out                   NPG.HVP(obs, act, v) for a fixed random v
+                                    (algos/npg_cg.py:55-74)
+  cg_b / cg_p / cg_z / cg_x         cg_solve trace: rhs, every f_Ax input / output,
+                                    the solution (utils/cg_solve.py:3-22)
+  theta0 / theta1                   get_param_values before / after the update
+  base_stats, log_*                 return value of train_from_paths and DataLog
+"""
+import os
+import sys
+import types
+
+sys.dont_write_bytecode = True
+REF = "/root/reference"
+sys.path.insert(0, REF)
+sys.modules.setdefault("gym", types.ModuleType("gym"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+torch.set_num_threads(1)
+
+from mjrl.utils.gym_env import EnvSpec  # noqa: E402
+from mjrl.policies.gaussian_mlp import MLP  # noqa: E402
+from mjrl.policies.gaussian_linear import LinearPolicy  # noqa: E402
+from mjrl.baselines.linear_baseline import LinearBaseline  # noqa: E402
+from mjrl.algos.npg_cg import NPG  # noqa: E402
+from mjrl.algos.trpo import TRPO  # noqa: E402
+from mjrl.algos.dapg import DAPG  # noqa: E402
+import mjrl.algos.npg_cg as npg_mod  # noqa: E402
+import mjrl.algos.trpo as trpo_mod  # noqa: E402
+import mjrl.algos.dapg as dapg_mod  # noqa: E402
+import mjrl.utils.process_samples as process_samples  # noqa: E402
+from mjrl.utils.cg_solve import cg_solve as ref_cg_solve  # noqa: E402
+
+OUT = os.path.dirname(os.path.abspath(__file__))
+CG_KEEP = 3
+
+
+def make_paths(rs, n, m, lengths, terminated):
+    """Synthetic paths in the sampler wire format (samplers/base_sampler.py:76-83).
+    obs / act are drawn as f32-representable doubles so the fixture can store them
+    as float32 losslessly."""
+    paths = []
+    for H, term in zip(lengths, terminated):
+        obs = rs.randn(H, n).astype(np.float32).astype(np.float64)
+        act = rs.randn(H, m).astype(np.float32).astype(np.float64)
+        rew = rs.randn(H)
+        paths.append(dict(observations=obs, actions=act, rewards=rew,
+                          agent_infos={}, env_infos={}, terminated=bool(term)))
+    return paths
+
+
+class Recorder:
+    """Wraps agent methods / cg_solve to record what the reference computes."""
+
+    def __init__(self, agent, modules):
+        self.agent = agent
+        self.surr = []
+        self.kl = []
+        self.adv_w = None
+        self.vpg = []
+        self.cg = None
+        self._orig = {}
+        a = agent
+        orig_surr, orig_kl, orig_vpg = a.CPI_surrogate, a.kl_old_new, a.flat_vpg
+
+        def surr(obs, act, adv):
+            if self.adv_w is None:
+                self.adv_w = np.array(adv, dtype=np.float64, copy=True)
+            out = orig_surr(obs, act, adv)
+            self.surr.append(float(out.data.numpy().ravel()[0]))
+            return out
+
+        def kl(obs, act):
+            out = orig_kl(obs, act)
+            self.kl.append(float(out.data.numpy().ravel()[0]))
+            return out
+
+        def vpg(obs, act, adv):
+            g = orig_vpg(obs, act, adv)
+            self.vpg.append(np.array(g, copy=True))
+            return g
+
+        a.CPI_surrogate, a.kl_old_new, a.flat_vpg = surr, kl, vpg
+
+        def cg(f_Ax, b, x_0=None, cg_iters=10, residual_tol=1e-10):
+            trace = dict(b=np.array(b, copy=True), p=[], z=[])
+
+            def f(p):
+                z = f_Ax(p)
+                trace["p"].append(np.array(p, copy=True))
+                trace["z"].append(np.array(z, copy=True))
+                return z
+
+            x = ref_cg_solve(f, b, x_0=x_0, cg_iters=cg_iters, residual_tol=residual_tol)
+            trace["x"] = np.array(x, copy=True)
+            self.cg = trace
+            return x
+
+        for mod in modules:
+            self._orig[mod] = mod.cg_solve
+            mod.cg_solve = cg
+
+    def restore(self):
+        for mod, fn in self._orig.items():
+            mod.cg_solve = fn
+
+
+def concat(paths, key):
+    return np.concatenate([p[key] for p in paths])
+
+
+def run_case(name, *, n, m, hidden, lengths, terminated, algo, algo_kwargs,
+             gamma=0.995, gae_lambda=0.97, seed=123, policy_seed=0,
+             log_std=None, transforms=None, demo=None, linear=False,
+             baseline_fit=True):
+    rs = np.random.RandomState(seed)
+    spec = EnvSpec(n, m, max(lengths), 1)
+    if linear:
+        policy = LinearPolicy(spec, seed=policy_seed)
+    else:
+        policy = MLP(spec, hidden_sizes=hidden, seed=policy_seed)
+    if transforms is not None:
+        for mdl in (policy.model, policy.old_model):
+            mdl.set_transformations(*transforms)
+    if log_std is not None:
+        th = policy.get_param_values()
+        th[-m:] = log_std
+        policy.set_param_values(th, set_new=True, set_old=True)
+    paths = make_paths(rs, n, m, lengths, terminated)
+    demo_paths = None
+    if demo is not None:
+        demo_paths = make_paths(rs, n, m, demo, [True] * len(demo))
+
+    baseline = LinearBaseline(spec)
+    if baseline_fit:
+        process_samples.compute_returns(paths, gamma)
+        baseline.fit(paths)
+
+    if algo == "npg":
+        agent = NPG(None, policy, baseline, save_logs=True, **algo_kwargs)
+    elif algo == "trpo":
+        agent = TRPO(None, policy, baseline, save_logs=True, **algo_kwargs)
+    elif algo == "dapg":
+        agent = DAPG(None, policy, baseline, demo_paths=demo_paths, save_logs=True, **algo_kwargs)
+    else:
+        raise ValueError(algo)
+
+    theta0 = policy.get_param_values()
+    obs = concat(paths, "observations")
+    act = concat(paths, "actions")
+    mean0, ll0 = policy.mean_LL(obs, act)
+    vrs = np.random.RandomState(seed + 7)
+    hvp_v = vrs.randn(policy.d).astype(np.float32)
+    hvp_out = agent.HVP(obs, act, hvp_v)
+
+    # the update proper (batch_reinforce.py:86-91 minus sampling and fit)
+    process_samples.compute_returns(paths, gamma)
+    process_samples.compute_advantages(paths, baseline, gamma, gae_lambda)
+    rec = Recorder(agent, [npg_mod, trpo_mod, dapg_mod])
+    try:
+        base_stats = agent.train_from_paths(paths)
+    finally:
+        rec.restore()
+    theta1 = policy.get_param_values()
+    keep = len(rec.cg["p"]) if policy.d <= 10000 else CG_KEEP
+
+    out = dict(
+        n=n, m=m, hidden=np.array(hidden if not linear else (0, 0)), linear=int(linear),
+        algo=algo, gamma=gamma, gae_lambda=(np.nan if gae_lambda is None else gae_lambda),
+        lengths=np.array(lengths, dtype=np.int64),
+        terminated=np.array(terminated, dtype=np.uint8),
+        obs=obs.astype(np.float32), act=act.astype(np.float32),
+        rewards=concat(paths, "rewards"),
+        baseline_coeffs=(baseline._coeffs if baseline._coeffs is not None else np.zeros(0)),
+        baseline=concat(paths, "baseline"),
+        returns=concat(paths, "returns"),
+        advantages=concat(paths, "advantages"),
+        adv_whitened=rec.adv_w,
+        theta0=theta0, theta1=theta1,
+        param_sizes=np.array(policy.param_sizes, dtype=np.int64),
+        mean0=mean0.data.numpy(), ll0=ll0.data.numpy(),
+        hvp_v=hvp_v, hvp_out=hvp_out,
+        surr_calls=np.array(rec.surr), kl_calls=np.array(rec.kl),
+        vpg_grad=rec.vpg[0],
+        # large-d cases keep the first CG_KEEP iterations of the trace (fixture size)
+        cg_b=rec.cg["b"], cg_p=np.array(rec.cg["p"][:keep]), cg_z=np.array(rec.cg["z"][:keep]),
+        cg_iters_run=len(rec.cg["p"]),
+        cg_x=rec.cg["x"],
+        base_stats=np.array(base_stats, dtype=np.float64),
+        running_score=agent.running_score,
+    )
+    for k, v in agent.logger.log.items():
+        out["log_" + k] = np.array(v[-1], dtype=np.float64)
+    for k, v in algo_kwargs.items():
+        out["kw_" + k] = np.array(np.nan if v is None else v, dtype=np.float64) \
+            if not isinstance(v, dict) else np.array([v["iters"], v["damping"]], dtype=np.float64)
+    if transforms is not None:
+        for k, v in zip(("in_shift", "in_scale", "out_shift", "out_scale"), transforms):
+            out[k] = np.float32(v)
+    if demo_paths is not None:
+        out["demo_lengths"] = np.array(demo, dtype=np.int64)
+        out["demo_obs"] = concat(demo_paths, "observations").astype(np.float32)
+        out["demo_act"] = concat(demo_paths, "actions").astype(np.float32)
+        out["demo_iter_count"] = agent.iter_count
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), **out)
+    print("%-22s T=%-6d d=%-6d surr=%s kl=%s alpha=%.6g" % (
+        name, obs.shape[0], policy.d, rec.surr[:2], rec.kl[-1:], out.get("log_alpha", np.nan)))
+    return out
+
+
+def main():
+    # C1: point_mass shape, linear Gaussian policy (tests/point_mass_test.py, config 1)
+    run_case("c1_pointmass_linear", n=6, m=2, hidden=None, linear=True,
+             lengths=[25] * 40, terminated=[False] * 40, algo="npg",
+             algo_kwargs=dict(normalized_step_size=0.1), gamma=0.95)
+    # C1b: the MLP(32,32) that tests/point_mass_test.py:12 actually builds
+    run_case("c1_pointmass_mlp32", n=6, m=2, hidden=(32, 32),
+             lengths=[25] * 40, terminated=[False] * 40, algo="npg",
+             algo_kwargs=dict(normalized_step_size=0.1), gamma=0.95)
+    # C2: Swimmer-v2 shape, full size (25 x 500)
+    run_case("c2_swimmer", n=8, m=2, hidden=(64, 64),
+             lengths=[500] * 25, terminated=[False] * 25, algo="npg",
+             algo_kwargs=dict(normalized_step_size=0.1))
+    # C2r: ragged lengths, length-1 path, mixed terminated flags
+    rs = np.random.RandomState(5)
+    lengths = [1, 2, 3, 64, 65, 127] + list(rs.randint(1, 300, size=24))
+    term = list(rs.randint(0, 2, size=len(lengths)).astype(bool))
+    run_case("c2_ragged", n=8, m=2, hidden=(64, 64), lengths=lengths, terminated=term,
+             algo="npg", algo_kwargs=dict(normalized_step_size=0.05), seed=321,
+             log_std=np.array([-0.7, 0.3]))
+    # C2n: non-GAE mode (gae_lambda=None is train_agent's default)
+    run_case("c2_nogae", n=8, m=2, hidden=(64, 64), lengths=[200] * 10,
+             terminated=[False] * 9 + [True], algo="npg",
+             algo_kwargs=dict(normalized_step_size=0.1), gae_lambda=None, seed=11)
+    # C2c: constant learn-rate NPG (npg_cg.py:130-132)
+    run_case("c2_constlr", n=8, m=2, hidden=(64, 64), lengths=[100] * 10,
+             terminated=[False] * 10, algo="npg",
+             algo_kwargs=dict(const_learn_rate=0.05), seed=12)
+    # C3: HalfCheetah shape, TRPO (reduced to 10 x 1000)
+    run_case("c3_halfcheetah_trpo", n=17, m=6, hidden=(128, 128),
+             lengths=[1000] * 10, terminated=[False] * 10, algo="trpo",
+             algo_kwargs=dict(kl_dist=0.01))
+    # C3b: TRPO with a step large enough that the line search backtracks
+    run_case("c3_trpo_backtrack", n=17, m=6, hidden=(128, 128),
+             lengths=[300] * 4, terminated=[False] * 4, algo="trpo",
+             algo_kwargs=dict(kl_dist=2.0), seed=77,
+             log_std=np.linspace(-1.0, 0.5, 6))
+    # C4: Humanoid shape (obs 376, act 17), reduced to 4 x 250
+    run_case("c4_humanoid", n=376, m=17, hidden=(64, 64),
+             lengths=[250] * 4, terminated=[False] * 4, algo="npg",
+             algo_kwargs=dict(normalized_step_size=0.01))
+    # C5: door shape, DAPG with BC-style in/out transformations and demos
+    rs = np.random.RandomState(9)
+    n, m = 39, 28
+    transforms = (rs.randn(n) * 0.5, rs.rand(n) + 0.5, rs.randn(m) * 0.1, rs.rand(m) + 0.5)
+    run_case("c5_door_dapg", n=n, m=m, hidden=(256, 256),
+             lengths=[200] * 10, terminated=[False] * 10, algo="dapg",
+             algo_kwargs=dict(), demo=[200] * 5, transforms=transforms,
+             log_std=np.linspace(-1.0, 0.0, m))
+
+
+if __name__ == "__main__":
+    main()

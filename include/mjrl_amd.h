@@ -1,0 +1,182 @@
+/*
+ * mjrl_amd.h — C ABI of the MI355X (gfx950) NPG / TRPO / DAPG update path.
+ *
+ * Drop-in boundary for bennevans/mjrl's per-iteration policy update.  The
+ * reference is pure Python (no FFI); each entry point below replaces one
+ * reference function, cited as path:line under the reference tree, and a
+ * maintainer would bind them from Python with ctypes.
+ *
+ * Conventions (all entry points):
+ *   - every pointer is DEVICE memory owned by the caller (hipMalloc / torch);
+ *   - every call is stream-ordered on the caller's `stream` (a hipStream_t,
+ *     passed as void*), never synchronises, never allocates, never throws;
+ *   - return 0 on success, a negative MJRL_E* code on bad arguments, or a
+ *     positive hipError_t if a launch failed;
+ *   - reductions are deterministic (fixed order, no float atomics).
+ *
+ * Device data layout:
+ *   rows t = 0..T-1 are the concatenated timesteps of the caller's paths
+ *   (np.concatenate order, mjrl/algos/npg_cg.py:87-89);
+ *   NP = round_up(n + 1, 16): xhat[T][NP] holds the normalised observation in
+ *   columns 0..n-1, 1.0 in column n (the bias column) and zeros after;
+ *   MP = round_up(m, 16) (m <= 64);  hidden sizes h0, h1 in {32, 64, 128, 256},
+ *   or h0 = h1 = 0 for the linear policy (mjrl/policies/gaussian_linear.py).
+ *   The flat parameter vector theta[d] is in the reference's trainable_params
+ *   order [W0(h0 x n), b0, W1(h1 x h0), b1, W2(m x h1), b2, log_std]
+ *   (mjrl/policies/gaussian_mlp.py:33-38, 61-64).
+ */
+#ifndef MJRL_AMD_H
+#define MJRL_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MJRL_OK 0
+#define MJRL_EINVAL (-1)      /* bad argument (null pointer, negative size) */
+#define MJRL_ESHAPE (-2)      /* policy shape not supported by the kernels */
+
+/* Policy shape and the padded sizes every buffer is laid out with. */
+typedef struct mjrl_shape {
+    int32_t n, m;             /* obs_dim, act_dim */
+    int32_t h0, h1;           /* hidden sizes; 0, 0 = linear policy */
+    int32_t np, mp;           /* padded: round_up(n+1,16), round_up(m,16) */
+    int32_t d;                /* flat parameter count */
+    int32_t packed;           /* floats in one packed parameter set */
+} mjrl_shape;
+
+/* Row-local buffers of one shard (all device, row-major, T rows). */
+typedef struct mjrl_rows {
+    int64_t T;                /* rows in this shard */
+    const float* xhat;        /* [T][np] */
+    const float* act;         /* [T][m]  actions, f32 */
+    const float* adv;         /* [T]     whitened advantages, f32 (surrogate) */
+    const float* adv_vpg;     /* [T]     advantages driving the VPG (DAPG: all_adv) */
+    float* a0;                /* [T][h0] cached tanh activations (layer 0) */
+    float* a1;                /* [T][h1] cached tanh activations (layer 1) */
+    float* mu0;               /* [T][m]  cached means at the old parameters */
+    float* ll0;               /* [T]     cached log-likelihoods at the old parameters */
+    float* gu0;               /* [T][h0] per-row upstream gradient at layer 0 */
+    float* gu1;               /* [T][h1] per-row upstream gradient at layer 1 */
+    float* gp;                /* [T][mp] per-row upstream gradient at the output */
+} mjrl_rows;
+
+/* Scratch the caller allocates once per (shape, T) — sizes from
+ * mjrl_scratch_floats(). */
+typedef struct mjrl_scratch {
+    float* wpart;             /* weight-gradient partial slabs */
+    double* rpart;            /* per-workgroup scalar partials */
+    int32_t slices;           /* T-slices of the weight-gradient reduction */
+} mjrl_scratch;
+
+/* Fills padded sizes / d / packed-set size for a policy shape.
+ * Returns MJRL_ESHAPE if the kernels were not built for it. */
+int mjrl_shape_init(mjrl_shape* s, int32_t n, int32_t m, int32_t h0, int32_t h1);
+
+/* Scratch sizes (in elements) for T rows: *wpart_floats, *rpart_doubles; also
+ * returns the T-slice count the kernels will use. */
+int mjrl_scratch_size(const mjrl_shape* s, int64_t T, int64_t* wpart_floats,
+                      int64_t* rpart_doubles, int32_t* slices);
+
+/* ---- batch assembly (npg_cg.py:87-89 concatenate + gaussian_mlp.py:103,177) ----
+ * obs f64 [T][n] -> xhat f32 [T][np] = (float(obs) - in_shift) / (in_scale + 1e-8),
+ * bias column 1.0, zero padding; act f64 [T][m] -> act32 f32 [T][m]. */
+int mjrl_pack_batch(const double* obs, const double* act, int64_t T, const mjrl_shape* s,
+                    const float* in_shift, const float* in_scale, float* xhat, float* act32,
+                    void* stream);
+
+/* ---- returns / GAE (process_samples.py:3-44) ----
+ * One lane per path, reverse recurrence in fp64, multiply-then-add (no FMA),
+ * bit-identical to discount_sum.  use_gae = 0 selects returns - baseline
+ * (process_samples.py:10-13).  Also path_ret[p] = sum(rewards of path p) in the
+ * order Python's builtin sum uses (npg_cg.py:97). */
+int mjrl_gae(const double* rew, const double* base, const int64_t* path_off,
+             const uint8_t* terminated, int64_t P, double gamma, double gae_lambda,
+             int32_t use_gae, double* ret, double* adv, double* path_ret, void* stream);
+
+/* ---- moments for whitening / stats (npg_cg.py:91, 97-102; dapg.py:70) ----
+ * out[0] = sum(x - c), out[1] = sum((x - c)^2), out[2] = N, out[3] = min(x),
+ * out[4] = max(x), out[5] = -min(x) over x[0..N-1] (out needs 6 doubles),
+ * c = center[0] / center[2] read from device
+ * (the out[] of an uncentred pass, i.e. its mean; center may be null: c = 0).
+ * Two launches (per-block partials into rpart[>= 4*256], fixed-order fold);
+ * the caller all-reduces out[0..2] between passes when sharded. */
+int mjrl_moments(const double* x, int64_t N, const double* center, double* rpart,
+                 double* out, void* stream);
+int mjrl_moments_f32(const float* x, int64_t N, const double* center, double* rpart,
+                     double* out, void* stream);
+
+/* w = (adv[t] - mean) / (std + eps), mean = m1[0]/m1[2], std = sqrt(m2[1]/m1[2]);
+ * adv32[t] = float(w) (eps = 1e-6: npg_cg.py:91 then the .float() of
+ * batch_reinforce.py:38) and/or w64[t] = w (eps = 1e-8: the `normalize` option of
+ * process_samples.py:14-19).  Either output may be null, not both. */
+int mjrl_whiten(const double* adv, int64_t T, const double* m1, const double* m2,
+                double eps, float* adv32, double* w64, void* stream);
+
+/* DAPG augmented advantages (dapg.py:65-70): adv_vpg[t] = float(1e-2 * w[t] /
+ * (std(w) + 1e-8)) for t < T (std from the moments mw1/mw2 of w64), and
+ * float(1e-2 * demo_coef) for the T_demo demo rows that follow. */
+int mjrl_dapg_adv(const double* w64, int64_t T, const double* mw1, const double* mw2,
+                  int64_t T_demo, double demo_coef, float* adv_vpg, void* stream);
+
+/* ---- parameter packing (gaussian_mlp.py:66-88 set_param_values) ----
+ * flat theta[d] -> packed[s->packed] (padded weights + transposes + log_std).
+ * clamp_log_std != 0 applies max(log_std, min_log_std) as set_param_values does. */
+int mjrl_pack_params(const mjrl_shape* s, const float* theta, float* packed,
+                     int32_t clamp_log_std, float min_log_std, void* stream);
+
+/* ---- policy passes; each writes UNSCALED sums over this shard's rows ----
+ * vpg:   gsum[d] = sum_t adv_vpg[t] * dLL_t/dtheta at old == new (LR == 1),
+ *        and caches a0/a1/mu0/ll0 (batch_reinforce.py:51-55, gaussian_mlp.py:100-128).
+ *        rows->T rows get the forward; only the first T_surr rows feed caches used
+ *        later (DAPG: RL rows first, demo rows after, dapg.py:68-69).
+ * fvp:   gsum[d] = sum_{t < T_fvp} J_t^T W J_t v (Gauss-Newton form of the
+ *        double-backprop HVP, npg_cg.py:55-74); the log_std block is left 0 and
+ *        added in closed form by mjrl_cg_step.
+ * eval:  sums[0] = sum_t exp(LL_new - LL_old) * adv[t], sums[1] = sum_t KL_t
+ *        (CPI_surrogate + kl_old_new at new params, batch_reinforce.py:37-49).
+ * `done` (device int, may be null): when *done != 0 the call is a no-op (lets a
+ * converged CG loop keep launching without host syncs, cg_solve.py:19-20). */
+int mjrl_policy_vpg(const mjrl_shape* s, const mjrl_rows* rows, const float* packed_theta,
+                    const float* out_shift, const float* out_scale,
+                    const mjrl_scratch* sc, float* gsum, void* stream);
+int mjrl_policy_fvp(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_fvp,
+                    const float* packed_theta, const float* packed_v,
+                    const float* out_scale, const mjrl_scratch* sc, const int32_t* done,
+                    float* gsum, void* stream);
+int mjrl_policy_eval(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_eval,
+                     const float* packed_theta_new, const float* packed_theta_old,
+                     const float* out_shift, const float* out_scale,
+                     const mjrl_scratch* sc, double* sums, void* stream);
+
+/* ---- conjugate gradient on device (cg_solve.py:3-22) ----
+ * State cg[8] (f32 scalars, device): [rdotr, v, mu, pz, done_flag(as int bits), iters, ...].
+ * init: x = 0, r = b, p = b, rdotr = b.b; packs p into packed_p.
+ * step: z = gsum * inv_T + c(sigma) * p_logstd + damping * p, then the
+ *       reference's update of x, r, p, rdotr and the residual_tol break. */
+int mjrl_cg_init(const mjrl_shape* s, const float* b, float* x, float* r, float* p,
+                 float* packed_p, float* cg, int32_t* done, void* stream);
+int mjrl_cg_step(const mjrl_shape* s, const float* gsum, double inv_T, float damping,
+                 const float* packed_theta, float* x, float* r, float* p, float* z,
+                 float* packed_p, float* cg, int32_t* done, float residual_tol,
+                 void* stream);
+
+/* g[d] = gsum * scale  (VPG normalisation: 1/T, DAPG: 1/T_rl, dapg.py:97-98) */
+int mjrl_scale_vec(const float* gsum, int32_t d, double scale, float* g, void* stream);
+
+/* ---- step (npg_cg.py:128-141, trpo.py:100-108, dapg.py:111-118) ----
+ * mode 0: alpha = sqrt(|delta / (g.x + 1e-20)|);  mode 1: alpha = alpha_in
+ * (const learn-rate or a TRPO backtrack trial); out[0] = alpha, out[1] = g.x,
+ * out[2] = delta (mode 1 with const_lr: alpha^2 * g.x).
+ * theta_new = clamp_logstd(theta + alpha * x); packs theta_new. */
+int mjrl_npg_step(const mjrl_shape* s, const float* g, const float* x, const float* theta,
+                  int32_t mode, float delta, float alpha_in, int32_t const_lr,
+                  float min_log_std, float* theta_new, float* packed_new, float* out,
+                  void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MJRL_AMD_H */

@@ -1,0 +1,117 @@
+"""ctypes binding of the gfx950 C ABI (include/mjrl_amd.h).
+
+The library is mjrl_amd/lib/libmjrl_amd.so, built in-tree by
+`python -m mjrl_amd.build` (or __graft_entry__.build()).  There is no CPU
+fallback: if the library or a GPU is missing, `lib()` raises.
+
+torch is imported first on purpose: torch-ROCm ships the HIP runtime
+(libamdhip64.so.7) and our library resolves against that already-loaded copy, so
+torch's hipStream_t handles are valid arguments.
+"""
+import ctypes as C
+import os
+
+import torch  # noqa: F401  (loads the HIP runtime the library binds to)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libmjrl_amd.so")
+
+MJRL_OK = 0
+MJRL_EINVAL = -1
+MJRL_ESHAPE = -2
+
+
+class Shape(C.Structure):
+    _fields_ = [("n", C.c_int32), ("m", C.c_int32), ("h0", C.c_int32), ("h1", C.c_int32),
+                ("np", C.c_int32), ("mp", C.c_int32), ("d", C.c_int32), ("packed", C.c_int32)]
+
+
+class Rows(C.Structure):
+    _fields_ = [("T", C.c_int64)] + [(k, C.c_void_p) for k in (
+        "xhat", "act", "adv", "adv_vpg", "a0", "a1", "mu0", "ll0", "gu0", "gu1", "gp")]
+
+
+class Scratch(C.Structure):
+    _fields_ = [("wpart", C.c_void_p), ("rpart", C.c_void_p), ("slices", C.c_int32)]
+
+
+P = C.c_void_p
+I32 = C.c_int32
+I64 = C.c_int64
+F32 = C.c_float
+F64 = C.c_double
+SP = C.POINTER(Shape)
+
+# name -> argtypes, in header order; every function returns int
+SIGNATURES = {
+    "mjrl_shape_init": [SP, I32, I32, I32, I32],
+    "mjrl_scratch_size": [SP, I64, C.POINTER(I64), C.POINTER(I64), C.POINTER(I32)],
+    "mjrl_pack_batch": [P, P, I64, SP, P, P, P, P, P],
+    "mjrl_gae": [P, P, P, P, I64, F64, F64, I32, P, P, P, P],
+    "mjrl_moments": [P, I64, P, P, P, P],
+    "mjrl_moments_f32": [P, I64, P, P, P, P],
+    "mjrl_whiten": [P, I64, P, P, F64, P, P, P],
+    "mjrl_dapg_adv": [P, I64, P, P, I64, F64, P, P],
+    "mjrl_pack_params": [SP, P, P, I32, F32, P],
+    "mjrl_policy_vpg": [SP, C.POINTER(Rows), P, P, P, C.POINTER(Scratch), P, P],
+    "mjrl_policy_fvp": [SP, C.POINTER(Rows), I64, P, P, P, C.POINTER(Scratch), P, P, P],
+    "mjrl_policy_eval": [SP, C.POINTER(Rows), I64, P, P, P, P, C.POINTER(Scratch), P, P],
+    "mjrl_cg_init": [SP, P, P, P, P, P, P, P, P],
+    "mjrl_cg_step": [SP, P, F64, F32, P, P, P, P, P, P, P, P, F32, P],
+    "mjrl_scale_vec": [P, I32, F64, P, P],
+    "mjrl_npg_step": [SP, P, P, P, I32, F32, F32, I32, F32, P, P, P, P],
+}
+
+_LIB = None
+
+
+class MjrlError(RuntimeError):
+    pass
+
+
+def load(path=LIB_PATH):
+    """Loads the shared library and declares every entry point (no GPU needed)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(path):
+        raise MjrlError("mjrl_amd HIP library not built: %s (run `python -m mjrl_amd.build`)" % path)
+    lib = C.CDLL(path)
+    for name, args in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = C.c_int
+    _LIB = lib
+    return lib
+
+
+def lib():
+    """The library, for compute calls: requires a visible GPU."""
+    if not torch.cuda.is_available():
+        raise MjrlError("mjrl_amd needs an AMD GPU (torch.cuda.is_available() is False); "
+                        "there is no CPU fallback")
+    return load()
+
+
+def check(rc, what):
+    if rc != MJRL_OK:
+        msg = {MJRL_EINVAL: "invalid argument", MJRL_ESHAPE: "unsupported policy shape"}.get(
+            rc, "HIP error %d" % rc)
+        raise MjrlError("%s failed: %s" % (what, msg))
+
+
+def make_shape(n, m, h0, h1, loader=load):
+    s = Shape()
+    rc = loader().mjrl_shape_init(C.byref(s), n, m, h0, h1)
+    check(rc, "mjrl_shape_init(n=%d, m=%d, hidden=(%d, %d))" % (n, m, h0, h1))
+    return s
+
+
+def ptr(t):
+    """Device pointer of a torch tensor (or None -> NULL)."""
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def stream_ptr(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return C.c_void_p(s.cuda_stream)

@@ -1,0 +1,64 @@
+"""Builds the gfx950 shared library mjrl_amd/lib/libmjrl_amd.so (the C-ABI of
+include/mjrl_amd.h) with hipcc.  One object per .hip source, compiled in
+parallel, then linked.  Rebuilds only when a source or header is newer.
+
+    python -m mjrl_amd.build [--force] [-j N]
+"""
+import argparse
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+OUTDIR = os.path.join(HERE, "lib")
+LIB = os.path.join(OUTDIR, "libmjrl_amd.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+FLAGS = [
+    "-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH,
+    "-ffp-contract=off",          # keep the reference's multiply-then-add order
+    "-Wall", "-Wno-unused-function", "-Wno-unused-variable",
+]
+SOURCES = ["batch.hip", "policy.hip", "cg.hip"]
+
+
+def _deps():
+    hdrs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    hdrs.append(os.path.join(ROOT, "include", "mjrl_amd.h"))
+    return max(os.path.getmtime(h) for h in hdrs)
+
+
+def _compile(src, force):
+    s = os.path.join(CSRC, src)
+    o = os.path.join(OUTDIR, src.replace(".hip", ".o"))
+    if not force and os.path.exists(o) and os.path.getmtime(o) >= max(os.path.getmtime(s), _deps()):
+        return o
+    cmd = [HIPCC] + FLAGS + ["-c", s, "-o", o]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("hipcc failed for %s:\n%s\n%s" % (src, " ".join(cmd), r.stderr[-8000:]))
+    return o
+
+
+def build(force=False, jobs=None):
+    os.makedirs(OUTDIR, exist_ok=True)
+    jobs = jobs or min(len(SOURCES), os.cpu_count() or 1, 16)
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(lambda s: _compile(s, force), SOURCES))
+    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
+        cmd = [HIPCC, "-shared", "--offload-arch=" + ARCH, "-fPIC"] + objs + ["-o", LIB]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("link failed:\n%s\n%s" % (" ".join(cmd), r.stderr[-8000:]))
+    return LIB
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", type=int, default=None)
+    args = ap.parse_args()
+    print(build(args.force, args.j))

@@ -1,0 +1,76 @@
+"""Collectives used by the sharded update (one process per GPU).
+
+The update is data-parallel over paths: every rank owns a contiguous range of
+paths (balanced by timestep count, `partition_paths`) and all full-batch
+quantities are sums over timesteps, so the only exchange is an all-reduce SUM of
+  - the whitening moments (2 x 3 doubles) and the path-return moments,
+  - the flat VPG sum (d floats) and every Fisher-vector-product sum (d floats),
+  - the post-step surrogate / KL sums (2 doubles per line-search trial),
+plus one MAX of the path-return extrema.  Backend "nccl" is RCCL over xGMI on
+ROCm; the same code runs on "gloo" for the CPU tests.
+"""
+import numpy as np
+import torch
+
+
+class LocalComm:
+    """world_size 1: every collective is the identity."""
+    rank = 0
+    world_size = 1
+
+    def allreduce_sum(self, t):
+        return t
+
+    def allreduce_max(self, t):
+        return t
+
+
+class DistComm:
+    """torch.distributed process group (RCCL on GPU, gloo on CPU)."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world_size = dist.get_world_size(group)
+
+    def allreduce_sum(self, t):
+        if self.world_size > 1:
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group)
+        return t
+
+    def allreduce_max(self, t):
+        if self.world_size > 1:
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
+        return t
+
+
+def default_comm():
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        return DistComm()
+    return LocalComm()
+
+
+def partition_paths(lengths, world_size):
+    """Contiguous path ranges per rank, balanced by timestep count.
+
+    Returns a list of (p_begin, p_end).  Deterministic; every rank computes the
+    same split from the same lengths.  A rank may get an empty range when there
+    are fewer paths than ranks."""
+    lengths = np.asarray(lengths, dtype=np.int64)
+    P = len(lengths)
+    if world_size <= 1:
+        return [(0, P)]
+    cum = np.concatenate([[0], np.cumsum(lengths)])
+    total = cum[-1]
+    bounds = [0]
+    for r in range(1, world_size):
+        target = total * r / world_size
+        # first path boundary at or after the target, never before the previous bound
+        b = int(np.searchsorted(cum, target, side="left"))
+        b = min(max(b, bounds[-1]), P)
+        bounds.append(b)
+    bounds.append(P)
+    return [(bounds[i], bounds[i + 1]) for i in range(world_size)]

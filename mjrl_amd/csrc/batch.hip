@@ -1,0 +1,263 @@
+// batch.hip — batch assembly, returns / GAE scan, moments and whitening.
+//
+// HBM-bound fp64 / byte work: coalesced grid-stride loops, no MFMA.
+// Reference: mjrl/utils/process_samples.py:3-44, mjrl/algos/npg_cg.py:86-105,
+// mjrl/algos/dapg.py:62-74, mjrl/policies/gaussian_mlp.py:103,177.
+#include "common.h"
+
+using namespace mjrl;
+
+namespace {
+
+constexpr int MOM_BLOCKS = 256;
+constexpr int MOM_THREADS = 256;
+
+// obs f64 [T][n] -> xhat f32 [T][np]; act f64 [T][m] -> f32.  One thread per 4
+// output columns so the xhat stores are 16 B per lane.
+__global__ void __launch_bounds__(256) k_pack_batch(const double* __restrict__ obs, const double* __restrict__ act,
+                                                    int64_t T, int n, int m, int np,
+                                                    const float* __restrict__ in_shift,
+                                                    const float* __restrict__ in_scale, float* __restrict__ xhat,
+                                                    float* __restrict__ act32) {
+    const int64_t nq = (int64_t)T * (np / 4);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nq; i += stride) {
+        const int64_t row = i / (np / 4);
+        const int c0 = (int)(i - row * (np / 4)) * 4;
+        float v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int c = c0 + u;
+            float x;
+            if (c < n) {
+                x = (float)obs[row * n + c];                  // torch .float(): round to nearest
+                if (in_shift) x = (x - in_shift[c]) / (in_scale[c] + 1e-8f);   // MuNet.forward:177
+            } else {
+                x = (c == n) ? 1.0f : 0.0f;                   // bias column, zero pad
+            }
+            v[u] = x;
+        }
+        *reinterpret_cast<float4*>(xhat + row * np + c0) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+    const int64_t na = (int64_t)T * m;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < na; i += stride) act32[i] = (float)act[i];
+}
+
+// One lane per path; reverse recurrences in fp64 with separate multiply and add
+// (__dmul_rn / __dadd_rn cannot be contracted) — bit-identical to discount_sum.
+__global__ void __launch_bounds__(64) k_gae(const double* __restrict__ rew, const double* __restrict__ base,
+                                            const int64_t* __restrict__ off, const uint8_t* __restrict__ term,
+                                            int64_t P, double gamma, double gl, int use_gae,
+                                            double* __restrict__ ret, double* __restrict__ adv,
+                                            double* __restrict__ path_ret) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P) return;
+    const int64_t b = off[p], e = off[p + 1];
+    // sum(p["rewards"]) — Python's builtin sum, front to back (npg_cg.py:97)
+    double s = 0.0;
+    for (int64_t t = b; t < e; ++t) s = __dadd_rn(s, rew[t]);
+    path_ret[p] = s;
+    if (e <= b) return;
+    // returns: discount_sum(rewards, gamma) (process_samples.py:3-5, 37-44)
+    double acc = 0.0;
+    for (int64_t t = e - 1; t >= b; --t) {
+        acc = __dadd_rn(rew[t], __dmul_rn(gamma, acc));
+        ret[t] = acc;
+    }
+    if (!use_gae) {   // process_samples.py:10-13
+        for (int64_t t = b; t < e; ++t) adv[t] = __dsub_rn(ret[t], base[t]);
+        return;
+    }
+    // GAE (process_samples.py:21-29): b1 = append(b, 0 if terminated else b[-1]),
+    // td = r + gamma*b1[1:] - b1[:-1], adv = discount_sum(td, gamma*lambda)
+    double bnext = term[p] ? 0.0 : base[e - 1];
+    acc = 0.0;
+    for (int64_t t = e - 1; t >= b; --t) {
+        const double bt = base[t];
+        const double td = __dsub_rn(__dadd_rn(rew[t], __dmul_rn(gamma, bnext)), bt);
+        acc = __dadd_rn(td, __dmul_rn(gl, acc));
+        adv[t] = acc;
+        bnext = bt;
+    }
+}
+
+// Moments pass 1: per-block partials of sum(x-c), sum((x-c)^2), min, max.
+template <typename T>
+__global__ void __launch_bounds__(MOM_THREADS) k_moments_part(const T* __restrict__ x, int64_t N,
+                                                              const double* __restrict__ cstat,
+                                                              double* __restrict__ part) {
+    __shared__ double red[MOM_THREADS / 64];
+    const double c = cstat ? cstat[0] / cstat[2] : 0.0;
+    double s1 = 0.0, s2 = 0.0, mn = __builtin_inf(), mx = -__builtin_inf();
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += stride) {
+        const double v = (double)x[i];
+        const double dv = v - c;
+        s1 += dv;
+        s2 += dv * dv;
+        mn = fmin(mn, v);
+        mx = fmax(mx, v);
+    }
+    const double t1 = block_sum<MOM_THREADS>(s1, red);
+    const double t2 = block_sum<MOM_THREADS>(s2, red);
+    // min / max through the same LDS words (order irrelevant for min/max)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mn = fmin(mn, __shfl_xor(mn, o, 64));
+        mx = fmax(mx, __shfl_xor(mx, o, 64));
+    }
+    __shared__ double mm[2][MOM_THREADS / 64];
+    if ((threadIdx.x & 63) == 0) {
+        mm[0][threadIdx.x >> 6] = mn;
+        mm[1][threadIdx.x >> 6] = mx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < MOM_THREADS / 64; ++i) {
+            mn = fmin(mn, mm[0][i]);
+            mx = fmax(mx, mm[1][i]);
+        }
+        part[blockIdx.x * 4 + 0] = t1;
+        part[blockIdx.x * 4 + 1] = t2;
+        part[blockIdx.x * 4 + 2] = fmin(mm[0][0], mn);
+        part[blockIdx.x * 4 + 3] = fmax(mm[1][0], mx);
+    }
+}
+
+// Moments pass 2: one workgroup folds the block partials in block order.
+__global__ void __launch_bounds__(64) k_moments_final(const double* __restrict__ part, int nb, int64_t N,
+                                                      double* __restrict__ out) {
+    if (threadIdx.x != 0) return;
+    double s1 = 0.0, s2 = 0.0, mn = __builtin_inf(), mx = -__builtin_inf();
+    for (int b = 0; b < nb; ++b) {
+        s1 += part[b * 4 + 0];
+        s2 += part[b * 4 + 1];
+        mn = fmin(mn, part[b * 4 + 2]);
+        mx = fmax(mx, part[b * 4 + 3]);
+    }
+    out[0] = s1;
+    out[1] = s2;
+    out[2] = (double)N;
+    out[3] = mn;
+    out[4] = mx;
+    out[5] = -mn;   // so one MAX all-reduce over out[4..5] gives the global extrema
+}
+
+// adv32 = float((adv - mean) / (std + 1e-6)) (npg_cg.py:91; .float() at batch_reinforce.py:38)
+__global__ void __launch_bounds__(256) k_whiten(const double* __restrict__ adv, int64_t T,
+                                                const double* __restrict__ m1, const double* __restrict__ m2,
+                                                double eps, float* __restrict__ adv32, double* __restrict__ w64) {
+    const double mean = m1[0] / m1[2];
+    const double sd = sqrt(m2[1] / m1[2]);
+    const double den = sd + eps;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < T; i += stride) {
+        const double w = (adv[i] - mean) / den;
+        if (adv32) adv32[i] = (float)w;
+        if (w64) w64[i] = w;
+    }
+}
+
+// DAPG augmented advantages (dapg.py:65-70):
+// all_adv = 1e-2 * concat(w / (std(w) + 1e-8), demo_coef * ones)
+__global__ void __launch_bounds__(256) k_dapg_adv(const double* __restrict__ w64, int64_t T,
+                                                  const double* __restrict__ mw1, const double* __restrict__ mw2,
+                                                  int64_t T_demo, double demo_coef, float* __restrict__ adv_vpg) {
+    const double sd = sqrt(mw2[1] / mw1[2]);
+    const double den = sd + 1e-8;
+    const float dv = (float)(1e-2 * demo_coef);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < T + T_demo; i += stride)
+        adv_vpg[i] = i < T ? (float)(1e-2 * (w64[i] / den)) : dv;
+}
+
+__global__ void __launch_bounds__(256) k_scale_vec(const float* __restrict__ gsum, int d, double scale,
+                                                   float* __restrict__ g) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < d) g[i] = (float)((double)gsum[i] * scale);
+}
+
+inline int grid_for(int64_t work, int per_block, int cap) {
+    int64_t g = (work + per_block - 1) / per_block;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (int)g;
+}
+
+inline int err(hipError_t e) { return e == hipSuccess ? MJRL_OK : (int)e; }
+
+}  // namespace
+
+extern "C" {
+
+int mjrl_pack_batch(const double* obs, const double* act, int64_t T, const mjrl_shape* s, const float* in_shift,
+                    const float* in_scale, float* xhat, float* act32, void* stream) {
+    if (!s || T < 0 || (T > 0 && (!obs || !act || !xhat || !act32))) return MJRL_EINVAL;
+    if ((in_shift == nullptr) != (in_scale == nullptr)) return MJRL_EINVAL;
+    if (T == 0) return MJRL_OK;
+    const int g = grid_for(T * (s->np / 4), 256, 2048);
+    hipLaunchKernelGGL(k_pack_batch, dim3(g), dim3(256), 0, (hipStream_t)stream, obs, act, T, s->n, s->m, s->np,
+                       in_shift, in_scale, xhat, act32);
+    return err(hipGetLastError());
+}
+
+int mjrl_gae(const double* rew, const double* base, const int64_t* path_off, const uint8_t* terminated, int64_t P,
+             double gamma, double gae_lambda, int32_t use_gae, double* ret, double* adv, double* path_ret,
+             void* stream) {
+    if (P < 0 || (P > 0 && (!rew || !base || !path_off || !terminated || !ret || !adv || !path_ret)))
+        return MJRL_EINVAL;
+    if (P == 0) return MJRL_OK;
+    const double gl = gamma * gae_lambda;   // python: gamma*gae_lambda (process_samples.py:29)
+    hipLaunchKernelGGL(k_gae, dim3((unsigned)((P + 63) / 64)), dim3(64), 0, (hipStream_t)stream, rew, base, path_off,
+                       terminated, P, gamma, gl, use_gae, ret, adv, path_ret);
+    return err(hipGetLastError());
+}
+
+static int moments_impl(bool f32, const void* x, int64_t N, const double* center, double* rpart, double* out,
+                        void* stream) {
+    if (N < 0 || !rpart || !out || (N > 0 && !x)) return MJRL_EINVAL;
+    const int nb = grid_for(N, MOM_THREADS * 4, MOM_BLOCKS);
+    if (f32)
+        hipLaunchKernelGGL(k_moments_part<float>, dim3(nb), dim3(MOM_THREADS), 0, (hipStream_t)stream,
+                           (const float*)x, N, center, rpart);
+    else
+        hipLaunchKernelGGL(k_moments_part<double>, dim3(nb), dim3(MOM_THREADS), 0, (hipStream_t)stream,
+                           (const double*)x, N, center, rpart);
+    hipLaunchKernelGGL(k_moments_final, dim3(1), dim3(64), 0, (hipStream_t)stream, rpart, nb, N, out);
+    return err(hipGetLastError());
+}
+
+int mjrl_moments(const double* x, int64_t N, const double* center, double* rpart, double* out, void* stream) {
+    return moments_impl(false, x, N, center, rpart, out, stream);
+}
+
+int mjrl_moments_f32(const float* x, int64_t N, const double* center, double* rpart, double* out, void* stream) {
+    return moments_impl(true, x, N, center, rpart, out, stream);
+}
+
+int mjrl_whiten(const double* adv, int64_t T, const double* m1, const double* m2, double eps, float* adv32,
+                double* w64, void* stream) {
+    if (T < 0 || !m1 || !m2 || (T > 0 && (!adv || (!adv32 && !w64)))) return MJRL_EINVAL;
+    if (T == 0) return MJRL_OK;
+    hipLaunchKernelGGL(k_whiten, dim3(grid_for(T, 256, 2048)), dim3(256), 0, (hipStream_t)stream, adv, T, m1, m2,
+                       eps, adv32, w64);
+    return err(hipGetLastError());
+}
+
+int mjrl_dapg_adv(const double* w64, int64_t T, const double* mw1, const double* mw2, int64_t T_demo,
+                  double demo_coef, float* adv_vpg, void* stream) {
+    if (T < 0 || T_demo < 0 || !mw1 || !mw2 || !adv_vpg || (T > 0 && !w64)) return MJRL_EINVAL;
+    if (T + T_demo == 0) return MJRL_OK;
+    hipLaunchKernelGGL(k_dapg_adv, dim3(grid_for(T + T_demo, 256, 2048)), dim3(256), 0, (hipStream_t)stream, w64,
+                       T, mw1, mw2, T_demo, demo_coef, adv_vpg);
+    return err(hipGetLastError());
+}
+
+int mjrl_scale_vec(const float* gsum, int32_t d, double scale, float* g, void* stream) {
+    if (d < 0 || (d > 0 && (!gsum || !g))) return MJRL_EINVAL;
+    if (d == 0) return MJRL_OK;
+    hipLaunchKernelGGL(k_scale_vec, dim3((d + 255) / 256), dim3(256), 0, (hipStream_t)stream, gsum, d, scale, g);
+    return err(hipGetLastError());
+}
+
+}  // extern "C"

@@ -1,0 +1,231 @@
+// cg.hip — parameter packing, conjugate gradient and the natural-gradient step,
+// all on device so the CG loop never synchronises with the host.
+//
+// Reference: mjrl/utils/cg_solve.py:3-22, mjrl/algos/npg_cg.py:128-144,
+// mjrl/algos/trpo.py:100-108, mjrl/policies/gaussian_mlp.py:66-88.
+// The d-length vector work is tiny (d <= ~1e5): one 1024-thread workgroup,
+// fp64 accumulation of the dot products, fp32 scalar arithmetic in the
+// reference's order (numpy fp32 arrays).
+#include <math.h>
+
+#include "common.h"
+
+using namespace mjrl;
+
+namespace {
+
+constexpr int CG_THREADS = 1024;
+
+struct PackMap {
+    int n, m, h0, h1, np, mp;
+    Packed pk;
+    __host__ __device__ PackMap(const mjrl_shape& s)
+        : n(s.n), m(s.m), h0(s.h0), h1(s.h1), np(s.np), mp(s.mp), pk(s.h0, s.h1, s.np, s.mp) {}
+
+    // Packed positions of flat parameter f (second = transpose copy or -1);
+    // returns the log_std index j when f is a log-std entry, else -1.
+    __device__ int map(int f, int& p1, int& p2) const {
+        p2 = -1;
+        int g = f;
+        if (h0 == 0) {
+            if (g < m * n) { p1 = pk.W0 + (g / n) * np + g % n; return -1; }
+            if ((g -= m * n) < m) { p1 = pk.W0 + g * np + n; return -1; }
+            g -= m;
+            p1 = pk.ls + g;
+            return g;
+        }
+        if (g < h0 * n) { p1 = pk.W0 + (g / n) * np + g % n; return -1; }
+        if ((g -= h0 * n) < h0) { p1 = pk.W0 + g * np + n; return -1; }
+        if ((g -= h0) < h1 * h0) {
+            const int j = g / h0, k = g % h0;
+            p1 = pk.W1 + g;
+            p2 = pk.W1T + k * h1 + j;
+            return -1;
+        }
+        if ((g -= h1 * h0) < h1) { p1 = pk.b1 + g; return -1; }
+        if ((g -= h1) < m * h1) {
+            const int j = g / h1, k = g % h1;
+            p1 = pk.W2 + j * h1 + k;
+            p2 = pk.W2T + k * mp + j;
+            return -1;
+        }
+        if ((g -= m * h1) < m) { p1 = pk.b2 + g; return -1; }
+        g -= m;
+        p1 = pk.ls + g;
+        return g;
+    }
+};
+
+__device__ __forceinline__ void pack_one(const PackMap& pm, int f, float v, float* packed, bool clamp, float min_ls) {
+    int p1, p2;
+    const int j = pm.map(f, p1, p2);
+    if (j >= 0 && clamp) v = v < min_ls ? min_ls : v;   // torch.clamp(log_std, min) (gaussian_mlp.py:74-78)
+    packed[p1] = v;
+    if (p2 >= 0) packed[p2] = v;
+}
+
+__global__ void __launch_bounds__(256) k_pack(mjrl_shape s, const float* __restrict__ theta, float* __restrict__ packed,
+                                              int clamp, float min_ls) {
+    const PackMap pm(s);
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f < s.d) pack_one(pm, f, theta[f], packed, clamp != 0, min_ls);
+}
+
+__device__ __forceinline__ double block_sum1024(double v, double* red) { return block_sum<CG_THREADS>(v, red); }
+
+// cg_solve.py:4-7: x = 0, r = b, p = r, rdotr = r.r
+__global__ void __launch_bounds__(CG_THREADS) k_cg_init(mjrl_shape s, const float* __restrict__ b, float* __restrict__ x,
+                                                        float* __restrict__ r, float* __restrict__ p,
+                                                        float* __restrict__ packed_p, float* __restrict__ cg,
+                                                        int32_t* __restrict__ done) {
+    __shared__ double red[CG_THREADS / 64];
+    const PackMap pm(s);
+    double acc = 0.0;
+    for (int f = threadIdx.x; f < s.d; f += CG_THREADS) {
+        const float v = b[f];
+        x[f] = 0.f;
+        r[f] = v;
+        p[f] = v;
+        pack_one(pm, f, v, packed_p, false, 0.f);
+        acc += (double)v * (double)v;
+    }
+    const double rr = block_sum1024(acc, red);
+    if (threadIdx.x == 0) {
+        cg[0] = (float)rr;   // rdotr
+        cg[1] = 0.f;         // iterations run
+        *done = 0;
+    }
+}
+
+// One CG iteration (cg_solve.py:10-20) given the raw FVP sums for direction p:
+// z = F p + damping p with F p = gsum / T on the mean block and c(sigma) p on the
+// log-std block (closed form of the double-backprop HVP).
+__global__ void __launch_bounds__(CG_THREADS) k_cg_step(mjrl_shape s, const float* __restrict__ gsum, double inv_T,
+                                                        float damping, const float* __restrict__ packed_theta,
+                                                        float* __restrict__ x, float* __restrict__ r,
+                                                        float* __restrict__ p, float* __restrict__ z,
+                                                        float* __restrict__ packed_p, float* __restrict__ cg,
+                                                        int32_t* __restrict__ done, float tol) {
+    __shared__ double red[CG_THREADS / 64];
+    if (*done) return;
+    const PackMap pm(s);
+    const int ls0 = s.d - s.m;
+    double acc = 0.0;
+    for (int f = threadIdx.x; f < s.d; f += CG_THREADS) {
+        const float pf = p[f];
+        float hv;
+        if (f >= ls0) {
+            const float sg = expf(packed_theta[pm.pk.ls + (f - ls0)]);
+            const double u = (double)sg * (double)sg;
+            const double c = 4.0 * u * (2.0 * u - 1e-8) / ((2.0 * u + 1e-8) * (2.0 * u + 1e-8));
+            hv = (float)(c * (double)pf);
+        } else {
+            hv = (float)((double)gsum[f] * inv_T);
+        }
+        const float zf = __fadd_rn(hv, __fmul_rn(damping, pf));   // hvp_flat + regu_coef*vector
+        z[f] = zf;
+        acc += (double)pf * (double)zf;
+    }
+    const float pz = (float)block_sum1024(acc, red);
+    const float rdotr = cg[0];
+    const float v = rdotr / pz;
+    acc = 0.0;
+    for (int f = threadIdx.x; f < s.d; f += CG_THREADS) {
+        x[f] = __fadd_rn(x[f], __fmul_rn(v, p[f]));
+        const float rf = __fsub_rn(r[f], __fmul_rn(v, z[f]));
+        r[f] = rf;
+        acc += (double)rf * (double)rf;
+    }
+    const float rr = (float)block_sum1024(acc, red);
+    const float mu = rr / rdotr;
+    for (int f = threadIdx.x; f < s.d; f += CG_THREADS) {
+        const float pf = __fadd_rn(r[f], __fmul_rn(mu, p[f]));
+        p[f] = pf;
+        pack_one(pm, f, pf, packed_p, false, 0.f);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        cg[0] = rr;
+        cg[1] += 1.f;
+        cg[2] = v;
+        cg[3] = mu;
+        cg[4] = pz;
+        if (rr < tol) *done = 1;   // cg_solve.py:19-20
+    }
+}
+
+// Step size and parameter update (npg_cg.py:128-141).
+__global__ void __launch_bounds__(CG_THREADS) k_npg_step(mjrl_shape s, const float* __restrict__ g,
+                                                         const float* __restrict__ x,
+                                                         const float* __restrict__ theta, int mode, float delta,
+                                                         float alpha_in, int const_lr, float min_ls,
+                                                         float* __restrict__ theta_new, float* __restrict__ packed_new,
+                                                         float* __restrict__ out) {
+    __shared__ double red[CG_THREADS / 64];
+    const PackMap pm(s);
+    double acc = 0.0;
+    for (int f = threadIdx.x; f < s.d; f += CG_THREADS) acc += (double)g[f] * (double)x[f];
+    const float gx = (float)block_sum1024(acc, red);
+    float alpha, dl = delta;
+    if (mode == 0) {
+        alpha = sqrtf(fabsf(delta / __fadd_rn(gx, 1e-20f)));
+    } else {
+        alpha = alpha_in;
+        if (const_lr) dl = __fmul_rn(alpha * alpha, gx);
+    }
+    for (int f = threadIdx.x; f < s.d; f += CG_THREADS) {
+        float v = __fadd_rn(theta[f], __fmul_rn(alpha, x[f]));
+        int p1, p2;
+        if (pm.map(f, p1, p2) >= 0) v = v < min_ls ? min_ls : v;   // set_param_values clamp
+        theta_new[f] = v;
+        packed_new[p1] = v;
+        if (p2 >= 0) packed_new[p2] = v;
+    }
+    if (threadIdx.x == 0) {
+        out[0] = alpha;
+        out[1] = gx;
+        out[2] = dl;
+    }
+}
+
+inline int err(hipError_t e) { return e == hipSuccess ? MJRL_OK : (int)e; }
+
+}  // namespace
+
+extern "C" {
+
+int mjrl_pack_params(const mjrl_shape* s, const float* theta, float* packed, int32_t clamp_log_std,
+                     float min_log_std, void* stream) {
+    if (!s || !theta || !packed) return MJRL_EINVAL;
+    hipLaunchKernelGGL(k_pack, dim3((s->d + 255) / 256), dim3(256), 0, (hipStream_t)stream, *s, theta, packed,
+                       clamp_log_std, min_log_std);
+    return err(hipGetLastError());
+}
+
+int mjrl_cg_init(const mjrl_shape* s, const float* b, float* x, float* r, float* p, float* packed_p, float* cg,
+                 int32_t* done, void* stream) {
+    if (!s || !b || !x || !r || !p || !packed_p || !cg || !done) return MJRL_EINVAL;
+    hipLaunchKernelGGL(k_cg_init, dim3(1), dim3(CG_THREADS), 0, (hipStream_t)stream, *s, b, x, r, p, packed_p, cg,
+                       done);
+    return err(hipGetLastError());
+}
+
+int mjrl_cg_step(const mjrl_shape* s, const float* gsum, double inv_T, float damping, const float* packed_theta,
+                 float* x, float* r, float* p, float* z, float* packed_p, float* cg, int32_t* done,
+                 float residual_tol, void* stream) {
+    if (!s || !gsum || !packed_theta || !x || !r || !p || !z || !packed_p || !cg || !done) return MJRL_EINVAL;
+    hipLaunchKernelGGL(k_cg_step, dim3(1), dim3(CG_THREADS), 0, (hipStream_t)stream, *s, gsum, inv_T, damping,
+                       packed_theta, x, r, p, z, packed_p, cg, done, residual_tol);
+    return err(hipGetLastError());
+}
+
+int mjrl_npg_step(const mjrl_shape* s, const float* g, const float* x, const float* theta, int32_t mode, float delta,
+                  float alpha_in, int32_t const_lr, float min_log_std, float* theta_new, float* packed_new,
+                  float* out, void* stream) {
+    if (!s || !g || !x || !theta || !theta_new || !packed_new || !out) return MJRL_EINVAL;
+    hipLaunchKernelGGL(k_npg_step, dim3(1), dim3(CG_THREADS), 0, (hipStream_t)stream, *s, g, x, theta, mode, delta,
+                       alpha_in, const_lr, min_log_std, theta_new, packed_new, out);
+    return err(hipGetLastError());
+}
+
+}  // extern "C"

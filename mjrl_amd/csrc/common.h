@@ -1,0 +1,132 @@
+// common.h — shared device building blocks for the gfx950 update-path kernels.
+//
+// Everything here is written for CDNA4 directly: 64-lane waves, the exact-f32
+// MFMA `v_mfma_f32_16x16x4_f32`, LDS-staged operands.  No CUDA shims.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mjrl_amd.h"
+
+namespace mjrl {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+constexpr int WAVE = 64;
+constexpr int NTHREADS = 256;   // 4 waves per workgroup for the row / wgrad kernels
+
+__device__ __forceinline__ floatx4 zero4() { return floatx4{0.f, 0.f, 0.f, 0.f}; }
+
+// D = A(16x4) * B(4x16) + C, exact f32 (a k-ordered fma chain).
+// Lane l supplies A[l&15][l>>4] and B[l>>4][l&15]; D[(l>>4)*4+r][l&15] = c[r].
+__device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// Four MFMAs over one 16-wide k group.  Lane group q = lane>>4 owns
+// k = 16g + 4q + s for step s, so both operands come in as one float4 each
+// (the same permutation on A and B keeps the product exact).
+__device__ __forceinline__ floatx4 mfma_k16(const float4& a, const float4& b, floatx4 c) {
+    c = mfma4(a.x, b.x, c);
+    c = mfma4(a.y, b.y, c);
+    c = mfma4(a.z, b.z, c);
+    c = mfma4(a.w, b.w, c);
+    return c;
+}
+
+// ---------------------------------------------------------------------------
+// Wave decomposition of an output tile [BT x N] (BT = 16*RB rows, N = 16*CB cols)
+// over the 4 waves of a workgroup: each wave owns NRW row blocks x NCW col blocks
+// and loads one B (weight) fragment per col block per k-step, reused across its
+// row blocks.
+// ---------------------------------------------------------------------------
+template <int RB, int CB>
+struct Split {
+    static constexpr int NCW = CB >= 4 ? CB / 4 : 1;
+    static constexpr int NRW = CB >= 4 ? RB : (CB == 2 ? (RB / 2 > 0 ? RB / 2 : 1) : (RB / 4 > 0 ? RB / 4 : 1));
+    static constexpr int CBS = CB >= 4 ? 4 : 1;        // col block stride
+    static constexpr int RBS = CB >= 4 ? 1 : (CB == 2 ? 2 : 4);
+    __device__ static int cb0(int w) { return CB >= 4 ? w : (CB == 2 ? (w & 1) : 0); }
+    __device__ static int rb0(int w) { return CB >= 4 ? 0 : (CB == 2 ? (w >> 1) : w); }
+};
+
+// acc[i][j] += A[rows of rb(i)][k] * W[cols of cb(j)][k], k in [kb, ke) (multiples of 16).
+// A: LDS row-major (lda floats), columns offset by a_col0 relative to k.
+// W: global row-major [N][ldw] (weights, L2-resident).
+template <int NRW, int NCW>
+__device__ __forceinline__ void gemm_tile(floatx4 (&acc)[NRW][NCW], const float* As, int lda, int a_col0,
+                                          int rb0, int rbs, int rb_lim, const float* __restrict__ W, int ldw,
+                                          int cb0, int cbs, int kb, int ke, int lane) {
+    const int r = lane & 15, q = lane >> 4;
+#pragma unroll 2
+    for (int k = kb; k < ke; k += 16) {
+        float4 b[NCW];
+#pragma unroll
+        for (int j = 0; j < NCW; ++j)
+            b[j] = *reinterpret_cast<const float4*>(W + (size_t)((cb0 + j * cbs) * 16 + r) * ldw + k + 4 * q);
+#pragma unroll
+        for (int i = 0; i < NRW; ++i) {
+            const int rb = rb0 + i * rbs;
+            if (rb >= rb_lim) continue;
+            const float4 a = *reinterpret_cast<const float4*>(As + (rb * 16 + r) * lda + (k - a_col0) + 4 * q);
+#pragma unroll
+            for (int j = 0; j < NCW; ++j) acc[i][j] = mfma_k16(a, b[j], acc[i][j]);
+        }
+    }
+}
+
+template <int NRW, int NCW>
+__device__ __forceinline__ void zero_acc(floatx4 (&acc)[NRW][NCW]) {
+#pragma unroll
+    for (int i = 0; i < NRW; ++i)
+#pragma unroll
+        for (int j = 0; j < NCW; ++j) acc[i][j] = zero4();
+}
+
+// ---------------------------------------------------------------------------
+// Deterministic block reductions (fixed tree order).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+template <int NT>
+__device__ __forceinline__ double block_sum(double v, double* red /* LDS, >= NT/64 */) {
+    v = wave_sum(v);
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    __syncthreads();
+    if (l == 0) red[w] = v;
+    __syncthreads();
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) s += red[i];
+    return s;
+}
+
+__host__ __device__ __forceinline__ int round_up(int x, int m) { return (x + m - 1) / m * m; }
+
+// Offsets (in floats) of the packed parameter set — see pack_params.
+struct Packed {
+    int W0, W1, b1, W2, b2, W1T, W2T, ls, total;
+    __host__ __device__ Packed(int h0, int h1, int np, int mp) {
+        int o = 0;
+        if (h0 == 0) {                 // linear: Wp [MP][NP] only
+            W0 = o; o += mp * np;
+            W1 = b1 = W2 = b2 = W1T = W2T = o;
+        } else {
+            W0 = o;  o += h0 * np;
+            W1 = o;  o += h1 * h0;
+            b1 = o;  o += h1;
+            W2 = o;  o += mp * h1;
+            b2 = o;  o += mp;
+            W1T = o; o += h0 * h1;
+            W2T = o; o += h1 * mp;
+        }
+        ls = o; o += mp;
+        total = round_up(o, 4);
+    }
+};
+
+}  // namespace mjrl

@@ -1,0 +1,849 @@
+// policy.hip — Gaussian-MLP / linear policy passes over the timestep batch.
+//
+// Three launches per pass:
+//   k_rows<H0,H1,MP,MODE>  persistent, one 64-row (32 for 256-wide layers) tile of
+//                          timesteps at a time; the whole per-row chain runs out of
+//                          LDS on v_mfma_f32_16x16x4_f32:
+//                            FWD  forward + LL + VPG upstream + backprop to every layer
+//                            FVP  JVP of the tangent + Gauss-Newton weight + backprop
+//                            EVAL forward at new params + likelihood ratio + KL
+//   k_wgrad                split-K over timesteps: weight gradients G^T A per layer
+//                          (bias gradients ride along: the obs bias column / column sums)
+//   k_gather               fixed-order sum of the slabs into the flat d-vector
+//
+// Reference math: mjrl/policies/gaussian_mlp.py:100-182, gaussian_linear.py:98-175,
+// mjrl/algos/batch_reinforce.py:37-55, mjrl/algos/npg_cg.py:55-74.
+#include <math.h>
+
+#include "common.h"
+
+using namespace mjrl;
+
+namespace {
+
+enum { FWD = 0, FVP = 1, EVAL = 2 };
+
+struct RowArgs {
+    int64_t T;            // rows processed by this call
+    int np, m;
+    const float* xhat;
+    const float* act;
+    const float* adv;     // EVAL: surrogate advantages
+    const float* adv_vpg; // FWD: advantages driving the gradient
+    float* a0;
+    float* a1;
+    float* mu0;
+    float* ll0;
+    float* gu0;
+    float* gu1;
+    float* gp;
+    const float* P;       // packed theta (new)
+    const float* V;       // FVP: packed tangent;  EVAL: packed old theta (log_std)
+    const float* out_shift;
+    const float* out_scale;
+    double* rpart;        // per-workgroup partials
+    const int32_t* done;
+    float llc;            // -0.5 * m * log(2 pi) rounded to f32
+};
+
+template <int H0, int H1, int MP>
+struct Layout {
+    static constexpr bool LIN = (H0 == 0);
+    static constexpr int HMAX = H0 > H1 ? H0 : H1;
+    static constexpr int BT = HMAX >= 256 ? 32 : 64;
+    static constexpr int RB = BT / 16;
+    static constexpr int LD0 = LIN ? 0 : H0 + 4;
+    static constexpr int LD1 = LIN ? 0 : H1 + 4;
+    static constexpr int LDP = MP + 4;
+    static constexpr int KC = 64;
+    static constexpr int LDX = KC + 4;
+    static constexpr int oD0 = 0;
+    static constexpr int oA0 = oD0 + BT * LD0;
+    static constexpr int oD1 = oA0 + BT * LD0;
+    static constexpr int oA1 = oD1 + BT * LD1;
+    static constexpr int oGP = oA1 + BT * LD1;
+    static constexpr int XS = 2 * BT * LDX;
+    static constexpr bool XS_ALIAS = !LIN && 2 * BT * LD1 >= XS;
+    static constexpr int oXS = XS_ALIAS ? oD1 : oGP + BT * LDP;
+    static constexpr int end1 = XS_ALIAS ? oGP + BT * LDP : oXS + XS;
+    static constexpr int SCR = BT * MP + 4 * BT;   // log-std scratch [BT][MP] + 2*BT doubles
+    static constexpr bool SCR_IN_D0 = !LIN && BT * LD0 >= SCR;
+    static constexpr int oSCR = SCR_IN_D0 ? oD0 : end1;
+    static constexpr int total = SCR_IN_D0 ? end1 : end1 + SCR;
+    static constexpr int bytes = total * 4;
+};
+
+__device__ __forceinline__ float tanh_f(float x) { return tanhf(x); }
+
+template <int H0, int H1, int MP, int MODE>
+__global__ void __launch_bounds__(NTHREADS, (Layout<H0, H1, MP>::bytes > 81920 ? 1 : 2)) k_rows(RowArgs a) {
+    using L = Layout<H0, H1, MP>;
+    constexpr int BT = L::BT, RB = L::RB;
+    constexpr int N1 = L::LIN ? MP : H0;
+    using S1 = Split<RB, N1 / 16>;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* D0 = smem + L::oD0;
+    float* A0s = smem + L::oA0;
+    float* D1 = smem + L::oD1;
+    float* A1s = smem + L::oA1;
+    float* GPs = smem + L::oGP;
+    float* XS = smem + L::oXS;
+    float* LSs = smem + L::oSCR;                                   // [BT][MP]
+    double* RED = reinterpret_cast<double*>(smem + L::oSCR + BT * MP);   // [2][BT]
+
+    if (MODE == FVP && a.done && *a.done) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int r16 = lane & 15, q = lane >> 4;
+    const int np = a.np, m = a.m;
+    const int64_t T = a.T;
+    const int64_t ntiles = (T + BT - 1) / BT;
+
+    const float* P = a.P;
+    const Packed pk(H0, H1, np, MP);
+    // per-lane output-column constants for the output layer
+    double ls_acc = 0.0;             // FWD: log-std gradient partial (thread j < MP)
+    double surr_acc = 0.0, kl_acc = 0.0;   // EVAL partials (thread 0)
+
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t row_base = tile * BT;
+
+        // ---------------- phase 1: [BT x N1] = xhat[BT x np] * W^T, K = np ----------------
+        floatx4 acc1[S1::NRW][S1::NCW];
+        zero_acc(acc1);
+        {
+            const float* W = (MODE == FVP ? a.V : P) + pk.W0;
+            constexpr int PER = BT * (L::KC / 4) / NTHREADS;
+            float4 st[PER];
+            const int nch = (np + L::KC - 1) / L::KC;
+            auto gload = [&](int c) {
+#pragma unroll
+                for (int u = 0; u < PER; ++u) {
+                    const int idx = tid + u * NTHREADS;
+                    const int row = idx / (L::KC / 4), c4 = idx % (L::KC / 4);
+                    const int col = c * L::KC + c4 * 4;
+                    const int64_t gr = row_base + row;
+                    st[u] = (gr < T && col < np) ? *reinterpret_cast<const float4*>(a.xhat + gr * np + col)
+                                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+            };
+            gload(0);
+            for (int c = 0; c < nch; ++c) {
+                float* xs = XS + (c & 1) * BT * L::LDX;
+#pragma unroll
+                for (int u = 0; u < PER; ++u) {
+                    const int idx = tid + u * NTHREADS;
+                    const int row = idx / (L::KC / 4), c4 = idx % (L::KC / 4);
+                    *reinterpret_cast<float4*>(xs + row * L::LDX + c4 * 4) = st[u];
+                }
+                __syncthreads();
+                if (c + 1 < nch) gload(c + 1);
+                const int kb = c * L::KC;
+                const int ke = kb + L::KC < np ? kb + L::KC : np;
+                gemm_tile(acc1, xs, L::LDX, kb, S1::rb0(w), S1::RBS, RB, W, np, S1::cb0(w), S1::CBS, kb, ke, lane);
+            }
+            __syncthreads();
+        }
+
+        if constexpr (L::LIN) {
+            // ---------------- linear policy: phase 1 is the output layer -----------
+#pragma unroll
+            for (int i = 0; i < S1::NRW; ++i) {
+                const int rb = S1::rb0(w) + i * S1::RBS;
+                if (rb >= RB) continue;
+#pragma unroll
+                for (int j = 0; j < S1::NCW; ++j) {
+                    const int col = (S1::cb0(w) + j * S1::CBS) * 16 + r16;
+                    const float ls = P[pk.ls + col];
+                    const float os = a.out_scale ? (col < m ? a.out_scale[col] : 1.f) : 1.f;
+                    const float osh = a.out_shift ? (col < m ? a.out_shift[col] : 0.f) : 0.f;
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) {
+                        const int row = rb * 16 + 4 * q + rr;
+                        const float v = acc1[i][j][rr];
+                        if (MODE == FVP) {
+                            const float sg = expf(ls);
+                            const float wq = os * os * (2.f / (2.f * sg * sg + 1e-8f));
+                            const float g = col < m ? wq * v : 0.f;
+                            const int64_t gr = row_base + row;
+                            if (gr < T) a.gp[gr * MP + col] = g;
+                        } else {
+                            GPs[row * L::LDP + col] = col < m ? v * os + osh : 0.f;
+                        }
+                    }
+                }
+            }
+        } else {
+            // ---------------- epilogue 1 ----------------
+#pragma unroll
+            for (int i = 0; i < S1::NRW; ++i) {
+                const int rb = S1::rb0(w) + i * S1::RBS;
+                if (rb >= RB) continue;
+#pragma unroll
+                for (int j = 0; j < S1::NCW; ++j) {
+                    const int col = (S1::cb0(w) + j * S1::CBS) * 16 + r16;
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) {
+                        const int row = rb * 16 + 4 * q + rr;
+                        const int64_t gr = row_base + row;
+                        const float v = acc1[i][j][rr];
+                        if (MODE == FVP) {
+                            const float av = gr < T ? a.a0[gr * H0 + col] : 0.f;
+                            D0[row * L::LD0 + col] = (1.f - av * av) * v;
+                            A0s[row * L::LD0 + col] = av;
+                        } else {
+                            const float av = tanh_f(v);
+                            A0s[row * L::LD0 + col] = av;
+                            if (MODE == FWD && gr < T) a.a0[gr * H0 + col] = av;
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+
+            // ---------------- phase 2: [BT x H1], K = H0 ----------------
+            using S2 = Split<RB, H1 / 16>;
+            floatx4 acc2[S2::NRW][S2::NCW];
+            zero_acc(acc2);
+            if (MODE == FVP) {
+                gemm_tile(acc2, D0, L::LD0, 0, S2::rb0(w), S2::RBS, RB, P + pk.W1, H0, S2::cb0(w), S2::CBS, 0, H0,
+                          lane);
+                gemm_tile(acc2, A0s, L::LD0, 0, S2::rb0(w), S2::RBS, RB, a.V + pk.W1, H0, S2::cb0(w), S2::CBS, 0,
+                          H0, lane);
+            } else {
+                gemm_tile(acc2, A0s, L::LD0, 0, S2::rb0(w), S2::RBS, RB, P + pk.W1, H0, S2::cb0(w), S2::CBS, 0, H0,
+                          lane);
+            }
+            // epilogue 2
+#pragma unroll
+            for (int i = 0; i < S2::NRW; ++i) {
+                const int rb = S2::rb0(w) + i * S2::RBS;
+                if (rb >= RB) continue;
+#pragma unroll
+                for (int j = 0; j < S2::NCW; ++j) {
+                    const int col = (S2::cb0(w) + j * S2::CBS) * 16 + r16;
+                    const float bias = (MODE == FVP ? a.V : P)[pk.b1 + col];
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) {
+                        const int row = rb * 16 + 4 * q + rr;
+                        const int64_t gr = row_base + row;
+                        const float v = acc2[i][j][rr] + bias;
+                        if (MODE == FVP) {
+                            const float av = gr < T ? a.a1[gr * H1 + col] : 0.f;
+                            D1[row * L::LD1 + col] = (1.f - av * av) * v;
+                            A1s[row * L::LD1 + col] = av;
+                        } else {
+                            const float av = tanh_f(v);
+                            A1s[row * L::LD1 + col] = av;
+                            if (MODE == FWD && gr < T) a.a1[gr * H1 + col] = av;
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+
+            // ---------------- phase 3: [BT x MP], K = H1 ----------------
+            using S3 = Split<RB, MP / 16>;
+            floatx4 acc3[S3::NRW][S3::NCW];
+            zero_acc(acc3);
+            if (MODE == FVP) {
+                gemm_tile(acc3, D1, L::LD1, 0, S3::rb0(w), S3::RBS, RB, P + pk.W2, H1, S3::cb0(w), S3::CBS, 0, H1,
+                          lane);
+                gemm_tile(acc3, A1s, L::LD1, 0, S3::rb0(w), S3::RBS, RB, a.V + pk.W2, H1, S3::cb0(w), S3::CBS, 0,
+                          H1, lane);
+            } else {
+                gemm_tile(acc3, A1s, L::LD1, 0, S3::rb0(w), S3::RBS, RB, P + pk.W2, H1, S3::cb0(w), S3::CBS, 0, H1,
+                          lane);
+            }
+#pragma unroll
+            for (int i = 0; i < S3::NRW; ++i) {
+                const int rb = S3::rb0(w) + i * S3::RBS;
+                if (rb >= RB) continue;
+#pragma unroll
+                for (int j = 0; j < S3::NCW; ++j) {
+                    const int col = (S3::cb0(w) + j * S3::CBS) * 16 + r16;
+                    const float bias = (MODE == FVP ? a.V : P)[pk.b2 + col];
+                    const float os = a.out_scale ? (col < m ? a.out_scale[col] : 1.f) : 1.f;
+                    const float osh = a.out_shift ? (col < m ? a.out_shift[col] : 0.f) : 0.f;
+                    float wq = 0.f;
+                    if (MODE == FVP) {
+                        const float sg = expf(P[pk.ls + col]);
+                        wq = os * os * (2.f / (2.f * sg * sg + 1e-8f));
+                    }
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) {
+                        const int row = rb * 16 + 4 * q + rr;
+                        const float v = acc3[i][j][rr] + bias;
+                        if (MODE == FVP) {
+                            const float g = col < m ? wq * v : 0.f;
+                            GPs[row * L::LDP + col] = g;
+                            const int64_t gr = row_base + row;
+                            if (gr < T) a.gp[gr * MP + col] = g;
+                        } else {
+                            GPs[row * L::LDP + col] = col < m ? v * os + osh : 0.f;
+                        }
+                    }
+                }
+            }
+        }
+        __syncthreads();
+
+        // ---------------- per-row pass: log-likelihood, VPG upstream, LR, KL -------------
+        if (MODE != FVP) {
+            if (tid < BT) {
+                const int row = tid;
+                const int64_t gr = row_base + row;
+                float* gpr = GPs + row * L::LDP;
+                if (gr < T) {
+                    float s2 = 0.f, sls = 0.f;
+                    if (MODE == FWD) {
+                        const float adv = a.adv_vpg[gr];
+                        for (int j = 0; j < m; ++j) {
+                            const float ls = P[pk.ls + j];
+                            const float sg = expf(ls);
+                            const float mu = gpr[j];
+                            const float zs = (a.act[gr * m + j] - mu) / sg;
+                            s2 += zs * zs;
+                            sls += ls;
+                            a.mu0[gr * m + j] = mu;
+                            LSs[row * MP + j] = adv * (zs * zs - 1.f);
+                            const float os = a.out_scale ? a.out_scale[j] : 1.f;
+                            gpr[j] = adv * (zs / sg) * os;
+                        }
+                        for (int j = m; j < MP; ++j) LSs[row * MP + j] = 0.f;
+                        a.ll0[gr] = ((-0.5f * s2) + (-sls)) + a.llc;
+                        for (int j = 0; j < MP; ++j) a.gp[gr * MP + j] = gpr[j];
+                    } else {   // EVAL
+                        float kl = 0.f, slo = 0.f;
+                        for (int j = 0; j < m; ++j) {
+                            const float lsn = P[pk.ls + j], lso = a.V[pk.ls + j];
+                            const float sn = expf(lsn), so = expf(lso);
+                            const float mun = gpr[j], muo = a.mu0[gr * m + j];
+                            const float zs = (a.act[gr * m + j] - mun) / sn;
+                            s2 += zs * zs;
+                            sls += lsn;
+                            slo += lso;
+                            const float dm = muo - mun;
+                            const float nr = (dm * dm + so * so) - sn * sn;
+                            const float dr = 2.f * sn * sn + 1e-8f;
+                            kl += (nr / dr + lsn) - lso;
+                        }
+                        const float lln = ((-0.5f * s2) + (-sls)) + a.llc;
+                        const float lr = expf(lln - a.ll0[gr]);
+                        RED[row] = (double)(lr * a.adv[gr]);
+                        RED[BT + row] = (double)kl;
+                    }
+                } else {
+                    if (MODE == FWD) {
+                        for (int j = 0; j < MP; ++j) {
+                            gpr[j] = 0.f;
+                            LSs[row * MP + j] = 0.f;
+                        }
+                    } else {
+                        RED[row] = 0.0;
+                        RED[BT + row] = 0.0;
+                    }
+                }
+            }
+            __syncthreads();
+            if (MODE == FWD) {
+                if (tid < MP) {
+                    double s = 0.0;
+                    for (int row = 0; row < BT; ++row) s += (double)LSs[row * MP + tid];
+                    ls_acc += s;
+                }
+            } else if (MODE == EVAL) {
+                if (tid == 0) {
+                    double s = 0.0, k = 0.0;
+                    for (int row = 0; row < BT; ++row) {
+                        s += RED[row];
+                        k += RED[BT + row];
+                    }
+                    surr_acc += s;
+                    kl_acc += k;
+                }
+            }
+            __syncthreads();
+        }
+
+        if constexpr (!L::LIN) {
+            if (MODE != EVAL) {
+                // ---------------- phase 4: ga1 = g * W2, K = MP ----------------
+                using S2 = Split<RB, H1 / 16>;
+                floatx4 acc4[S2::NRW][S2::NCW];
+                zero_acc(acc4);
+                gemm_tile(acc4, GPs, L::LDP, 0, S2::rb0(w), S2::RBS, RB, P + pk.W2T, MP, S2::cb0(w), S2::CBS, 0, MP,
+                          lane);
+#pragma unroll
+                for (int i = 0; i < S2::NRW; ++i) {
+                    const int rb = S2::rb0(w) + i * S2::RBS;
+                    if (rb >= RB) continue;
+#pragma unroll
+                    for (int j = 0; j < S2::NCW; ++j) {
+                        const int col = (S2::cb0(w) + j * S2::CBS) * 16 + r16;
+#pragma unroll
+                        for (int rr = 0; rr < 4; ++rr) {
+                            const int row = rb * 16 + 4 * q + rr;
+                            const float av = A1s[row * L::LD1 + col];
+                            const float g = (1.f - av * av) * acc4[i][j][rr];
+                            D1[row * L::LD1 + col] = g;
+                            const int64_t gr = row_base + row;
+                            if (gr < T) a.gu1[gr * H1 + col] = g;
+                        }
+                    }
+                }
+                __syncthreads();
+                // ---------------- phase 5: ga0 = gu1 * W1, K = H1 ----------------
+                floatx4 acc5[S1::NRW][S1::NCW];
+                zero_acc(acc5);
+                gemm_tile(acc5, D1, L::LD1, 0, S1::rb0(w), S1::RBS, RB, P + pk.W1T, H1, S1::cb0(w), S1::CBS, 0, H1,
+                          lane);
+#pragma unroll
+                for (int i = 0; i < S1::NRW; ++i) {
+                    const int rb = S1::rb0(w) + i * S1::RBS;
+                    if (rb >= RB) continue;
+#pragma unroll
+                    for (int j = 0; j < S1::NCW; ++j) {
+                        const int col = (S1::cb0(w) + j * S1::CBS) * 16 + r16;
+#pragma unroll
+                        for (int rr = 0; rr < 4; ++rr) {
+                            const int row = rb * 16 + 4 * q + rr;
+                            const float av = A0s[row * L::LD0 + col];
+                            const int64_t gr = row_base + row;
+                            if (gr < T) a.gu0[gr * H0 + col] = (1.f - av * av) * acc5[i][j][rr];
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+    }
+
+    if (MODE == FWD) {
+        if (tid < MP) a.rpart[(int64_t)blockIdx.x * MP + tid] = ls_acc;
+    } else if (MODE == EVAL) {
+        if (tid == 0) {
+            a.rpart[(int64_t)blockIdx.x * 2 + 0] = surr_acc;
+            a.rpart[(int64_t)blockIdx.x * 2 + 1] = kl_acc;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Weight gradients: C[N][K] = sum_t G[t][n] * A[t][k], split over T into S slices.
+// ---------------------------------------------------------------------------
+struct WJob {
+    const float* G;
+    const float* A;
+    int ldg, lda, N, K;
+    int nbN, nbK, bias;
+    int64_t off;    // float offset of slice 0's [N][K] slab in wpart
+    int64_t boff;   // float offset of slice 0's [N] bias slab
+};
+
+struct WArgs {
+    WJob job[3];
+    int njobs;
+    int start[4];   // prefix sums of blocks per slice per job
+    int S;
+    int64_t T;
+    int64_t rows_per_slice;
+    float* wpart;
+    const int32_t* done;
+};
+
+constexpr int WB = 64;        // output block edge
+constexpr int WT = 64;        // rows per staged tile
+constexpr int WLD = WB + 16;  // LDS row stride (floats): rows 4 apart land 16 banks apart
+
+__global__ void __launch_bounds__(NTHREADS, 2) k_wgrad(WArgs a) {
+    if (a.done && *a.done) return;
+    __shared__ __attribute__((aligned(16))) float Gs[WT * WLD];
+    __shared__ __attribute__((aligned(16))) float As[WT * WLD];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int r16 = lane & 15, q = lane >> 4;
+    const int jb = blockIdx.x / a.S, s = blockIdx.x % a.S;
+    int ji = 0;
+    while (ji + 1 < a.njobs && jb >= a.start[ji + 1]) ++ji;
+    const WJob& J = a.job[ji];
+    const int local = jb - a.start[ji];
+    const int nb = local / J.nbK, kb = local % J.nbK;
+    const int n0 = nb * WB, k0 = kb * WB;
+    const int64_t r0 = (int64_t)s * a.rows_per_slice;
+    int64_t r1 = r0 + a.rows_per_slice;
+    if (r1 > a.T) r1 = a.T;
+
+    floatx4 acc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = zero4();
+    double bsum = 0.0;
+    const bool do_bias = J.bias && kb == 0;
+
+    // staging: 64 rows x 64 cols of G and of A = 1024 float4 each, 4 per thread
+    float4 g4[4], a4[4];
+    auto gload = [&](int64_t t0) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int idx = tid + u * NTHREADS;
+            const int row = idx >> 4, c4 = (idx & 15) * 4;
+            const int64_t t = t0 + row;
+            const bool rv = t < r1;
+            g4[u] = (rv && n0 + c4 < J.N) ? *reinterpret_cast<const float4*>(J.G + t * J.ldg + n0 + c4)
+                                          : make_float4(0.f, 0.f, 0.f, 0.f);
+            a4[u] = (rv && k0 + c4 < J.K) ? *reinterpret_cast<const float4*>(J.A + t * J.lda + k0 + c4)
+                                          : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    if (r0 < r1) gload(r0);
+    for (int64_t t0 = r0; t0 < r1; t0 += WT) {
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int idx = tid + u * NTHREADS;
+            const int row = idx >> 4, c4 = (idx & 15) * 4;
+            *reinterpret_cast<float4*>(Gs + row * WLD + c4) = g4[u];
+            *reinterpret_cast<float4*>(As + row * WLD + c4) = a4[u];
+        }
+        __syncthreads();
+        if (t0 + WT < r1) gload(t0 + WT);
+        if (n0 + 16 * w < J.N) {
+#pragma unroll 4
+            for (int tt = 0; tt < WT; tt += 4) {
+                const float ga = Gs[(tt + q) * WLD + 16 * w + r16];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float ab = As[(tt + q) * WLD + 16 * i + r16];
+                    acc[i] = mfma4(ga, ab, acc[i]);
+                }
+            }
+        }
+        if (do_bias && tid < WB) {
+            double cs = 0.0;
+            for (int row = 0; row < WT; ++row) cs += (double)Gs[row * WLD + tid];
+            bsum += cs;
+        }
+    }
+    // write this slice's partial block
+    float* out = a.wpart + J.off + (int64_t)s * J.N * J.K;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int k = k0 + 16 * i + r16;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            const int n = n0 + 16 * w + 4 * q + rr;
+            if (n < J.N && k < J.K) out[(int64_t)n * J.K + k] = acc[i][rr];
+        }
+    }
+    if (do_bias && tid < WB && n0 + tid < J.N) a.wpart[J.boff + (int64_t)s * J.N + n0 + tid] = (float)bsum;
+}
+
+// ---------------------------------------------------------------------------
+// Gather: gsum[f] = sum over slices (fixed order) of the slab element feeding
+// flat parameter f (reference order, gaussian_mlp.py:61-64).
+// ---------------------------------------------------------------------------
+struct GArgs {
+    int n, m, h0, h1, np, mp, d, S;
+    int64_t off0, off1, off2, boff1, boff2;
+    const float* wpart;
+    const double* lspart;   // FWD: per-row-kernel-WG log-std partials [G][mp]; null for FVP
+    int G;
+    float* gsum;
+    const int32_t* done;
+};
+
+__global__ void __launch_bounds__(256) k_gather(GArgs a) {
+    if (a.done && *a.done) return;
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= a.d) return;
+    int64_t src = -1, stride = 0;
+    int lsj = -1;
+    int g = f;
+    if (a.h0 == 0) {
+        if (g < a.m * a.n) {
+            src = a.off0 + (int64_t)(g / a.n) * a.np + g % a.n;
+            stride = (int64_t)a.mp * a.np;
+        } else if ((g -= a.m * a.n) < a.m) {
+            src = a.off0 + (int64_t)g * a.np + a.n;
+            stride = (int64_t)a.mp * a.np;
+        } else {
+            lsj = g - a.m;
+        }
+    } else {
+        const int s0 = a.h0 * a.n, s1 = a.h0, s2 = a.h1 * a.h0, s3 = a.h1, s4 = a.m * a.h1, s5 = a.m;
+        if (g < s0) {
+            src = a.off0 + (int64_t)(g / a.n) * a.np + g % a.n;
+            stride = (int64_t)a.h0 * a.np;
+        } else if ((g -= s0) < s1) {
+            src = a.off0 + (int64_t)g * a.np + a.n;
+            stride = (int64_t)a.h0 * a.np;
+        } else if ((g -= s1) < s2) {
+            src = a.off1 + g;
+            stride = (int64_t)a.h1 * a.h0;
+        } else if ((g -= s2) < s3) {
+            src = a.boff1 + g;
+            stride = a.h1;
+        } else if ((g -= s3) < s4) {
+            src = a.off2 + g;   // [mp][h1] with rows < m contiguous as [m][h1]
+            stride = (int64_t)a.mp * a.h1;
+        } else if ((g -= s4) < s5) {
+            src = a.boff2 + g;
+            stride = a.mp;
+        } else {
+            lsj = g - s5;
+        }
+    }
+    double acc = 0.0;
+    if (src >= 0) {
+        for (int s = 0; s < a.S; ++s) acc += (double)a.wpart[src + s * stride];
+    } else if (a.lspart) {
+        for (int b = 0; b < a.G; ++b) acc += a.lspart[(int64_t)b * a.mp + lsj];
+    }
+    a.gsum[f] = (float)acc;
+}
+
+__global__ void __launch_bounds__(64) k_eval_final(const double* __restrict__ rpart, int G, double* __restrict__ sums) {
+    if (threadIdx.x != 0) return;
+    double s = 0.0, k = 0.0;
+    for (int b = 0; b < G; ++b) {
+        s += rpart[2 * b];
+        k += rpart[2 * b + 1];
+    }
+    sums[0] = s;
+    sums[1] = k;
+}
+
+// ---------------------------------------------------------------------------
+// host side: dispatch, grids, scratch sizes
+// ---------------------------------------------------------------------------
+constexpr int ROW_GRID_CAP = 512;
+constexpr int WGRAD_SLICES_CAP = 128;
+
+inline int bt_for(int h0, int h1) { return (h0 >= 256 || h1 >= 256) ? 32 : 64; }
+
+inline int row_grid(const mjrl_shape* s, int64_t T) {
+    const int bt = bt_for(s->h0, s->h1);
+    int64_t nt = (T + bt - 1) / bt;
+    if (nt < 1) nt = 1;
+    return (int)(nt < ROW_GRID_CAP ? nt : ROW_GRID_CAP);
+}
+
+inline int wgrad_slices(int64_t T) {
+    int64_t nt = (T + WT - 1) / WT;
+    if (nt < 1) nt = 1;
+    return (int)(nt < WGRAD_SLICES_CAP ? nt : WGRAD_SLICES_CAP);
+}
+
+struct JobSet {
+    int njobs;
+    WJob job[3];
+    int64_t floats;   // per full set (all slices)
+};
+
+JobSet make_jobs(const mjrl_shape* s, const mjrl_rows* r, int S) {
+    JobSet js{};
+    auto add = [&](const float* G, int ldg, const float* A, int lda, int N, int K, int bias) {
+        WJob& j = js.job[js.njobs++];
+        j.G = G; j.ldg = ldg; j.A = A; j.lda = lda; j.N = N; j.K = K;
+        j.nbN = (N + WB - 1) / WB; j.nbK = (K + WB - 1) / WB; j.bias = bias;
+        j.off = js.floats;
+        js.floats += (int64_t)S * N * K;
+        j.boff = js.floats;
+        if (bias) js.floats += (int64_t)S * N;
+    };
+    if (s->h0 == 0) {
+        add(r ? r->gp : nullptr, s->mp, r ? r->xhat : nullptr, s->np, s->mp, s->np, 0);
+    } else {
+        add(r ? r->gu0 : nullptr, s->h0, r ? r->xhat : nullptr, s->np, s->h0, s->np, 0);
+        add(r ? r->gu1 : nullptr, s->h1, r ? r->a0 : nullptr, s->h0, s->h1, s->h0, 1);
+        add(r ? r->gp : nullptr, s->mp, r ? r->a1 : nullptr, s->h1, s->mp, s->h1, 1);
+    }
+    return js;
+}
+
+template <int H0, int H1, int MP, int MODE>
+int launch_rows_t(const RowArgs& ra, int grid, hipStream_t st) {
+    using L = Layout<H0, H1, MP>;
+    auto fn = k_rows<H0, H1, MP, MODE>;
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, L::bytes);
+        if (e != hipSuccess) return (int)e;
+        attr = true;
+    }
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(NTHREADS), L::bytes, st, ra);
+    return (int)hipGetLastError();
+}
+
+template <int MODE>
+int launch_rows(const mjrl_shape* s, const RowArgs& ra, int grid, hipStream_t st) {
+#define MJRL_ROWS_CASE(H0_, H1_, MP_) \
+    if (s->h0 == H0_ && s->h1 == H1_ && s->mp == MP_) return launch_rows_t<H0_, H1_, MP_, MODE>(ra, grid, st);
+#define MJRL_ROWS_MP(H0_, H1_) MJRL_ROWS_CASE(H0_, H1_, 16) MJRL_ROWS_CASE(H0_, H1_, 32) MJRL_ROWS_CASE(H0_, H1_, 64)
+    MJRL_ROWS_MP(0, 0)
+    MJRL_ROWS_MP(32, 32)
+    MJRL_ROWS_MP(64, 64)
+    MJRL_ROWS_MP(128, 128)
+    MJRL_ROWS_MP(256, 256)
+#undef MJRL_ROWS_MP
+#undef MJRL_ROWS_CASE
+    return MJRL_ESHAPE;
+}
+
+bool shape_supported(int h0, int h1, int mp) {
+    if (mp != 16 && mp != 32 && mp != 64) return false;
+    if (h0 == 0 && h1 == 0) return true;
+    return h0 == h1 && (h0 == 32 || h0 == 64 || h0 == 128 || h0 == 256);
+}
+
+RowArgs row_args(const mjrl_shape* s, const mjrl_rows* r, int64_t T) {
+    RowArgs ra{};
+    ra.T = T;
+    ra.np = s->np;
+    ra.m = s->m;
+    ra.xhat = r->xhat; ra.act = r->act; ra.adv = r->adv; ra.adv_vpg = r->adv_vpg;
+    ra.a0 = r->a0; ra.a1 = r->a1; ra.mu0 = r->mu0; ra.ll0 = r->ll0;
+    ra.gu0 = r->gu0; ra.gu1 = r->gu1; ra.gp = r->gp;
+    ra.llc = (float)(-0.5 * (double)s->m * log(2.0 * M_PI));
+    return ra;
+}
+
+int run_wgrad_gather(const mjrl_shape* s, const mjrl_rows* r, int64_t T, const mjrl_scratch* sc,
+                     const double* lspart, int G, const int32_t* done, float* gsum, hipStream_t st) {
+    const int S = sc->slices;
+    JobSet js = make_jobs(s, r, S);
+    WArgs wa{};
+    wa.njobs = js.njobs;
+    int tot = 0;
+    for (int j = 0; j < js.njobs; ++j) {
+        wa.job[j] = js.job[j];
+        wa.start[j] = tot;
+        tot += js.job[j].nbN * js.job[j].nbK;
+    }
+    wa.start[js.njobs] = tot;
+    wa.S = S;
+    wa.T = T;
+    const int64_t tiles = (T + WT - 1) / WT;
+    wa.rows_per_slice = ((tiles + S - 1) / S) * WT;
+    wa.wpart = sc->wpart;
+    wa.done = done;
+    if (T > 0) {
+        hipLaunchKernelGGL(k_wgrad, dim3(tot * S), dim3(NTHREADS), 0, st, wa);
+    } else {
+        hipMemsetAsync(sc->wpart, 0, js.floats * sizeof(float), st);
+    }
+    GArgs ga{};
+    ga.n = s->n; ga.m = s->m; ga.h0 = s->h0; ga.h1 = s->h1; ga.np = s->np; ga.mp = s->mp; ga.d = s->d; ga.S = S;
+    ga.off0 = js.job[0].off;
+    if (s->h0) {
+        ga.off1 = js.job[1].off; ga.boff1 = js.job[1].boff;
+        ga.off2 = js.job[2].off; ga.boff2 = js.job[2].boff;
+    }
+    ga.wpart = sc->wpart;
+    ga.lspart = lspart;
+    ga.G = G;
+    ga.gsum = gsum;
+    ga.done = done;
+    hipLaunchKernelGGL(k_gather, dim3((s->d + 255) / 256), dim3(256), 0, st, ga);
+    return (int)hipGetLastError();
+}
+
+bool rows_ok(const mjrl_shape* s, const mjrl_rows* r) {
+    if (!s || !r || r->T < 0 || !r->xhat) return false;
+    if (s->h0 && (!r->a0 || !r->a1 || !r->gu0 || !r->gu1)) return false;
+    return r->gp != nullptr;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mjrl_shape_init(mjrl_shape* s, int32_t n, int32_t m, int32_t h0, int32_t h1) {
+    if (!s || n <= 0 || m <= 0 || h0 < 0 || h1 < 0) return MJRL_EINVAL;
+    s->n = n;
+    s->m = m;
+    s->h0 = h0;
+    s->h1 = h1;
+    s->np = round_up(n + 1, 16);
+    s->mp = m <= 16 ? 16 : (m <= 32 ? 32 : (m <= 64 ? 64 : round_up(m, 16)));
+    if (h0 == 0)
+        s->d = m * n + m + m;
+    else
+        s->d = h0 * n + h0 + h1 * h0 + h1 + m * h1 + m + m;
+    s->packed = Packed(h0, h1, s->np, s->mp).total;
+    return shape_supported(h0, h1, s->mp) ? MJRL_OK : MJRL_ESHAPE;
+}
+
+int mjrl_scratch_size(const mjrl_shape* s, int64_t T, int64_t* wpart_floats, int64_t* rpart_doubles,
+                      int32_t* slices) {
+    if (!s || T < 0 || !wpart_floats || !rpart_doubles || !slices) return MJRL_EINVAL;
+    const int S = wgrad_slices(T);
+    *slices = S;
+    *wpart_floats = make_jobs(s, nullptr, S).floats;
+    const int64_t rp = (int64_t)ROW_GRID_CAP * (s->mp > 2 ? s->mp : 2);
+    *rpart_doubles = rp + 4 * 256 + 16;
+    return MJRL_OK;
+}
+
+int mjrl_policy_vpg(const mjrl_shape* s, const mjrl_rows* rows, const float* packed_theta, const float* out_shift,
+                    const float* out_scale, const mjrl_scratch* sc, float* gsum, void* stream) {
+    if (!rows_ok(s, rows) || !packed_theta || !sc || !gsum || !rows->act || !rows->adv_vpg || !rows->mu0 ||
+        !rows->ll0)
+        return MJRL_EINVAL;
+    if (!shape_supported(s->h0, s->h1, s->mp)) return MJRL_ESHAPE;
+    hipStream_t st = (hipStream_t)stream;
+    RowArgs ra = row_args(s, rows, rows->T);
+    ra.P = packed_theta;
+    ra.out_shift = out_shift;
+    ra.out_scale = out_scale;
+    ra.rpart = sc->rpart;
+    const int G = row_grid(s, rows->T);
+    int e = MJRL_OK;
+    if (rows->T > 0) e = launch_rows<FWD>(s, ra, G, st);
+    else hipMemsetAsync(sc->rpart, 0, sizeof(double) * G * s->mp, st);
+    if (e) return e;
+    return run_wgrad_gather(s, rows, rows->T, sc, sc->rpart, G, nullptr, gsum, st);
+}
+
+int mjrl_policy_fvp(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_fvp, const float* packed_theta,
+                    const float* packed_v, const float* out_scale, const mjrl_scratch* sc, const int32_t* done,
+                    float* gsum, void* stream) {
+    if (!rows_ok(s, rows) || !packed_theta || !packed_v || !sc || !gsum || T_fvp < 0 || T_fvp > rows->T)
+        return MJRL_EINVAL;
+    if (!shape_supported(s->h0, s->h1, s->mp)) return MJRL_ESHAPE;
+    hipStream_t st = (hipStream_t)stream;
+    RowArgs ra = row_args(s, rows, T_fvp);
+    ra.P = packed_theta;
+    ra.V = packed_v;
+    ra.out_scale = out_scale;
+    ra.done = done;
+    int e = MJRL_OK;
+    if (T_fvp > 0) e = launch_rows<FVP>(s, ra, row_grid(s, T_fvp), st);
+    if (e) return e;
+    return run_wgrad_gather(s, rows, T_fvp, sc, nullptr, 0, done, gsum, st);
+}
+
+int mjrl_policy_eval(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_eval, const float* packed_theta_new,
+                     const float* packed_theta_old, const float* out_shift, const float* out_scale,
+                     const mjrl_scratch* sc, double* sums, void* stream) {
+    if (!rows_ok(s, rows) || !packed_theta_new || !packed_theta_old || !sc || !sums || T_eval < 0 ||
+        T_eval > rows->T || !rows->adv || !rows->mu0 || !rows->ll0)
+        return MJRL_EINVAL;
+    if (!shape_supported(s->h0, s->h1, s->mp)) return MJRL_ESHAPE;
+    hipStream_t st = (hipStream_t)stream;
+    RowArgs ra = row_args(s, rows, T_eval);
+    ra.P = packed_theta_new;
+    ra.V = packed_theta_old;
+    ra.out_shift = out_shift;
+    ra.out_scale = out_scale;
+    ra.rpart = sc->rpart;
+    const int G = row_grid(s, T_eval);
+    if (T_eval > 0) {
+        int e = launch_rows<EVAL>(s, ra, G, st);
+        if (e) return e;
+    } else {
+        hipMemsetAsync(sc->rpart, 0, sizeof(double) * 2 * G, st);
+    }
+    hipLaunchKernelGGL(k_eval_final, dim3(1), dim3(64), 0, st, sc->rpart, G, sums);
+    return (int)hipGetLastError();
+}
+
+}  // extern "C"

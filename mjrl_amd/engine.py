@@ -1,0 +1,419 @@
+"""Device-side update engine: one NPG / TRPO / DAPG / vanilla-PG update over a
+trajectory batch resident in HBM, driven through the C ABI (include/mjrl_amd.h).
+
+Everything between the batch and the host readback at the end is stream-ordered
+device work: no host synchronisation inside the CG loop (a device `done` flag
+replaces cg_solve's early break, mjrl/utils/cg_solve.py:19-20).  With a
+torch.distributed group every rank runs this on its own shard of paths and the
+sums listed in mjrl_amd/comm.py are all-reduced (RCCL) between the kernels.
+
+Reference this replaces: mjrl/algos/npg_cg.py:84-165 (NPG.train_from_paths),
+mjrl/algos/trpo.py:54-145, mjrl/algos/dapg.py:54-141,
+mjrl/algos/batch_reinforce.py:106-164, mjrl/utils/process_samples.py:3-44.
+"""
+import ctypes as C
+import math
+
+import numpy as np
+import torch
+
+from . import _lib
+from .comm import LocalComm
+
+# slots (doubles) in the per-update stats buffer; each moments result takes 8
+S_M1, S_M2, S_PM1, S_PM2, S_MS, S_MW1, S_MW2, S_EVAL = 0, 8, 16, 24, 32, 40, 48, 56
+N_STATS = 64
+
+
+class DeviceBatch:
+    """One shard of trajectories in HBM — the hot path's input.
+
+    obs / act: f64 [T_all][n] / [T_all][m], the T RL rows (path order) followed by
+    T_demo demonstration rows (DAPG).  rewards, baseline: f64 [T].  path_off:
+    i64 [P+1] row offsets; terminated: u8 [P].  advantages (optional, f64 [T]):
+    when given, the GAE scan is skipped (train_from_paths semantics)."""
+
+    def __init__(self, obs, act, rewards, baseline, path_off, terminated, advantages=None, T_demo=0):
+        self.obs, self.act = obs, act
+        self.rewards, self.baseline = rewards, baseline
+        self.path_off, self.terminated = path_off, terminated
+        self.advantages = advantages
+        self.T_demo = int(T_demo)
+        self.T = int(obs.shape[0]) - self.T_demo
+        self.P = int(path_off.shape[0]) - 1
+        self.lengths = None   # host copy, set by from_paths
+
+    @classmethod
+    def from_paths(cls, paths, device, baseline=None, use_advantages=False, demo_paths=None):
+        """Stages sampler-format paths (mjrl/samplers/base_sampler.py:76-83) into HBM.
+
+        The concatenation goes straight into pinned host buffers and one H2D
+        copy per array (np.concatenate of npg_cg.py:87-89 without the extra
+        temporary).  Baseline predictions come from the caller's baseline object,
+        per path, as compute_advantages does (process_samples.py:23)."""
+        lengths = np.array([len(p["rewards"]) for p in paths], dtype=np.int64)
+        T = int(lengths.sum())
+        n = paths[0]["observations"].shape[1]
+        m = paths[0]["actions"].shape[1]
+        dlen = [len(p["observations"]) for p in (demo_paths or [])]
+        T_demo = int(sum(dlen))
+
+        def stage(arrs, shape, dtype=np.float64):
+            h = torch.empty(shape, dtype=torch.float64 if dtype == np.float64 else torch.int64, pin_memory=True)
+            if len(arrs):
+                np.concatenate(arrs, axis=0, out=h.numpy())
+            return h.to(device, non_blocking=True)
+
+        obs = stage([p["observations"] for p in paths] + [p["observations"] for p in demo_paths or []],
+                    (T + T_demo, n))
+        act = stage([p["actions"] for p in paths] + [p["actions"] for p in demo_paths or []], (T + T_demo, m))
+        rew = stage([p["rewards"] for p in paths], (T,))
+        if use_advantages:
+            base = None
+            adv = stage([p["advantages"] for p in paths], (T,))
+        else:
+            base = stage([baseline.predict(p) if baseline is not None else np.zeros(len(p["rewards"]))
+                          for p in paths], (T,))
+            adv = None
+        off = torch.from_numpy(np.concatenate([[0], np.cumsum(lengths)]).astype(np.int64)).to(device)
+        term = torch.tensor([bool(p.get("terminated", False)) for p in paths], dtype=torch.uint8).to(device)
+        b = cls(obs, act, rew, base, off, term, advantages=adv, T_demo=T_demo)
+        b.lengths = lengths
+        return b
+
+
+class UpdateEngine:
+    """Owns the HBM workspace for one policy shape and runs updates on it."""
+
+    def __init__(self, n, m, hidden, device=None, comm=None, min_log_std=-3.0):
+        self.lib = _lib.lib()
+        h0, h1 = (0, 0) if hidden is None else (int(hidden[0]), int(hidden[1]))
+        self.shape = _lib.make_shape(int(n), int(m), h0, h1)
+        self.device = torch.device(device if device is not None else "cuda")
+        self.comm = comm or LocalComm()
+        self.min_log_std = float(min_log_std)
+        self.cap_T = -1
+        self.cap_P = -1
+        s = self.shape
+        dev = self.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.packed_theta = torch.zeros(s.packed, **f32)
+        self.packed_new = torch.zeros(s.packed, **f32)
+        self.packed_p = torch.zeros(s.packed, **f32)
+        self.vec = {k: torch.zeros(s.d, **f32) for k in ("g", "gsum", "x", "r", "p", "z", "theta_new")}
+        self.cg = torch.zeros(8, **f32)
+        self.done = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.out = torch.zeros(4, **f32)
+        self.stats = torch.zeros(N_STATS, dtype=torch.float64, device=dev)
+        self.mom_part = torch.zeros(4 * 256 + 16, dtype=torch.float64, device=dev)
+        self.transforms = (None, None, None, None)
+
+    # ------------------------------------------------------------------
+    def set_transformations(self, in_shift=None, in_scale=None, out_shift=None, out_scale=None):
+        """MuNet.set_transformations (gaussian_mlp.py:160-174), as f32 device vectors."""
+        def dv(v):
+            return None if v is None else torch.from_numpy(np.float32(np.asarray(v))).to(self.device)
+        ins, isc = dv(in_shift), dv(in_scale)
+        if (ins is None) != (isc is None):   # the kernel needs both; defaults are 0 / 1
+            ins = ins if ins is not None else torch.zeros(self.shape.n, dtype=torch.float32, device=self.device)
+            isc = isc if isc is not None else torch.ones(self.shape.n, dtype=torch.float32, device=self.device)
+        self.transforms = (ins, isc, dv(out_shift), dv(out_scale))
+
+    def _ensure(self, T_all, P):
+        if T_all <= self.cap_T and P <= self.cap_P:
+            return
+        s = self.shape
+        T_all = max(T_all, 1)
+        P = max(P, 1)
+        dev = self.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        f64 = dict(dtype=torch.float64, device=dev)
+        self.ws = {}
+        w = self.ws
+        w["xhat"] = torch.empty((T_all, s.np), **f32)
+        w["act32"] = torch.empty((T_all, s.m), **f32)
+        w["ret"] = torch.empty(T_all, **f64)
+        w["adv64"] = torch.empty(T_all, **f64)
+        w["w64"] = torch.empty(T_all, **f64)
+        w["path_ret"] = torch.empty(P, **f64)
+        w["adv32"] = torch.empty(T_all, **f32)
+        w["adv_vpg"] = torch.empty(T_all, **f32)
+        h0 = max(s.h0, 1)
+        h1 = max(s.h1, 1)
+        w["a0"] = torch.empty((T_all, h0), **f32)
+        w["a1"] = torch.empty((T_all, h1), **f32)
+        w["gu0"] = torch.empty((T_all, h0), **f32)
+        w["gu1"] = torch.empty((T_all, h1), **f32)
+        w["mu0"] = torch.empty((T_all, s.m), **f32)
+        w["ll0"] = torch.empty(T_all, **f32)
+        w["gp"] = torch.empty((T_all, s.mp), **f32)
+        wf, rd, sl = C.c_int64(), C.c_int64(), C.c_int32()
+        _lib.check(self.lib.mjrl_scratch_size(C.byref(s), T_all, C.byref(wf), C.byref(rd), C.byref(sl)),
+                   "mjrl_scratch_size")
+        w["wpart"] = torch.empty(max(wf.value, 1), **f32)
+        w["rpart"] = torch.zeros(max(rd.value, 1), **f64)
+        self.scratch_slices = sl.value
+        self.cap_T, self.cap_P = T_all, P
+
+    def _scratch(self, T):
+        wf, rd, sl = C.c_int64(), C.c_int64(), C.c_int32()
+        self.lib.mjrl_scratch_size(C.byref(self.shape), T, C.byref(wf), C.byref(rd), C.byref(sl))
+        sc = _lib.Scratch()
+        sc.wpart = self.ws["wpart"].data_ptr()
+        sc.rpart = self.ws["rpart"].data_ptr()
+        sc.slices = sl.value
+        return sc
+
+    def _rows(self, T, adv_vpg):
+        w = self.ws
+        r = _lib.Rows()
+        r.T = T
+        for k, key in (("xhat", "xhat"), ("act", "act32"), ("adv", "adv32"), ("a0", "a0"), ("a1", "a1"),
+                       ("mu0", "mu0"), ("ll0", "ll0"), ("gu0", "gu0"), ("gu1", "gu1"), ("gp", "gp")):
+            setattr(r, k, w[key].data_ptr())
+        r.adv_vpg = adv_vpg.data_ptr()
+        return r
+
+    def _stat(self, slot, n=3):
+        return self.stats[slot:slot + n]
+
+    def _moments(self, x, N, out_slot, center_slot=None, f32=False):
+        fn = self.lib.mjrl_moments_f32 if f32 else self.lib.mjrl_moments
+        center = None if center_slot is None else C.c_void_p(self.stats[center_slot:].data_ptr())
+        _lib.check(fn(_lib.ptr(x), N, center, _lib.ptr(self.mom_part),
+                      C.c_void_p(self.stats[out_slot:].data_ptr()), self.st), "mjrl_moments")
+        self.comm.allreduce_sum(self._stat(out_slot))
+
+    # ------------------------------------------------------------------
+    def returns_advantages(self, batch, gamma, gae_lambda):
+        """process_samples.compute_returns + compute_advantages on device (a1-a3).
+        Leaves f64 returns / advantages in ws['ret'] / ws['adv64']."""
+        self.st = _lib.stream_ptr()
+        self._ensure(batch.T + batch.T_demo, batch.P)
+        w = self.ws
+        use_gae = not (gae_lambda is None or gae_lambda < 0.0 or gae_lambda > 1.0)
+        base = batch.baseline if batch.baseline is not None else torch.zeros_like(batch.rewards)
+        _lib.check(self.lib.mjrl_gae(
+            _lib.ptr(batch.rewards), _lib.ptr(base), _lib.ptr(batch.path_off), _lib.ptr(batch.terminated),
+            batch.P, float(gamma), float(gae_lambda) if use_gae else 0.0, int(use_gae),
+            _lib.ptr(w["ret"]), _lib.ptr(w["adv64"]), _lib.ptr(w["path_ret"]), self.st), "mjrl_gae")
+        return w["ret"][:batch.T], w["adv64"][:batch.T]
+
+    def normalize_advantages(self, T):
+        """The `normalize` option of compute_advantages (process_samples.py:14-19,30-35)."""
+        w = self.ws
+        self._moments(w["adv64"], T, S_M1)
+        self._moments(w["adv64"], T, S_M2, center_slot=S_M1)
+        _lib.check(self.lib.mjrl_whiten(_lib.ptr(w["adv64"]), T, C.c_void_p(self.stats[S_M1:].data_ptr()),
+                                        C.c_void_p(self.stats[S_M2:].data_ptr()), 1e-8, None,
+                                        _lib.ptr(w["w64"]), self.st), "mjrl_whiten")
+        return w["w64"][:T]
+
+    def update(self, batch, theta, *, algo="npg", gamma=0.995, gae_lambda=0.98, n_step_size=0.01,
+               const_lr=None, kl_dist=None, cg_iters=10, damping=1e-4, residual_tol=1e-10,
+               demo_coef=None, learn_rate=0.01, T_global=None, trpo_verbose=True, skip_gae=False):
+        """One policy update.  `theta`: f32 device tensor [d] (flat params, reference
+        order).  algo in {'npg', 'trpo', 'dapg', 'vpg'}.
+
+        npg:  alpha = sqrt(|delta/(g.x)|), delta = n_step_size (or const_lr)  npg_cg.py:128-141
+        trpo: delta = 2 kl_dist + KL backtracking                              trpo.py:98-124
+        dapg: g = (T_all/T) vpg(all rows), delta = 2 kl_dist                   dapg.py:62-121
+        vpg:  theta + learn_rate * g (BatchREINFORCE)                          batch_reinforce.py:134-145
+        Returns host scalars plus the new device theta (self.vec['theta_new'])."""
+        L = self.lib
+        s = self.shape
+        self.st = st = _lib.stream_ptr()
+        T, T_demo, P = batch.T, batch.T_demo, batch.P
+        T_all = T + T_demo
+        self._ensure(T_all, P)
+        w = self.ws
+        v = self.vec
+        sp = C.byref(s)
+        ins, isc, osh, osc = self.transforms
+        timing = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+
+        # a5: batch assembly (f64 -> f32, input normalisation, bias column)
+        _lib.check(L.mjrl_pack_batch(_lib.ptr(batch.obs), _lib.ptr(batch.act), T_all, sp, _lib.ptr(ins),
+                                     _lib.ptr(isc), _lib.ptr(w["xhat"]), _lib.ptr(w["act32"]), st),
+                   "mjrl_pack_batch")
+        # a1-a3: returns / advantages
+        if batch.advantages is not None:
+            adv64 = batch.advantages
+            # path returns still come from the rewards (npg_cg.py:97)
+            self.returns_advantages(batch, gamma, None)
+        elif skip_gae:
+            adv64 = w["adv64"]
+        else:
+            self.returns_advantages(batch, gamma, gae_lambda)
+            adv64 = w["adv64"]
+        # whitening (npg_cg.py:91), two-pass fp64 moments, all-reduced when sharded
+        self._moments(adv64, T, S_M1)
+        self._moments(adv64, T, S_M2, center_slot=S_M1)
+        dapg = algo == "dapg" and demo_coef is not None
+        _lib.check(L.mjrl_whiten(_lib.ptr(adv64), T, C.c_void_p(self.stats[S_M1:].data_ptr()),
+                                 C.c_void_p(self.stats[S_M2:].data_ptr()), 1e-6, _lib.ptr(w["adv32"]),
+                                 _lib.ptr(w["w64"]) if dapg else None, st), "mjrl_whiten")
+        # surr_before = mean(LR * adv) with LR == 1 (npg_cg.py:113)
+        self._moments(w["adv32"], T, S_MS, f32=True)
+        # path-return statistics (npg_cg.py:97-102)
+        self._moments(w["path_ret"], P, S_PM1)
+        self.comm.allreduce_max(self.stats[S_PM1 + 4:S_PM1 + 6])
+        self._moments(w["path_ret"], P, S_PM2, center_slot=S_PM1)
+        if dapg:
+            self._moments(w["w64"], T, S_MW1)
+            self._moments(w["w64"], T, S_MW2, center_slot=S_MW1)
+            _lib.check(L.mjrl_dapg_adv(_lib.ptr(w["w64"]), T, C.c_void_p(self.stats[S_MW1:].data_ptr()),
+                                       C.c_void_p(self.stats[S_MW2:].data_ptr()), T_demo, float(demo_coef),
+                                       _lib.ptr(w["adv_vpg"]), st), "mjrl_dapg_adv")
+            adv_vpg = w["adv_vpg"]
+            T_vpg = T_all
+        else:
+            adv_vpg = w["adv32"]
+            T_vpg = T
+        # global row count (all ranks): scales every mean
+        if T_global is None:
+            tg = torch.tensor([float(T)], dtype=torch.float64, device=self.device)
+            self.comm.allreduce_sum(tg)
+            T_global = float(tg.item()) if self.comm.world_size > 1 else float(T)
+        inv_T = 1.0 / T_global
+        self.last_T, self.last_T_global = T, T_global
+
+        # a6-a11: forward + VPG (caches a0, a1, mu0, ll0)
+        _lib.check(L.mjrl_pack_params(sp, _lib.ptr(theta), _lib.ptr(self.packed_theta), 1, self.min_log_std, st),
+                   "mjrl_pack_params")
+        sc = self._scratch(T_vpg)
+        rows = self._rows(T_vpg, adv_vpg)
+        timing[0].record()
+        _lib.check(L.mjrl_policy_vpg(sp, C.byref(rows), _lib.ptr(self.packed_theta), _lib.ptr(osh), _lib.ptr(osc),
+                                     C.byref(sc), _lib.ptr(v["gsum"]), st), "mjrl_policy_vpg")
+        self.comm.allreduce_sum(v["gsum"])
+        _lib.check(L.mjrl_scale_vec(_lib.ptr(v["gsum"]), s.d, inv_T, _lib.ptr(v["g"]), st), "mjrl_scale_vec")
+        timing[1].record()
+
+        # a12-a13: conjugate gradient with the device FVP
+        rows_fvp = self._rows(T, adv_vpg)
+        sc_fvp = self._scratch(T) if T_vpg != T else sc
+        if algo == "vpg":
+            x = v["g"]
+            cg_iters_run = 0
+        else:
+            _lib.check(L.mjrl_cg_init(sp, _lib.ptr(v["g"]), _lib.ptr(v["x"]), _lib.ptr(v["r"]), _lib.ptr(v["p"]),
+                                      _lib.ptr(self.packed_p), _lib.ptr(self.cg), _lib.ptr(self.done), st),
+                       "mjrl_cg_init")
+            for _ in range(int(cg_iters)):
+                _lib.check(L.mjrl_policy_fvp(sp, C.byref(rows_fvp), T, _lib.ptr(self.packed_theta),
+                                             _lib.ptr(self.packed_p), _lib.ptr(osc), C.byref(sc_fvp),
+                                             _lib.ptr(self.done), _lib.ptr(v["gsum"]), st), "mjrl_policy_fvp")
+                self.comm.allreduce_sum(v["gsum"])
+                _lib.check(L.mjrl_cg_step(sp, _lib.ptr(v["gsum"]), inv_T, float(damping), _lib.ptr(self.packed_theta),
+                                          _lib.ptr(v["x"]), _lib.ptr(v["r"]), _lib.ptr(v["p"]), _lib.ptr(v["z"]),
+                                          _lib.ptr(self.packed_p), _lib.ptr(self.cg), _lib.ptr(self.done),
+                                          float(residual_tol), st), "mjrl_cg_step")
+            x = v["x"]
+            cg_iters_run = None
+        timing[2].record()
+
+        # a14: step size + update; a16 TRPO backtracking
+        def step(mode, delta, alpha_in, const):
+            _lib.check(L.mjrl_npg_step(sp, _lib.ptr(v["g"]), _lib.ptr(x), _lib.ptr(theta), mode, float(delta),
+                                       float(alpha_in), int(const), self.min_log_std, _lib.ptr(v["theta_new"]),
+                                       _lib.ptr(self.packed_new), _lib.ptr(self.out), st), "mjrl_npg_step")
+
+        def evaluate():
+            _lib.check(L.mjrl_policy_eval(sp, C.byref(rows_fvp), T, _lib.ptr(self.packed_new),
+                                          _lib.ptr(self.packed_theta), _lib.ptr(osh), _lib.ptr(osc),
+                                          C.byref(sc_fvp), C.c_void_p(self.stats[S_EVAL:].data_ptr()), st),
+                       "mjrl_policy_eval")
+            self.comm.allreduce_sum(self.stats[S_EVAL:S_EVAL + 2])
+
+        trials = []
+        if algo == "vpg":
+            step(1, 0.0, np.float32(learn_rate), 0)
+            delta = None
+        elif algo == "npg" and const_lr is not None:
+            step(1, 0.0, np.float32(const_lr), 1)
+            delta = None
+        elif algo == "npg":
+            delta = n_step_size if kl_dist is None else 2.0 * kl_dist
+            step(0, delta, 0.0, 0)
+        else:   # trpo / dapg: delta = 2 kl_dist
+            delta = 2.0 * kl_dist
+            step(0, delta, 0.0, 0)
+        evaluate()
+
+        if algo == "trpo":
+            res = self.stats[S_EVAL:S_EVAL + 2].cpu().numpy()
+            alpha = np.float32(self.out[0].item())
+            surr_before = float(self.stats[S_MS].item() / self.stats[S_MS + 2].item())
+            for k in range(100):
+                kl = np.float32(res[1] * inv_T)
+                surr = np.float32(res[0] * inv_T)
+                trials.append((float(alpha), float(kl), float(surr)))
+                if kl < kl_dist:
+                    break
+                alpha = np.float32(0.9 * alpha)   # trpo.py:114 (python float * np.float32)
+                if trpo_verbose:
+                    print("Step size too high. Backtracking. | kl = %f | surr diff = %f" % (kl, surr - surr_before))
+                if k == 99:
+                    alpha = np.float32(0.0)
+                    break
+                step(1, delta, alpha, 0)
+                evaluate()
+                res = self.stats[S_EVAL:S_EVAL + 2].cpu().numpy()
+            if float(alpha) != trials[-1][0]:   # final re-evaluation (trpo.py:120-123)
+                step(1, delta, alpha, 0)
+                evaluate()
+        timing[3].record()
+
+        # single readback
+        torch.cuda.current_stream().synchronize()
+        stats = self.stats.cpu().numpy()
+        out = self.out.cpu().numpy()
+        cg = self.cg.cpu().numpy()
+        n_p = stats[S_PM1 + 2]
+        base_stats = [stats[S_PM1] / n_p, math.sqrt(stats[S_PM2 + 1] / n_p), -stats[S_PM1 + 5], stats[S_PM1 + 4]]
+        result = dict(
+            alpha=float(out[0]),
+            gx=float(out[1]),
+            delta=(float(out[2]) if (const_lr is not None and algo == "npg") else delta),
+            surr_before=float(np.float32(stats[S_MS] / stats[S_MS + 2])),
+            surr_after=float(np.float32(stats[S_EVAL] * inv_T)),
+            kl_dist=float(np.float32(stats[S_EVAL + 1] * inv_T)),
+            base_stats=base_stats,
+            cg_iters=int(cg[1]) if algo != "vpg" else 0,
+            trials=trials,
+            time_vpg=timing[0].elapsed_time(timing[1]) / 1e3,
+            time_npg=timing[1].elapsed_time(timing[2]) / 1e3,
+            time_step=timing[2].elapsed_time(timing[3]) / 1e3,
+            T_global=T_global,
+        )
+        if algo == "vpg":
+            result["delta"] = None
+        return result
+
+    # ------------------------------------------------------------------
+    def fvp(self, v, damping=1e-4, T=None):
+        """F v + damping v at the parameters of the last update's forward pass
+        (the caches a0/a1/mu0 and packed_theta of that pass) — NPG.HVP
+        (npg_cg.py:55-74) as a standalone call, used by parity tests and
+        `NPG.HVP`.  `v`: f32 device tensor [d].  Returns a new device tensor."""
+        L = self.lib
+        s = self.shape
+        sp = C.byref(s)
+        self.st = st = _lib.stream_ptr()
+        T = self.last_T if T is None else T
+        vv = self.vec
+        scratch = self._scratch(T)
+        rows = self._rows(T, self.ws["adv32"])
+        _lib.check(L.mjrl_cg_init(sp, _lib.ptr(v), _lib.ptr(vv["x"]), _lib.ptr(vv["r"]), _lib.ptr(vv["p"]),
+                                  _lib.ptr(self.packed_p), _lib.ptr(self.cg), _lib.ptr(self.done), st), "mjrl_cg_init")
+        _lib.check(L.mjrl_policy_fvp(sp, C.byref(rows), T, _lib.ptr(self.packed_theta), _lib.ptr(self.packed_p),
+                                     _lib.ptr(self.transforms[3]), C.byref(scratch), _lib.ptr(self.done),
+                                     _lib.ptr(vv["gsum"]), st), "mjrl_policy_fvp")
+        self.comm.allreduce_sum(vv["gsum"])
+        T_global = self.last_T_global
+        _lib.check(L.mjrl_cg_step(sp, _lib.ptr(vv["gsum"]), 1.0 / T_global, float(damping),
+                                  _lib.ptr(self.packed_theta), _lib.ptr(vv["x"]), _lib.ptr(vv["r"]), _lib.ptr(vv["p"]),
+                                  _lib.ptr(vv["z"]), _lib.ptr(self.packed_p), _lib.ptr(self.cg), _lib.ptr(self.done),
+                                  0.0, st), "mjrl_cg_step")
+        return vv["z"].clone()

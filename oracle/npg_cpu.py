@@ -125,10 +125,14 @@ def param_shapes(n, m, hidden):
 
 
 class Policy:
-    """fp32 torch policy on the flat parameter vector (new + old copies)."""
+    """fp32 torch policy on the flat parameter vector (new + old copies).
 
-    def __init__(self, n, m, hidden, theta, transforms=None, min_log_std=-3.0):
+    dtype=torch.float64 gives the same computation in double precision: the
+    "truth" the parity tests measure the reference's own fp32 error against."""
+
+    def __init__(self, n, m, hidden, theta, transforms=None, min_log_std=-3.0, dtype=torch.float32):
         self.n, self.m = n, m
+        self.dtype = dtype
         self.shapes = param_shapes(n, m, hidden)
         self.sizes = [int(np.prod(s)) for s in self.shapes]
         self.d = sum(self.sizes)
@@ -138,13 +142,15 @@ class Policy:
         self.in_scale = torch.from_numpy(np.float32(tr[1])) if tr[1] is not None else torch.ones(n)
         self.out_shift = torch.from_numpy(np.float32(tr[2])) if tr[2] is not None else torch.zeros(m)
         self.out_scale = torch.from_numpy(np.float32(tr[3])) if tr[3] is not None else torch.ones(m)
+        self.in_shift, self.in_scale, self.out_shift, self.out_scale = (
+            t.to(dtype) for t in (self.in_shift, self.in_scale, self.out_shift, self.out_scale))
         self.new = self._tensors(theta, grad=True)
         self.old = self._tensors(theta, grad=False)
 
     def _tensors(self, theta, grad):
         out, i = [], 0
         for shp, sz in zip(self.shapes, self.sizes):
-            t = torch.from_numpy(np.asarray(theta[i:i + sz]).reshape(shp)).float()
+            t = torch.from_numpy(np.asarray(theta[i:i + sz]).reshape(shp)).to(self.dtype)
             out.append(t)
             i += sz
         out[-1] = torch.clamp(out[-1], self.min_log_std)   # gaussian_mlp.py:74-78
@@ -163,7 +169,7 @@ class Policy:
         return np.concatenate([t.detach().reshape(-1).numpy() for t in self.new]).copy()
 
     def mean(self, params, obs_f64):
-        x = torch.from_numpy(obs_f64).float()          # per-call f64->f32 (gaussian_mlp.py:103)
+        x = torch.from_numpy(obs_f64).to(self.dtype)   # per-call f64->f32 (gaussian_mlp.py:103)
         h = (x - self.in_shift) / (self.in_scale + 1e-8)
         if len(params) == 3:
             pre = torch.addmm(params[1], h, params[0].t())
@@ -176,7 +182,7 @@ class Policy:
 
     def mean_ll(self, params, obs, act):
         mu = self.mean(params, obs)
-        a = torch.from_numpy(act).float()
+        a = torch.from_numpy(act).to(self.dtype)
         s = params[-1]
         zs = (a - mu) / torch.exp(s)
         ll = -0.5 * torch.sum(zs ** 2, dim=1) - torch.sum(s) - 0.5 * self.m * LOG2PI
@@ -184,7 +190,7 @@ class Policy:
 
     def surrogate(self, obs, act, adv_f64):
         """CPI surrogate mean(exp(LL_new - LL_old) * adv) (batch_reinforce.py:37-43)."""
-        adv = torch.from_numpy(adv_f64).float()
+        adv = torch.from_numpy(adv_f64).to(self.dtype)
         _, ll_old = self.mean_ll(self.old, obs, act)
         _, ll_new = self.mean_ll(self.new, obs, act)
         return torch.mean(torch.exp(ll_new - ll_old) * adv)
@@ -204,7 +210,7 @@ class Policy:
 
     def fvp(self, obs, act, v, damping):
         """Hessian of mean KL times v by double backprop (npg_cg.py:55-74)."""
-        vt = torch.from_numpy(np.asarray(v)).float()
+        vt = torch.from_numpy(np.asarray(v)).to(self.dtype)
         g1 = torch.autograd.grad(self.kl(obs, act), self.new, create_graph=True)
         h = torch.sum(torch.cat([t.reshape(-1) for t in g1]) * vt)
         g2 = torch.autograd.grad(h, self.new)

@@ -134,10 +134,58 @@ def concat(paths, key):
     return np.concatenate([p[key] for p in paths])
 
 
-def run_case(name, *, n, m, hidden, lengths, terminated, algo, algo_kwargs,
-             gamma=0.995, gae_lambda=0.97, seed=123, policy_seed=0,
-             log_std=None, transforms=None, demo=None, linear=False,
-             baseline_fit=True):
+def run_case(name, **kw):
+    """Runs the reference at 1 torch thread (the fixture), again at 8 threads, and
+    again at 1 thread with the path order reversed (the same batch, every sum over
+    timesteps reordered).  The largest difference to the fixture (the reference's
+    own reduction-order sensitivity) is stored as spread_*
+    and calibrates the end-to-end tolerances of the GPU parity tests."""
+    torch.set_num_threads(8)
+    alt8 = _run(None, **kw)
+    torch.set_num_threads(1)
+    altr = _run(None, reverse=True, **kw)
+    out = _run(name, alt=[alt8, altr], **kw)
+    _err64(name, out)
+    return out
+
+
+def _err64(name, out):
+    """The reference's own error against an fp64 evaluation of the same update
+    (the oracle in float64 — oracle/npg_cpu.py, itself pinned to these fixtures):
+    err64_* bound how far ANY fp32 implementation may land from the reference."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(OUT)))
+    from oracle import npg_cpu as O
+    c = O.load_case(os.path.join(OUT, name + ".npz"))
+    pol = O.Policy(int(c["n"]), int(c["m"]), c["hidden_t"], c["theta0"], c["transforms"], dtype=torch.float64)
+    kw = O.case_kwargs(c)
+    for k in ("demo_obs", "demo_act"):
+        if k in kw:
+            kw[k] = kw[k].astype(np.float64)
+    r = O.update(pol, c["obs64"], c["act64"], c["advantages"], c["rewards"], c["lengths"], **kw)
+    rel = lambda a, b: abs(float(a) / float(b) - 1.0) if float(b) != 0 else abs(float(a))
+    z = dict(c)
+    for k in ("obs64", "act64", "hidden_t", "transforms"):
+        z.pop(k)
+    z["err64_x"] = _nrel(c["cg_x"], r["npg_grad"])
+    z["err64_theta"] = _nrel(c["theta1"], r["theta1"])
+    z["err64_alpha"] = rel(c["log_alpha"], r["alpha"])
+    z["err64_kl"] = rel(c["log_kl_dist"], r["kl_dist"])
+    z["err64_surr"] = rel(c["log_surr_improvement"], r["surr_after"] - r["surr_before"])
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), **z)
+    print("   err64 x %.1e theta %.1e alpha %.1e kl %.1e surr %.1e" % (
+        z["err64_x"], z["err64_theta"], z["err64_alpha"], z["err64_kl"], z["err64_surr"]))
+
+
+def _nrel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def _run(name, *, n, m, hidden, lengths, terminated, algo, algo_kwargs,
+         gamma=0.995, gae_lambda=0.97, seed=123, policy_seed=0,
+         log_std=None, transforms=None, demo=None, linear=False,
+         baseline_fit=True, alt=None, reverse=False):
     rs = np.random.RandomState(seed)
     spec = EnvSpec(n, m, max(lengths), 1)
     if linear:
@@ -156,6 +204,9 @@ def run_case(name, *, n, m, hidden, lengths, terminated, algo, algo_kwargs,
     if demo is not None:
         demo_paths = make_paths(rs, n, m, demo, [True] * len(demo))
 
+    if reverse:
+        paths = paths[::-1]
+        demo_paths = demo_paths[::-1] if demo_paths is not None else None
     baseline = LinearBaseline(spec)
     if baseline_fit:
         process_samples.compute_returns(paths, gamma)
@@ -190,6 +241,12 @@ def run_case(name, *, n, m, hidden, lengths, terminated, algo, algo_kwargs,
     keep = len(rec.cg["p"]) if policy.d <= 10000 else CG_KEEP
 
     out = dict(
+        spread_x=max(_nrel(a["cg_x"], rec.cg["x"]) for a in alt) if alt else 0.0,
+        spread_theta=max(_nrel(a["theta1"], theta1) for a in alt) if alt else 0.0,
+        spread_kl=max(abs(a["log_kl_dist"] / agent.logger.log["kl_dist"][-1] - 1) for a in alt) if alt else 0.0,
+        spread_alpha=max(abs(a["log_alpha"] / agent.logger.log["alpha"][-1] - 1) for a in alt) if alt else 0.0,
+        spread_surr=max(abs(a["log_surr_improvement"] / agent.logger.log["surr_improvement"][-1] - 1)
+                        for a in alt) if alt else 0.0,
         n=n, m=m, hidden=np.array(hidden if not linear else (0, 0)), linear=int(linear),
         algo=algo, gamma=gamma, gae_lambda=(np.nan if gae_lambda is None else gae_lambda),
         lengths=np.array(lengths, dtype=np.int64),
@@ -227,9 +284,12 @@ def run_case(name, *, n, m, hidden, lengths, terminated, algo, algo_kwargs,
         out["demo_obs"] = concat(demo_paths, "observations").astype(np.float32)
         out["demo_act"] = concat(demo_paths, "actions").astype(np.float32)
         out["demo_iter_count"] = agent.iter_count
+    if name is None:
+        return out
     np.savez_compressed(os.path.join(OUT, name + ".npz"), **out)
-    print("%-22s T=%-6d d=%-6d surr=%s kl=%s alpha=%.6g" % (
-        name, obs.shape[0], policy.d, rec.surr[:2], rec.kl[-1:], out.get("log_alpha", np.nan)))
+    print("%-22s T=%-6d d=%-6d kl=%s alpha=%.6g spread x %.1e kl %.1e" % (
+        name, obs.shape[0], policy.d, rec.kl[-1:], out.get("log_alpha", np.nan), out["spread_x"],
+        out["spread_kl"]))
     return out
 
 

@@ -1,0 +1,214 @@
+"""Benchmark: NPG update throughput (timesteps/s) on the Humanoid 1M-step batch.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (BASELINE.json configs[3]): obs 376, act 17, MLP(64,64),
+NPG with 10 CG iterations, damping 1e-4, delta 0.01, gamma 0.995, lambda 0.97;
+1000 paths x 1000 steps = 1,000,000 timesteps per update, split by paths over
+the N ranks (strong scaling: the batch is fixed).  Synthetic data: obs / act /
+rewards ~ N(0,1) from a per-path seeded generator; LinearBaseline fitted once on
+20 paths and frozen.  A step = one full update from the device-resident f64
+paths: batch assembly, GAE, whitening, forward + VPG, 10 Fisher-vector products
++ CG, step, post-step surrogate / KL, host readback of the statistics.
+
+Rank 0 prints one JSON line.  `roofline` is measured live with HIP events on the
+stream the kernels run on, `cpu_baseline` times the oracle (the CPU restatement
+of the reference update, oracle/npg_cpu.py) on a bounded sample on this host.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "NPG train_step timesteps/sec, Humanoid 1M-step batch @ 1/2/4/8 MI355X"
+N_OBS, N_ACT, HIDDEN = 376, 17, (64, 64)
+N_PATHS, HORIZON = 1000, 1000
+GAMMA, LAM, DELTA, CG_ITERS, DAMPING = 0.995, 0.97, 0.01, 10, 1e-4
+PEAK_F32_MFMA = 157.3   # TFLOP/s, MI355X dense fp32 matrix (MI355X_MICROARCH.md)
+PEAK_HBM = 8000.0       # GB/s
+
+
+def flops_per_row(n, m, h0, h1):
+    """Algorithmic FLOPs per timestep, split by kernel."""
+    jvp = 2 * (n * h0) + 4 * (h0 * h1) + 4 * (h1 * m)
+    vjp_act = 2 * (h1 * m) + 2 * (h0 * h1)
+    wgrad = 2 * (n * h0) + 2 * (h0 * h1) + 2 * (h1 * m)
+    return dict(rows_fvp=jvp + vjp_act, weight_grads=wgrad)
+
+
+def make_paths(p0, p1, seed=123):
+    """Paths p0..p1-1 of the synthetic batch, each from its own seeded stream
+    (so a rank generates only its shard and N does not change the data)."""
+    obs, act, rew = [], [], []
+    for p in range(p0, p1):
+        g = np.random.Generator(np.random.PCG64(seed * 100003 + p))
+        obs.append(g.standard_normal((HORIZON, N_OBS), dtype=np.float32))
+        act.append(g.standard_normal((HORIZON, N_ACT), dtype=np.float32))
+        rew.append(g.standard_normal(HORIZON))
+    return obs, act, rew
+
+
+def baseline_coeffs():
+    from mjrl_amd.utils.gym_env import EnvSpec
+    from mjrl_amd.baselines.linear_baseline import LinearBaseline
+    obs, _, rew = make_paths(0, 20)
+    paths = []
+    for o, r in zip(obs, rew):
+        ret = np.zeros_like(r)
+        acc = 0.0
+        for t in range(len(r) - 1, -1, -1):
+            acc = r[t] + GAMMA * acc
+            ret[t] = acc
+        paths.append(dict(observations=o.astype(np.float64), rewards=r, returns=ret))
+    b = LinearBaseline(EnvSpec(N_OBS, N_ACT, HORIZON, 1))
+    b.fit(paths)
+    return b
+
+
+def stage_shard(p0, p1, device, base):
+    from mjrl_amd.engine import DeviceBatch
+    obs, act, rew = make_paths(p0, p1)
+    P = p1 - p0
+    T = P * HORIZON
+    ho = torch.empty((T, N_OBS), dtype=torch.float64, pin_memory=True)
+    np.concatenate(obs, out=ho.numpy())
+    ha = torch.empty((T, N_ACT), dtype=torch.float64, pin_memory=True)
+    np.concatenate(act, out=ha.numpy())
+    rw = np.concatenate(rew)
+    bl = np.concatenate([base.predict(dict(observations=o.astype(np.float64), rewards=r)) for o, r in zip(obs, rew)])
+    off = (np.arange(P + 1, dtype=np.int64) * HORIZON)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)
+    return DeviceBatch(ho.to(device), ha.to(device), t(rw), t(bl), t(off), t(np.zeros(P, np.uint8)))
+
+
+def cpu_baseline(rows, base):
+    """The oracle (CPU restatement of the reference update) on `rows` timesteps."""
+    from oracle import npg_cpu as O
+    P = rows // HORIZON
+    obs, act, rew = make_paths(0, P)
+    obs = np.concatenate(obs).astype(np.float64)
+    act = np.concatenate(act).astype(np.float64)
+    rew = np.concatenate(rew)
+    lengths = np.full(P, HORIZON)
+    bl = np.concatenate([base.predict(dict(observations=o, rewards=r))
+                         for o, r in zip(O.split(obs, lengths), O.split(rew, lengths))])
+    torch.manual_seed(0)
+    theta = np.concatenate([(np.random.RandomState(1).randn(int(np.prod(s))) * 0.05).ravel()
+                            for s in O.param_shapes(N_OBS, N_ACT, HIDDEN)]).astype(np.float32)
+    theta[-N_ACT:] = 0.0
+    pol = O.Policy(N_OBS, N_ACT, HIDDEN, theta.astype(np.float64), None)
+    t0 = time.perf_counter()
+    ret, adv = O.returns_and_advantages(rew, bl, lengths, np.zeros(P, bool), GAMMA, LAM)
+    O.update(pol, obs, act, adv, rew, lengths, algo="npg", n_step_size=DELTA, cg_iters=CG_ITERS, damping=DAMPING)
+    dt = time.perf_counter() - t0
+    return dict(value=rows / dt, unit="timesteps/s", cores=torch.get_num_threads(), kind="port",
+                sample="%d paths x %d steps (%d timesteps) of the same Humanoid-shape workload, one update "
+                       "(returns + GAE + train_from_paths), oracle/npg_cpu.py on %d torch threads: %.2f s"
+                       % (P, HORIZON, rows, torch.get_num_threads(), dt))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--paths", type=int, default=N_PATHS)
+    ap.add_argument("--cpu-rows", type=int, default=100000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    comm = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=device)
+        from mjrl_amd.comm import DistComm
+        comm = DistComm()
+    from mjrl_amd.comm import partition_paths
+    from mjrl_amd.engine import UpdateEngine
+
+    base = baseline_coeffs()
+    p0, p1 = partition_paths(np.full(args.paths, HORIZON), world)[rank]
+    batch = stage_shard(p0, p1, device, base)
+    T_total = args.paths * HORIZON
+
+    eng = UpdateEngine(N_OBS, N_ACT, HIDDEN, device=device, comm=comm)
+    rs = np.random.RandomState(0)
+    theta = np.concatenate([(rs.randn(int(np.prod(s))) * 0.05).ravel()
+                            for s in [(HIDDEN[0], N_OBS), (HIDDEN[0],), (HIDDEN[1], HIDDEN[0]), (HIDDEN[1],),
+                                      (N_ACT, HIDDEN[1]), (N_ACT,), (N_ACT,)]]).astype(np.float32)
+    theta[-N_ACT:] = 0.0
+    th = torch.from_numpy(theta).to(device)
+    upd = dict(algo="npg", gamma=GAMMA, gae_lambda=LAM, n_step_size=DELTA, cg_iters=CG_ITERS, damping=DAMPING,
+               T_global=float(T_total))
+
+    def step():
+        nonlocal th
+        eng.update(batch, th, **upd)
+        th = eng.vec["theta_new"].clone()
+
+    for _ in range(args.warmup):
+        step()
+    eng.kernel_timing = []
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # dominant-kernel roofline from the live events of the timed region
+    ev = eng.kernel_timing
+    t_rows = np.mean([a.elapsed_time(b) for a, b, _ in ev]) / 1e3
+    t_grad = np.mean([b.elapsed_time(c) for _, b, c in ev]) / 1e3
+    fl = flops_per_row(N_OBS, N_ACT, *HIDDEN)
+    rows_rank = batch.T
+    kern = {"rows_fvp": dict(avg_ms=t_rows * 1e3, tflops=fl["rows_fvp"] * rows_rank / t_rows / 1e12),
+            "weight_grads": dict(avg_ms=t_grad * 1e3, tflops=fl["weight_grads"] * rows_rank / t_grad / 1e12)}
+    dom = max(kern, key=lambda k: kern[k]["avg_ms"])
+    roof = dict(bound="mfma", kernel="k_rows<64,64,32,FVP>" if dom == "rows_fvp" else "k_wgrad",
+                achieved=round(kern[dom]["tflops"], 3), peak=PEAK_F32_MFMA, unit="TFLOP/s",
+                frac=round(kern[dom]["tflops"] / PEAK_F32_MFMA, 4), traffic=None,
+                flops_per_timestep=fl[dom], rows_per_launch=rows_rank, launches=len(ev),
+                kernels={k: {kk: round(vv, 4) for kk, vv in v.items()} for k, v in kern.items()})
+
+    if rank == 0:
+        ms = elapsed / args.steps * 1e3
+        out = dict(metric=METRIC, value=round(T_total * args.steps / elapsed, 1), unit="timesteps/s",
+                   n_gpus=world, steps=args.steps, warmup=args.warmup, ms_per_step=round(ms, 3),
+                   higher_is_better=True, scaling="strong", vs_baseline=None, dtype="f32",
+                   data="synthetic (seeded N(0,1) obs/act/rewards, LinearBaseline fitted on 20 paths)",
+                   config=dict(workload="humanoid_npg_1M", obs_dim=N_OBS, act_dim=N_ACT, hidden=list(HIDDEN),
+                               timesteps=T_total, paths=args.paths, horizon=HORIZON, cg_iters=CG_ITERS,
+                               parallelism="dp%d" % world),
+                   roofline=roof)
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_rows, base)
+        print(json.dumps(out))
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

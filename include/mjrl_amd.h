@@ -151,6 +151,20 @@ int mjrl_policy_eval(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_eval,
                      const float* out_shift, const float* out_scale,
                      const mjrl_scratch* sc, double* sums, void* stream);
 
+/* The three launches behind the composites above, for callers that time or
+ * overlap them separately: the per-row chain (rows_*) writes gu0/gu1/gp (and the
+ * caches / log-std partials for vpg); weight_grads reduces them into gsum
+ * (with_log_std = 1 after rows_vpg). */
+int mjrl_rows_vpg(const mjrl_shape* s, const mjrl_rows* rows, const float* packed_theta,
+                  const float* out_shift, const float* out_scale, const mjrl_scratch* sc,
+                  void* stream);
+int mjrl_rows_fvp(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_fvp,
+                  const float* packed_theta, const float* packed_v, const float* out_scale,
+                  const int32_t* done, void* stream);
+int mjrl_weight_grads(const mjrl_shape* s, const mjrl_rows* rows, int64_t T,
+                      const mjrl_scratch* sc, int32_t with_log_std, const int32_t* done,
+                      float* gsum, void* stream);
+
 /* ---- conjugate gradient on device (cg_solve.py:3-22) ----
  * State cg[8] (f32 scalars, device): [rdotr, v, mu, pz, done_flag(as int bits), iters, ...].
  * init: x = 0, r = b, p = b, rdotr = b.b; packs p into packed_p.

@@ -56,6 +56,9 @@ SIGNATURES = {
     "mjrl_policy_vpg": [SP, C.POINTER(Rows), P, P, P, C.POINTER(Scratch), P, P],
     "mjrl_policy_fvp": [SP, C.POINTER(Rows), I64, P, P, P, C.POINTER(Scratch), P, P, P],
     "mjrl_policy_eval": [SP, C.POINTER(Rows), I64, P, P, P, P, C.POINTER(Scratch), P, P],
+    "mjrl_rows_vpg": [SP, C.POINTER(Rows), P, P, P, C.POINTER(Scratch), P],
+    "mjrl_rows_fvp": [SP, C.POINTER(Rows), I64, P, P, P, P, P],
+    "mjrl_weight_grads": [SP, C.POINTER(Rows), I64, C.POINTER(Scratch), I32, P, P, P],
     "mjrl_cg_init": [SP, P, P, P, P, P, P, P, P],
     "mjrl_cg_step": [SP, P, F64, F32, P, P, P, P, P, P, P, P, F32, P],
     "mjrl_scale_vec": [P, I32, F64, P, P],

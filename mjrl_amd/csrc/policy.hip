@@ -783,10 +783,9 @@ int mjrl_scratch_size(const mjrl_shape* s, int64_t T, int64_t* wpart_floats, int
     return MJRL_OK;
 }
 
-int mjrl_policy_vpg(const mjrl_shape* s, const mjrl_rows* rows, const float* packed_theta, const float* out_shift,
-                    const float* out_scale, const mjrl_scratch* sc, float* gsum, void* stream) {
-    if (!rows_ok(s, rows) || !packed_theta || !sc || !gsum || !rows->act || !rows->adv_vpg || !rows->mu0 ||
-        !rows->ll0)
+int mjrl_rows_vpg(const mjrl_shape* s, const mjrl_rows* rows, const float* packed_theta, const float* out_shift,
+                  const float* out_scale, const mjrl_scratch* sc, void* stream) {
+    if (!rows_ok(s, rows) || !packed_theta || !sc || !rows->act || !rows->adv_vpg || !rows->mu0 || !rows->ll0)
         return MJRL_EINVAL;
     if (!shape_supported(s->h0, s->h1, s->mp)) return MJRL_ESHAPE;
     hipStream_t st = (hipStream_t)stream;
@@ -796,29 +795,46 @@ int mjrl_policy_vpg(const mjrl_shape* s, const mjrl_rows* rows, const float* pac
     ra.out_scale = out_scale;
     ra.rpart = sc->rpart;
     const int G = row_grid(s, rows->T);
-    int e = MJRL_OK;
-    if (rows->T > 0) e = launch_rows<FWD>(s, ra, G, st);
-    else hipMemsetAsync(sc->rpart, 0, sizeof(double) * G * s->mp, st);
-    if (e) return e;
-    return run_wgrad_gather(s, rows, rows->T, sc, sc->rpart, G, nullptr, gsum, st);
+    if (rows->T > 0) return launch_rows<FWD>(s, ra, G, st);
+    hipMemsetAsync(sc->rpart, 0, sizeof(double) * G * s->mp, st);
+    return (int)hipGetLastError();
 }
 
-int mjrl_policy_fvp(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_fvp, const float* packed_theta,
-                    const float* packed_v, const float* out_scale, const mjrl_scratch* sc, const int32_t* done,
-                    float* gsum, void* stream) {
-    if (!rows_ok(s, rows) || !packed_theta || !packed_v || !sc || !gsum || T_fvp < 0 || T_fvp > rows->T)
-        return MJRL_EINVAL;
+int mjrl_rows_fvp(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_fvp, const float* packed_theta,
+                  const float* packed_v, const float* out_scale, const int32_t* done, void* stream) {
+    if (!rows_ok(s, rows) || !packed_theta || !packed_v || T_fvp < 0 || T_fvp > rows->T) return MJRL_EINVAL;
     if (!shape_supported(s->h0, s->h1, s->mp)) return MJRL_ESHAPE;
-    hipStream_t st = (hipStream_t)stream;
     RowArgs ra = row_args(s, rows, T_fvp);
     ra.P = packed_theta;
     ra.V = packed_v;
     ra.out_scale = out_scale;
     ra.done = done;
-    int e = MJRL_OK;
-    if (T_fvp > 0) e = launch_rows<FVP>(s, ra, row_grid(s, T_fvp), st);
+    if (T_fvp > 0) return launch_rows<FVP>(s, ra, row_grid(s, T_fvp), (hipStream_t)stream);
+    return MJRL_OK;
+}
+
+int mjrl_weight_grads(const mjrl_shape* s, const mjrl_rows* rows, int64_t T, const mjrl_scratch* sc,
+                      int32_t with_log_std, const int32_t* done, float* gsum, void* stream) {
+    if (!rows_ok(s, rows) || !sc || !gsum || T < 0 || T > rows->T) return MJRL_EINVAL;
+    if (!shape_supported(s->h0, s->h1, s->mp)) return MJRL_ESHAPE;
+    return run_wgrad_gather(s, rows, T, sc, with_log_std ? sc->rpart : nullptr, row_grid(s, T), done, gsum,
+                            (hipStream_t)stream);
+}
+
+int mjrl_policy_vpg(const mjrl_shape* s, const mjrl_rows* rows, const float* packed_theta, const float* out_shift,
+                    const float* out_scale, const mjrl_scratch* sc, float* gsum, void* stream) {
+    int e = mjrl_rows_vpg(s, rows, packed_theta, out_shift, out_scale, sc, stream);
     if (e) return e;
-    return run_wgrad_gather(s, rows, T_fvp, sc, nullptr, 0, done, gsum, st);
+    return mjrl_weight_grads(s, rows, rows->T, sc, 1, nullptr, gsum, stream);
+}
+
+int mjrl_policy_fvp(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_fvp, const float* packed_theta,
+                    const float* packed_v, const float* out_scale, const mjrl_scratch* sc, const int32_t* done,
+                    float* gsum, void* stream) {
+    if (!sc || !gsum) return MJRL_EINVAL;
+    int e = mjrl_rows_fvp(s, rows, T_fvp, packed_theta, packed_v, out_scale, done, stream);
+    if (e) return e;
+    return mjrl_weight_grads(s, rows, T_fvp, sc, 0, done, gsum, stream);
 }
 
 int mjrl_policy_eval(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_eval, const float* packed_theta_new,

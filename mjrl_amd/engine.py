@@ -107,6 +107,7 @@ class UpdateEngine:
         self.stats = torch.zeros(N_STATS, dtype=torch.float64, device=dev)
         self.mom_part = torch.zeros(4 * 256 + 16, dtype=torch.float64, device=dev)
         self.transforms = (None, None, None, None)
+        self.kernel_timing = None   # list -> (start, rows done, grads done) events per FVP
 
     # ------------------------------------------------------------------
     def set_transformations(self, in_shift=None, in_scale=None, out_shift=None, out_scale=None):
@@ -300,10 +301,21 @@ class UpdateEngine:
             _lib.check(L.mjrl_cg_init(sp, _lib.ptr(v["g"]), _lib.ptr(v["x"]), _lib.ptr(v["r"]), _lib.ptr(v["p"]),
                                       _lib.ptr(self.packed_p), _lib.ptr(self.cg), _lib.ptr(self.done), st),
                        "mjrl_cg_init")
+            prof = self.kernel_timing
             for _ in range(int(cg_iters)):
-                _lib.check(L.mjrl_policy_fvp(sp, C.byref(rows_fvp), T, _lib.ptr(self.packed_theta),
-                                             _lib.ptr(self.packed_p), _lib.ptr(osc), C.byref(sc_fvp),
-                                             _lib.ptr(self.done), _lib.ptr(v["gsum"]), st), "mjrl_policy_fvp")
+                if prof is not None:
+                    e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+                    e0.record()
+                _lib.check(L.mjrl_rows_fvp(sp, C.byref(rows_fvp), T, _lib.ptr(self.packed_theta),
+                                           _lib.ptr(self.packed_p), _lib.ptr(osc), _lib.ptr(self.done), st),
+                           "mjrl_rows_fvp")
+                if prof is not None:
+                    e1.record()
+                _lib.check(L.mjrl_weight_grads(sp, C.byref(rows_fvp), T, C.byref(sc_fvp), 0, _lib.ptr(self.done),
+                                               _lib.ptr(v["gsum"]), st), "mjrl_weight_grads")
+                if prof is not None:
+                    e2.record()
+                    prof.append((e0, e1, e2))
                 self.comm.allreduce_sum(v["gsum"])
                 _lib.check(L.mjrl_cg_step(sp, _lib.ptr(v["gsum"]), inv_T, float(damping), _lib.ptr(self.packed_theta),
                                           _lib.ptr(v["x"]), _lib.ptr(v["r"]), _lib.ptr(v["p"]), _lib.ptr(v["z"]),

@@ -177,6 +177,14 @@ int mjrl_cg_step(const mjrl_shape* s, const float* gsum, double inv_T, float dam
                  float* packed_p, float* cg, int32_t* done, float residual_tol,
                  void* stream);
 
+/* Generic CG (cg_solve.py:3-22 with a caller-supplied operator): init from b,
+ * then one update per z = A p the caller computed.  Same scalar arithmetic and
+ * residual_tol break as mjrl_cg_step. */
+int mjrl_cg_init_vec(int32_t d, const float* b, float* x, float* r, float* p, float* cg,
+                     int32_t* done, void* stream);
+int mjrl_cg_update(int32_t d, const float* z, float* x, float* r, float* p, float* cg,
+                   int32_t* done, float residual_tol, void* stream);
+
 /* g[d] = gsum * scale  (VPG normalisation: 1/T, DAPG: 1/T_rl, dapg.py:97-98) */
 int mjrl_scale_vec(const float* gsum, int32_t d, double scale, float* g, void* stream);
 

@@ -61,6 +61,8 @@ SIGNATURES = {
     "mjrl_weight_grads": [SP, C.POINTER(Rows), I64, C.POINTER(Scratch), I32, P, P, P],
     "mjrl_cg_init": [SP, P, P, P, P, P, P, P, P],
     "mjrl_cg_step": [SP, P, F64, F32, P, P, P, P, P, P, P, P, F32, P],
+    "mjrl_cg_init_vec": [I32, P, P, P, P, P, P, P],
+    "mjrl_cg_update": [I32, P, P, P, P, P, P, F32, P],
     "mjrl_scale_vec": [P, I32, F64, P, P],
     "mjrl_npg_step": [SP, P, P, P, I32, F32, F32, I32, F32, P, P, P, P],
 }

@@ -1,0 +1,65 @@
+"""Natural policy gradient (API of mjrl/algos/npg_cg.py:24-165) on the gfx950
+engine: VPG, 10 device Fisher-vector products inside a device-side CG, the
+normalised step and the post-step surrogate / KL, one host readback."""
+import numpy as np
+import torch
+
+from .batch_reinforce import BatchREINFORCE
+from ..utils.logger import DataLog
+
+
+class NPG(BatchREINFORCE):
+    algo = "npg"
+
+    def __init__(self, env, policy, baseline, normalized_step_size=0.01, const_learn_rate=None,
+                 FIM_invert_args={"iters": 10, "damping": 1e-4}, hvp_sample_frac=1.0, seed=None,
+                 save_logs=False, kl_dist=None, device=None, comm=None):
+        self.env = env
+        self.policy = policy
+        self.baseline = baseline
+        self.alpha = const_learn_rate
+        self.n_step_size = normalized_step_size if kl_dist is None else 2.0 * kl_dist
+        self.seed = seed
+        self.save_logs = save_logs
+        self.FIM_invert_args = FIM_invert_args
+        self.hvp_subsample = hvp_sample_frac
+        self.running_score = None
+        if save_logs:
+            self.logger = DataLog()
+        self._device = device
+        self._comm = comm
+        self._engine = None
+
+    def _check_subsample(self):
+        if self.hvp_subsample is not None and self.hvp_subsample < 0.99:
+            raise NotImplementedError("hvp_sample_frac < 0.99 (npg_cg.py:58-62) is not implemented on the "
+                                      "device path yet; use the full batch (the reference default)")
+
+    def HVP(self, observations, actions, vector, regu_coef=None):
+        """F v + damping v at the current (old == new) parameters (npg_cg.py:55-74)."""
+        self._check_subsample()
+        regu_coef = self.FIM_invert_args["damping"] if regu_coef is None else regu_coef
+        eng = self.engine()
+        T = eng.load_rows(observations, actions)
+        eng.forward_pass(self._theta(), T)
+        v = torch.from_numpy(np.ascontiguousarray(vector, dtype=np.float32)).to(eng.device)
+        return eng.fvp(v, damping=float(regu_coef), T=T).cpu().numpy()
+
+    def build_Hvp_eval(self, inputs, regu_coef=None):
+        def eval(v):
+            return self.HVP(*(list(inputs) + [v, regu_coef]))
+        return eval
+
+    def _update_args(self):
+        self._check_subsample()
+        return dict(algo="npg", n_step_size=self.n_step_size, const_lr=self.alpha,
+                    cg_iters=self.FIM_invert_args["iters"], damping=self.FIM_invert_args["damping"])
+
+    def _log_update(self, res):
+        self.logger.log_kv("alpha", res["alpha"])
+        self.logger.log_kv("delta", res["delta"])
+        self.logger.log_kv("time_vpg", res["time_vpg"])
+        self.logger.log_kv("time_npg", res["time_npg"])
+        self.logger.log_kv("kl_dist", res["kl_dist"])
+        self.logger.log_kv("surr_improvement", res["surr_after"] - res["surr_before"])
+        self.logger.log_kv("running_score", self.running_score)

@@ -188,6 +188,60 @@ __global__ void __launch_bounds__(CG_THREADS) k_npg_step(mjrl_shape s, const flo
     }
 }
 
+// Generic CG for an arbitrary operator (the f_Ax of cg_solve.py:3): init and
+// the update given z = A p computed by the caller.
+__global__ void __launch_bounds__(CG_THREADS) k_cg_init_vec(int d, const float* __restrict__ b, float* __restrict__ x,
+                                                            float* __restrict__ r, float* __restrict__ p,
+                                                            float* __restrict__ cg, int32_t* __restrict__ done) {
+    __shared__ double red[CG_THREADS / 64];
+    double acc = 0.0;
+    for (int f = threadIdx.x; f < d; f += CG_THREADS) {
+        const float v = b[f];
+        x[f] = 0.f;
+        r[f] = v;
+        p[f] = v;
+        acc += (double)v * (double)v;
+    }
+    const double rr = block_sum1024(acc, red);
+    if (threadIdx.x == 0) {
+        cg[0] = (float)rr;
+        cg[1] = 0.f;
+        *done = 0;
+    }
+}
+
+__global__ void __launch_bounds__(CG_THREADS) k_cg_update(int d, const float* __restrict__ z, float* __restrict__ x,
+                                                          float* __restrict__ r, float* __restrict__ p,
+                                                          float* __restrict__ cg, int32_t* __restrict__ done,
+                                                          float tol) {
+    __shared__ double red[CG_THREADS / 64];
+    if (*done) return;
+    double acc = 0.0;
+    for (int f = threadIdx.x; f < d; f += CG_THREADS) acc += (double)p[f] * (double)z[f];
+    const float pz = (float)block_sum1024(acc, red);
+    const float rdotr = cg[0];
+    const float v = rdotr / pz;
+    acc = 0.0;
+    for (int f = threadIdx.x; f < d; f += CG_THREADS) {
+        x[f] = __fadd_rn(x[f], __fmul_rn(v, p[f]));
+        const float rf = __fsub_rn(r[f], __fmul_rn(v, z[f]));
+        r[f] = rf;
+        acc += (double)rf * (double)rf;
+    }
+    const float rr = (float)block_sum1024(acc, red);
+    const float mu = rr / rdotr;
+    for (int f = threadIdx.x; f < d; f += CG_THREADS) p[f] = __fadd_rn(r[f], __fmul_rn(mu, p[f]));
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        cg[0] = rr;
+        cg[1] += 1.f;
+        cg[2] = v;
+        cg[3] = mu;
+        cg[4] = pz;
+        if (rr < tol) *done = 1;
+    }
+}
+
 inline int err(hipError_t e) { return e == hipSuccess ? MJRL_OK : (int)e; }
 
 }  // namespace
@@ -216,6 +270,21 @@ int mjrl_cg_step(const mjrl_shape* s, const float* gsum, double inv_T, float dam
     if (!s || !gsum || !packed_theta || !x || !r || !p || !z || !packed_p || !cg || !done) return MJRL_EINVAL;
     hipLaunchKernelGGL(k_cg_step, dim3(1), dim3(CG_THREADS), 0, (hipStream_t)stream, *s, gsum, inv_T, damping,
                        packed_theta, x, r, p, z, packed_p, cg, done, residual_tol);
+    return err(hipGetLastError());
+}
+
+int mjrl_cg_init_vec(int32_t d, const float* b, float* x, float* r, float* p, float* cg, int32_t* done,
+                     void* stream) {
+    if (d < 0 || !b || !x || !r || !p || !cg || !done) return MJRL_EINVAL;
+    hipLaunchKernelGGL(k_cg_init_vec, dim3(1), dim3(CG_THREADS), 0, (hipStream_t)stream, d, b, x, r, p, cg, done);
+    return err(hipGetLastError());
+}
+
+int mjrl_cg_update(int32_t d, const float* z, float* x, float* r, float* p, float* cg, int32_t* done,
+                   float residual_tol, void* stream) {
+    if (d < 0 || !z || !x || !r || !p || !cg || !done) return MJRL_EINVAL;
+    hipLaunchKernelGGL(k_cg_update, dim3(1), dim3(CG_THREADS), 0, (hipStream_t)stream, d, z, x, r, p, cg, done,
+                       residual_tol);
     return err(hipGetLastError());
 }
 

@@ -429,3 +429,99 @@ class UpdateEngine:
                                   _lib.ptr(vv["z"]), _lib.ptr(self.packed_p), _lib.ptr(self.cg), _lib.ptr(self.done),
                                   0.0, st), "mjrl_cg_step")
         return vv["z"].clone()
+
+    # ------------------------------------------------------------------
+    # standalone passes on explicit arrays (the reference's CPI_surrogate /
+    # kl_old_new / flat_vpg / HVP called directly, batch_reinforce.py:37-55,
+    # npg_cg.py:55-74); the update above never goes through these.  Local to
+    # this process (no collectives).
+    def load_rows(self, obs, act, adv=None):
+        """Stages f64 obs / act (and f64 advantages, cast to f32 as
+        batch_reinforce.py:38 does) as the current rows."""
+        T = int(obs.shape[0])
+        self._ensure(T, 1)
+        self.st = st = _lib.stream_ptr()
+        dev = self.device
+        o = torch.from_numpy(np.ascontiguousarray(obs, dtype=np.float64)).to(dev)
+        a = torch.from_numpy(np.ascontiguousarray(act, dtype=np.float64)).to(dev)
+        ins, isc, _, _ = self.transforms
+        _lib.check(self.lib.mjrl_pack_batch(_lib.ptr(o), _lib.ptr(a), T, C.byref(self.shape), _lib.ptr(ins),
+                                            _lib.ptr(isc), _lib.ptr(self.ws["xhat"]), _lib.ptr(self.ws["act32"]), st),
+                   "mjrl_pack_batch")
+        if adv is not None:
+            self.ws["adv32"][:T].copy_(torch.from_numpy(np.asarray(adv, dtype=np.float64)).float().to(dev))
+        else:
+            self.ws["adv32"][:T].zero_()
+        return T
+
+    def forward_pass(self, theta, T):
+        """Forward + VPG sums at theta over the loaded rows; fills the caches.
+        Returns the flat VPG mean (device) = sum / T."""
+        L, s = self.lib, self.shape
+        sp = C.byref(s)
+        self.st = st = _lib.stream_ptr()
+        _lib.check(L.mjrl_pack_params(sp, _lib.ptr(theta), _lib.ptr(self.packed_theta), 1, self.min_log_std, st),
+                   "mjrl_pack_params")
+        rows = self._rows(T, self.ws["adv32"])
+        sc = self._scratch(T)
+        _, _, osh, osc = self.transforms
+        _lib.check(L.mjrl_policy_vpg(sp, C.byref(rows), _lib.ptr(self.packed_theta), _lib.ptr(osh), _lib.ptr(osc),
+                                     C.byref(sc), _lib.ptr(self.vec["gsum"]), st), "mjrl_policy_vpg")
+        tg = float(T)
+        self.last_T, self.last_T_global = T, tg
+        _lib.check(L.mjrl_scale_vec(_lib.ptr(self.vec["gsum"]), s.d, 1.0 / tg, _lib.ptr(self.vec["g"]), st),
+                   "mjrl_scale_vec")
+        return self.vec["g"]
+
+    def eval_pass(self, theta_new, T):
+        """(surrogate, KL) at theta_new against the caches of the last forward_pass."""
+        L, s = self.lib, self.shape
+        sp = C.byref(s)
+        self.st = st = _lib.stream_ptr()
+        _lib.check(L.mjrl_pack_params(sp, _lib.ptr(theta_new), _lib.ptr(self.packed_new), 1, self.min_log_std, st),
+                   "mjrl_pack_params")
+        rows = self._rows(T, self.ws["adv32"])
+        sc = self._scratch(T)
+        _, _, osh, osc = self.transforms
+        _lib.check(L.mjrl_policy_eval(sp, C.byref(rows), T, _lib.ptr(self.packed_new), _lib.ptr(self.packed_theta),
+                                      _lib.ptr(osh), _lib.ptr(osc), C.byref(sc),
+                                      C.c_void_p(self.stats[S_EVAL:].data_ptr()), st), "mjrl_policy_eval")
+        res = self.stats[S_EVAL:S_EVAL + 2].cpu().numpy()
+        return np.float32(res[0] / T), np.float32(res[1] / T)
+
+
+def device_returns_advantages(rewards, baseline, lengths, terminated, gamma, gae_lambda, device=None,
+                              normalize=False):
+    """compute_returns / compute_advantages (process_samples.py:3-35) on the GPU for
+    host arrays; returns f64 numpy (returns, advantages), bit-identical to the
+    reference's discount_sum order.  normalize: (adv - mean) / (std + 1e-8) over
+    all paths (process_samples.py:14-19, 30-35), two-pass fp64 moments."""
+    L = _lib.lib()
+    dev = torch.device(device if device is not None else "cuda")
+    lengths = np.asarray(lengths, dtype=np.int64)
+    T = int(lengths.sum())
+    P = len(lengths)
+    use_gae = not (gae_lambda is None or gae_lambda < 0.0 or gae_lambda > 1.0)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(dev)
+    rw = t(rewards, np.float64)
+    bl = t(baseline if baseline is not None else np.zeros(T), np.float64)
+    off = t(np.concatenate([[0], np.cumsum(lengths)]), np.int64)
+    term = t(np.asarray(terminated, dtype=np.uint8), np.uint8)
+    ret = torch.empty(max(T, 1), dtype=torch.float64, device=dev)
+    adv = torch.empty(max(T, 1), dtype=torch.float64, device=dev)
+    pr = torch.empty(max(P, 1), dtype=torch.float64, device=dev)
+    _lib.check(L.mjrl_gae(_lib.ptr(rw), _lib.ptr(bl), _lib.ptr(off), _lib.ptr(term), P, float(gamma),
+                          float(gae_lambda) if use_gae else 0.0, int(use_gae), _lib.ptr(ret), _lib.ptr(adv),
+                          _lib.ptr(pr), _lib.stream_ptr()), "mjrl_gae")
+    if normalize and T > 0:
+        st = _lib.stream_ptr()
+        part = torch.zeros(4 * 256 + 16, dtype=torch.float64, device=dev)
+        m = torch.zeros(16, dtype=torch.float64, device=dev)
+        out = torch.empty(T, dtype=torch.float64, device=dev)
+        _lib.check(L.mjrl_moments(_lib.ptr(adv), T, None, _lib.ptr(part), _lib.ptr(m), st), "mjrl_moments")
+        _lib.check(L.mjrl_moments(_lib.ptr(adv), T, _lib.ptr(m), _lib.ptr(part), C.c_void_p(m[8:].data_ptr()), st),
+                   "mjrl_moments")
+        _lib.check(L.mjrl_whiten(_lib.ptr(adv), T, _lib.ptr(m), C.c_void_p(m[8:].data_ptr()), 1e-8, None,
+                                 _lib.ptr(out), st), "mjrl_whiten")
+        adv = out
+    return ret[:T].cpu().numpy(), adv[:T].cpu().numpy()

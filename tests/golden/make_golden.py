@@ -344,5 +344,28 @@ def main():
              log_std=np.linspace(-1.0, 0.0, m))
 
 
+def baselines_case():
+    """Reference LinearBaseline / QuadraticBaseline fit + predict on ragged paths."""
+    from mjrl.baselines.quadratic_baseline import QuadraticBaseline
+    rs = np.random.RandomState(31)
+    n = 5
+    lengths = [7, 1, 30, 12]
+    paths = make_paths(rs, n, 2, lengths, [False] * 4)
+    for p in paths:
+        p["observations"] = p["observations"] * 6.0   # exercise the +-10 clip
+    process_samples.compute_returns(paths, 0.99)
+    spec = EnvSpec(n, 2, 30, 1)
+    lin, quad = LinearBaseline(spec), QuadraticBaseline(spec)
+    lerr = lin.fit(paths, return_errors=True)
+    qerr = quad.fit(paths, return_errors=True)
+    np.savez_compressed(os.path.join(OUT, "baselines.npz"),
+                        obs=concat(paths, "observations"), rewards=concat(paths, "rewards"),
+                        returns=concat(paths, "returns"), lengths=np.array(lengths),
+                        lin_coeffs=lin._coeffs, lin_pred=np.concatenate([lin.predict(p) for p in paths]),
+                        lin_err=np.array(lerr), quad_coeffs=quad._coeffs,
+                        quad_pred=np.concatenate([quad.predict(p) for p in paths]), quad_err=np.array(qerr))
+
+
 if __name__ == "__main__":
     main()
+    baselines_case()

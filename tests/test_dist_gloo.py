@@ -1,0 +1,110 @@
+"""world_size-2 gloo test of the sharded update's collective schedule (CPU).
+
+Every rank takes its shard of a golden batch (mjrl_amd.comm.partition_paths),
+computes the per-shard SUMS the device kernels produce (whitening moments,
+path-return moments + extrema, VPG sum, FVP sums) — here with the oracle as the
+stand-in compute, since this container has no GPU — all-reduces them through
+mjrl_amd.comm.DistComm exactly as mjrl_amd.engine.UpdateEngine.update does, and
+finishes with the replicated CG.  The result must equal the unsharded update.
+The same schedule runs over RCCL on the GPU box (tests/test_gpu_dist.py)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import GOLDEN
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, name, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    try:
+        from mjrl_amd.comm import DistComm, partition_paths
+        from oracle import npg_cpu as O
+        comm = DistComm()
+        c = O.load_case(os.path.join(GOLDEN, name + ".npz"))
+        lengths = c["lengths"]
+        offs = np.concatenate([[0], np.cumsum(lengths)])
+        p0, p1 = partition_paths(lengths, world)[rank]
+        r0, r1 = offs[p0], offs[p1]
+        adv = c["advantages"][r0:r1]
+        T = float(r1 - r0)
+        # whitening: two-pass moments, all-reduced (engine.update S_M1 / S_M2)
+        m1 = torch.tensor([adv.sum(), 0.0, T], dtype=torch.float64)
+        comm.allreduce_sum(m1)
+        mean = m1[0].item() / m1[2].item()
+        m2 = torch.tensor([(adv - mean).sum(), ((adv - mean) ** 2).sum(), T], dtype=torch.float64)
+        comm.allreduce_sum(m2)
+        w = (adv - mean) / (np.sqrt(m2[1].item() / m1[2].item()) + 1e-6)
+        # path-return stats: sums + MAX over [max, -min]
+        pr = np.array([np.sum(c["rewards"][offs[i]:offs[i + 1]]) for i in range(p0, p1)])
+        pm1 = torch.tensor([pr.sum(), 0.0, float(len(pr))], dtype=torch.float64)
+        comm.allreduce_sum(pm1)
+        mx = torch.tensor([pr.max() if len(pr) else -np.inf, -pr.min() if len(pr) else -np.inf],
+                          dtype=torch.float64)
+        comm.allreduce_max(mx)
+        pmean = pm1[0].item() / pm1[2].item()
+        pm2 = torch.tensor([((pr - pmean) ** 2).sum()], dtype=torch.float64)
+        comm.allreduce_sum(pm2)
+        stats = [pmean, np.sqrt(pm2[0].item() / pm1[2].item()), -mx[1].item(), mx[0].item()]
+        Tg = m1[2].item()
+        # VPG: per-shard sum, all-reduced, divided by the global row count
+        pol = O.Policy(int(c["n"]), int(c["m"]), c["hidden_t"], c["theta0"], c["transforms"])
+        obs, act = c["obs64"][r0:r1], c["act64"][r0:r1]
+        gsum = torch.from_numpy(pol.flat_vpg(obs, act, w).astype(np.float64) * T)
+        comm.allreduce_sum(gsum)
+        g = (gsum / Tg).numpy().astype(np.float32)
+        # CG with the sharded FVP: sum_r T_r (F_r v) / T_global + damping v
+        def fvp(v):
+            z = torch.from_numpy((pol.fvp(obs, act, v, 0.0).astype(np.float64)) * T)
+            comm.allreduce_sum(z)
+            return ((z / Tg).numpy() + 1e-4 * v).astype(np.float32)
+        x = O.cg_solve(fvp, g, iters=10)
+        q.put((rank, w, stats, g, x))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name", ["c2_ragged", "c3_halfcheetah_trpo"])
+def test_sharded_schedule_equals_unsharded(name):
+    from oracle import npg_cpu as O
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, name, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(world):
+        r, *vals = q.get(timeout=300)
+        out[r] = vals
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    c = O.load_case(os.path.join(GOLDEN, name + ".npz"))
+    w = np.concatenate([out[r][0] for r in range(world)])
+    np.testing.assert_allclose(w, c["adv_whitened"], rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(out[0][1], c["base_stats"], rtol=1e-10)
+    np.testing.assert_allclose(out[1][1], c["base_stats"], rtol=1e-10)
+    g0, g1 = out[0][2], out[1][2]
+    assert np.array_equal(g0, g1)                                  # replicated after the all-reduce
+    assert np.linalg.norm(g0 - c["vpg_grad"]) / np.linalg.norm(c["vpg_grad"]) < 1e-5
+    x0, x1 = out[0][3], out[1][3]
+    assert np.array_equal(x0, x1)
+    tol = max(1e-3, 3 * float(c["spread_x"]), 2 * float(c["err64_x"]))
+    assert np.linalg.norm(x0 - c["cg_x"]) / np.linalg.norm(c["cg_x"]) < tol

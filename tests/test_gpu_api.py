@@ -1,0 +1,274 @@
+"""GPU tests of the drop-in API (mjrl_amd.algos / policies / utils) and of
+size-independent properties at full scale.  Fixture tolerances as in
+test_gpu_parity.py."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def nrel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
+
+
+def load(name):
+    from oracle import npg_cpu as O
+    return O.load_case(os.path.join(GOLDEN, name + ".npz"))
+
+
+def paths_of(c, with_adv=True):
+    offs = np.concatenate([[0], np.cumsum(c["lengths"])])
+    out = []
+    for i in range(len(c["lengths"])):
+        s = slice(offs[i], offs[i + 1])
+        p = dict(observations=c["obs64"][s], actions=c["act64"][s], rewards=c["rewards"][s],
+                 terminated=bool(c["terminated"][i]), agent_infos={}, env_infos={})
+        if with_adv:
+            p["advantages"] = c["advantages"][s]
+        out.append(p)
+    return out
+
+
+def make_policy(c):
+    from mjrl_amd.policies.gaussian_mlp import MLP
+    from mjrl_amd.policies.gaussian_linear import LinearPolicy
+    from mjrl_amd.utils.gym_env import EnvSpec
+    spec = EnvSpec(int(c["n"]), int(c["m"]), 1000, 1)
+    pol = LinearPolicy(spec, seed=0) if int(c["linear"]) else MLP(spec, hidden_sizes=c["hidden_t"], seed=0)
+    if c["transforms"] is not None:
+        for mdl in (pol.model, pol.old_model):
+            mdl.set_transformations(*c["transforms"])
+    pol.set_param_values(c["theta0"], set_new=True, set_old=True)
+    return pol, spec
+
+
+def tol(c, key, floor):
+    return max(floor, 3.0 * float(c["spread_" + key]), 2.0 * float(c["err64_" + key]))
+
+
+def make_agent(name, c, pol, spec):
+    from mjrl_amd.algos.npg_cg import NPG
+    from mjrl_amd.algos.trpo import TRPO
+    from mjrl_amd.algos.dapg import DAPG
+    from mjrl_amd.baselines.linear_baseline import LinearBaseline
+    from oracle import npg_cpu as O
+    base = LinearBaseline(spec)
+    if c["baseline_coeffs"].size:
+        base._coeffs = c["baseline_coeffs"]
+    kw = O.case_kwargs(c)
+    if kw["algo"] == "npg":
+        args = {}
+        if "kw_normalized_step_size" in c:
+            args["normalized_step_size"] = float(c["kw_normalized_step_size"])
+        if "kw_const_learn_rate" in c:
+            args["const_learn_rate"] = float(c["kw_const_learn_rate"])
+        return NPG(None, pol, base, save_logs=True, **args), base
+    if kw["algo"] == "trpo":
+        return TRPO(None, pol, base, kl_dist=kw["kl_dist"], save_logs=True), base
+    offs = np.concatenate([[0], np.cumsum(c["demo_lengths"])])
+    demos = [dict(observations=c["demo_obs"][offs[i]:offs[i + 1]].astype(np.float64),
+                  actions=c["demo_act"][offs[i]:offs[i + 1]].astype(np.float64))
+             for i in range(len(c["demo_lengths"]))]
+    return DAPG(None, pol, base, demo_paths=demos, save_logs=True), base
+
+
+REF_KEYS = {"npg": {"alpha", "delta", "time_vpg", "time_npg", "kl_dist", "surr_improvement", "running_score",
+                    "stoc_pol_mean", "stoc_pol_std", "stoc_pol_max", "stoc_pol_min"}}
+
+
+@pytest.mark.parametrize("name", ["c1_pointmass_linear", "c2_swimmer", "c3_trpo_backtrack", "c4_humanoid",
+                                  "c5_door_dapg", "c2_constlr"])
+def test_train_from_paths(name):
+    c = load(name)
+    pol, spec = make_policy(c)
+    agent, _ = make_agent(name, c, pol, spec)
+    stats = agent.train_from_paths(paths_of(c))
+    np.testing.assert_allclose(stats, c["base_stats"], rtol=1e-12)
+    assert nrel(pol.get_param_values(), c["theta1"]) < tol(c, "theta", 1e-3)
+    log = agent.logger.get_current_log()
+    assert REF_KEYS["npg"] <= set(log) | {"delta", "time_npg"}
+    np.testing.assert_allclose(log["alpha"], c["log_alpha"], rtol=tol(c, "alpha", 2e-3))
+    np.testing.assert_allclose(log["kl_dist"], c["log_kl_dist"], rtol=tol(c, "kl", 2e-3), atol=1e-7)
+    np.testing.assert_allclose(agent.running_score, c["base_stats"][0], rtol=1e-12)
+    # the CPU mirror now holds the device result, old == new
+    old = np.concatenate([p.data.reshape(-1).numpy() for p in pol.old_params])
+    assert np.array_equal(old, pol.get_param_values())
+
+
+@pytest.mark.parametrize("name", ["c2_ragged", "c2_nogae", "c2_swimmer"])
+def test_train_from_samples_fused_gae(name):
+    """train_step's path: raw paths + baseline -> GAE on device -> update; the
+    returns / baseline / advantages written back into the paths are bit-exact."""
+    c = load(name)
+    pol, spec = make_policy(c)
+    agent, base = make_agent(name, c, pol, spec)
+    paths = paths_of(c, with_adv=False)
+    lam = None if np.isnan(c["gae_lambda"]) else float(c["gae_lambda"])
+    stats = agent.train_from_samples(paths, float(c["gamma"]), lam)
+    assert np.array_equal(np.concatenate([p["returns"] for p in paths]), c["returns"])
+    assert np.array_equal(np.concatenate([p["baseline"] for p in paths]), c["baseline"])
+    assert np.array_equal(np.concatenate([p["advantages"] for p in paths]), c["advantages"])
+    np.testing.assert_allclose(stats, c["base_stats"], rtol=1e-12)
+    assert nrel(pol.get_param_values(), c["theta1"]) < tol(c, "theta", 1e-3)
+
+
+def test_process_samples_bitexact():
+    from mjrl_amd.baselines.linear_baseline import LinearBaseline
+    from mjrl_amd.utils import process_samples as ps
+    from mjrl_amd.utils.gym_env import EnvSpec
+    from oracle import npg_cpu as O
+    c = load("c2_ragged")
+    paths = paths_of(c, with_adv=False)
+    base = LinearBaseline(EnvSpec(8, 2, 10, 1))
+    base._coeffs = c["baseline_coeffs"]
+    ps.compute_returns(paths, float(c["gamma"]))
+    ps.compute_advantages(paths, base, float(c["gamma"]), float(c["gae_lambda"]))
+    assert np.array_equal(np.concatenate([p["returns"] for p in paths]), c["returns"])
+    assert np.array_equal(np.concatenate([p["advantages"] for p in paths]), c["advantages"])
+    x = np.random.RandomState(0).randn(37)
+    assert np.array_equal(ps.discount_sum(x, 0.9), O.discount_sum(x, 0.9))
+    assert np.array_equal(ps.discount_sum(x, 0.9, terminal=2.5), O.discount_sum(x, 0.9, terminal=2.5))
+    ps.compute_advantages(paths, base, float(c["gamma"]), float(c["gae_lambda"]), normalize=True)
+    a = c["advantages"]
+    np.testing.assert_allclose(np.concatenate([p["advantages"] for p in paths]),
+                               (a - a.mean()) / (a.std() + 1e-8), rtol=1e-12, atol=1e-12)
+
+
+def test_cg_solve_generic_matches_reference_semantics():
+    from mjrl_amd.utils.cg_solve import cg_solve
+    from oracle import npg_cpu as O
+    rs = np.random.RandomState(2)
+    A = rs.randn(300, 300).astype(np.float32)
+    A = (A @ A.T / 300 + np.eye(300, dtype=np.float32)).astype(np.float32)
+    b = rs.randn(300).astype(np.float32)
+    f = lambda v: (A @ v).astype(np.float32)
+    x = cg_solve(f, b, cg_iters=10)
+    xr = O.cg_solve(f, b.copy(), iters=10)
+    assert x.dtype == np.float32
+    assert nrel(x, xr) < 1e-5
+    x3 = cg_solve(f, b, cg_iters=300, residual_tol=1e-10)
+    assert nrel(A @ x3, b) < 1e-4
+
+
+def test_single_passes_match_reference():
+    """CPI_surrogate / kl_old_new / flat_vpg / HVP called directly (the reference API)."""
+    c = load("c2_swimmer")
+    pol, spec = make_policy(c)
+    agent, _ = make_agent("c2_swimmer", c, pol, spec)
+    obs, act = c["obs64"], c["act64"]
+    g = agent.flat_vpg(obs, act, c["adv_whitened"])
+    assert nrel(g, c["vpg_grad"]) < 1e-5
+    hv = agent.HVP(obs, act, c["hvp_v"])
+    assert nrel(hv, c["hvp_out"]) < 1e-5
+    assert abs(float(agent.kl_old_new(obs, act))) < 1e-7          # old == new
+    surr = float(agent.CPI_surrogate(obs, act, c["adv_whitened"]))
+    np.testing.assert_allclose(surr, c["surr_calls"][0], atol=1e-7)
+    # after moving only the new params, surrogate / KL against the oracle
+    from oracle import npg_cpu as O
+    pol.set_param_values(c["theta1"], set_new=True, set_old=False)
+    ref = O.Policy(8, 2, (64, 64), c["theta0"], None)
+    ref.set_params(c["theta1"], set_new=True, set_old=False)
+    np.testing.assert_allclose(float(agent.kl_old_new(obs, act)), float(ref.kl(obs, act).detach()), rtol=1e-4)
+    np.testing.assert_allclose(float(agent.CPI_surrogate(obs, act, c["adv_whitened"])),
+                               float(ref.surrogate(obs, act, c["adv_whitened"]).detach()), rtol=1e-4, atol=1e-7)
+    with pytest.raises(ValueError):
+        agent.flat_vpg(obs, act, c["adv_whitened"])
+
+
+# ---------------------------------------------------------------------------
+# size-independent properties at full scale (Humanoid shape)
+# ---------------------------------------------------------------------------
+def _engine_with_rows(T, seed=0):
+    from mjrl_amd.engine import UpdateEngine
+    rs = np.random.RandomState(seed)
+    eng = UpdateEngine(376, 17, (64, 64), device="cuda:0")
+    obs = rs.randn(T, 376)
+    act = rs.randn(T, 17)
+    eng.load_rows(obs, act, rs.randn(T))
+    theta = (rs.randn(29410) * 0.05).astype(np.float32)
+    theta[-17:] = np.linspace(-1, 0.5, 17)
+    th = torch.from_numpy(theta).cuda()
+    eng.forward_pass(th, T)
+    return eng, rs
+
+
+@pytest.mark.parametrize("T", [300000])
+def test_fvp_properties_full_scale(T):
+    eng, rs = _engine_with_rows(T)
+    d = 29410
+    v = torch.from_numpy(rs.randn(d).astype(np.float32)).cuda()
+    w = torch.from_numpy(rs.randn(d).astype(np.float32)).cuda()
+    Fv = eng.fvp(v, damping=0.0, T=T).double()
+    Fw = eng.fvp(w, damping=0.0, T=T).double()
+    # symmetry: w.Fv == v.Fw
+    a, b = torch.dot(w.double(), Fv).item(), torch.dot(v.double(), Fw).item()
+    assert abs(a - b) / abs(a) < 1e-4
+    # positive semi-definite
+    assert torch.dot(v.double(), Fv).item() > 0 and torch.dot(w.double(), Fw).item() > 0
+    # linearity
+    F2 = eng.fvp(2.0 * v - 3.0 * w, damping=0.0, T=T).double()
+    assert (torch.norm(F2 - (2 * Fv - 3 * Fw)) / torch.norm(F2)).item() < 1e-5
+    # damping adds exactly damping * v
+    Fd = eng.fvp(v, damping=0.5, T=T).double()
+    assert (torch.norm(Fd - Fv - 0.5 * v.double()) / torch.norm(Fd)).item() < 1e-6
+
+
+def test_fvp_row_permutation_invariance():
+    """Reordering timesteps only reorders sums (the update is path-order invariant)."""
+    from mjrl_amd.engine import UpdateEngine
+    T = 5000
+    rs = np.random.RandomState(3)
+    obs, act = rs.randn(T, 376), rs.randn(T, 17)
+    theta = (rs.randn(29410) * 0.05).astype(np.float32)
+    theta[-17:] = np.linspace(-1, 0.5, 17)
+    th = torch.from_numpy(theta).cuda()
+    v = torch.from_numpy(rs.randn(29410).astype(np.float32)).cuda()
+    eng = UpdateEngine(376, 17, (64, 64), device="cuda:0")
+    eng.load_rows(obs, act)
+    g1 = eng.forward_pass(th, T).cpu().numpy()
+    F1 = eng.fvp(v, damping=0.0, T=T).cpu().numpy()
+    perm = np.random.RandomState(9).permutation(T)
+    eng.load_rows(obs[perm], act[perm])
+    g2 = eng.forward_pass(th, T).cpu().numpy()
+    F2 = eng.fvp(v, damping=0.0, T=T).cpu().numpy()
+    assert nrel(F1, F2) < 1e-5
+    assert nrel(g1, g2) < 1e-5 or np.linalg.norm(g1) < 1e-6
+
+
+def test_edge_cases_tiny_and_ragged():
+    """One path of length 1, paths shorter than a tile, terminated flags, a
+    batch smaller than one 64-row tile: against the oracle."""
+    from mjrl_amd.engine import UpdateEngine, DeviceBatch
+    from oracle import npg_cpu as O
+    rs = np.random.RandomState(4)
+    for lengths in ([1], [1, 2, 3], [63, 1, 64, 65]):
+        lengths = np.array(lengths)
+        T = int(lengths.sum())
+        n, m = 6, 3
+        obs = rs.randn(T, n).astype(np.float32).astype(np.float64)
+        act = rs.randn(T, m).astype(np.float32).astype(np.float64)
+        rew = rs.randn(T)
+        base = rs.randn(T)
+        term = (np.arange(len(lengths)) % 2).astype(np.uint8)
+        theta = (rs.randn(6 * 32 + 32 + 32 * 32 + 32 + 3 * 32 + 3 + 3) * 0.1).astype(np.float32)
+        eng = UpdateEngine(n, m, (32, 32), device="cuda:0")
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+        off = np.concatenate([[0], np.cumsum(lengths)]).astype(np.int64)
+        b = DeviceBatch(t(obs), t(act), t(rew), t(base), t(off), t(term))
+        res = eng.update(b, t(theta), algo="npg", gamma=0.99, gae_lambda=0.95, n_step_size=0.05)
+        ret, adv = O.returns_and_advantages(rew, base, lengths, term.astype(bool), 0.99, 0.95)
+        assert np.array_equal(eng.ws["adv64"][:T].cpu().numpy(), adv)
+        assert np.array_equal(eng.ws["ret"][:T].cpu().numpy(), ret)
+        if T < 3:
+            continue   # whitening of 1-2 samples is degenerate in the reference too
+        pol = O.Policy(n, m, (32, 32), theta.astype(np.float64), None)
+        g = pol.flat_vpg(obs, act, O.whiten(adv))
+        assert nrel(eng.vec["g"].cpu().numpy(), g) < 1e-5
+        np.testing.assert_allclose(res["base_stats"], O.path_return_stats(rew, lengths), rtol=1e-12)

@@ -45,6 +45,22 @@ def flops_per_row(n, m, h0, h1):
     return dict(rows_fvp=jvp + vjp_act, weight_grads=wgrad)
 
 
+def pmc_traffic(kernel_key):
+    """HBM bytes per launch of a kernel from the newest committed PMC summary
+    (profiles/r*/pmc_traffic.json, written from separate rocprofv3 --pmc passes
+    of FETCH_SIZE and WRITE_SIZE with the gfx950 2x FETCH_SIZE correction; the
+    correction checks out on k_pack_batch, whose 3.14 GB read is known exactly)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")))
+    if not files:
+        return None, None
+    data = json.load(open(files[-1]))
+    for name, v in data.items():
+        if kernel_key in name:
+            return v["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+    return None, None
+
+
 def make_paths(p0, p1, seed=123):
     """Paths p0..p1-1 of the synthetic batch, each from its own seeded stream
     (so a rank generates only its shard and N does not change the data)."""
@@ -187,9 +203,15 @@ def main():
     kern = {"rows_fvp": dict(avg_ms=t_rows * 1e3, tflops=fl["rows_fvp"] * rows_rank / t_rows / 1e12),
             "weight_grads": dict(avg_ms=t_grad * 1e3, tflops=fl["weight_grads"] * rows_rank / t_grad / 1e12)}
     dom = max(kern, key=lambda k: kern[k]["avg_ms"])
+    traffic, tsrc = pmc_traffic("k_rows<64, 64, 32, 1>" if dom == "rows_fvp" else "k_wgrad")
+    if traffic is not None and world > 1:
+        traffic = traffic * rows_rank / T_total    # the committed PMC pass is the 1-GPU (1M-row) launch
     roof = dict(bound="mfma", kernel="k_rows<64,64,32,FVP>" if dom == "rows_fvp" else "k_wgrad",
                 achieved=round(kern[dom]["tflops"], 3), peak=PEAK_F32_MFMA, unit="TFLOP/s",
-                frac=round(kern[dom]["tflops"] / PEAK_F32_MFMA, 4), traffic=None,
+                frac=round(kern[dom]["tflops"] / PEAK_F32_MFMA, 4),
+                traffic=None if traffic is None else round(traffic),
+                traffic_unit="bytes/launch (HBM, PMC)", traffic_source=tsrc,
+                traffic_GBps=None if traffic is None else round(traffic / (kern[dom]["avg_ms"] * 1e-3) / 1e9, 1),
                 flops_per_timestep=fl[dom], rows_per_launch=rows_rank, launches=len(ev),
                 kernels={k: {kk: round(vv, 4) for kk, vv in v.items()} for k, v in kern.items()})
 

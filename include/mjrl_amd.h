@@ -96,6 +96,12 @@ int mjrl_gae(const double* rew, const double* base, const int64_t* path_off,
              const uint8_t* terminated, int64_t P, double gamma, double gae_lambda,
              int32_t use_gae, double* ret, double* adv, double* path_ret, void* stream);
 
+/* ---- LinearBaseline.predict on device (baselines/linear_baseline.py:10-18, 46-49) ----
+ * out[t] = [clip(obs_t, +-10), a, a^2, a^3, 1] . coeffs[n+4], a = (t - path start)/1000,
+ * for every row of every path (the input of mjrl_gae, process_samples.py:23). */
+int mjrl_linear_baseline(const double* obs, int64_t T, int32_t n, const int64_t* path_off,
+                         int64_t P, const double* coeffs, double* out, void* stream);
+
 /* ---- moments for whitening / stats (npg_cg.py:91, 97-102; dapg.py:70) ----
  * out[0] = sum(x - c), out[1] = sum((x - c)^2), out[2] = N, out[3] = min(x),
  * out[4] = max(x), out[5] = -min(x) over x[0..N-1] (out needs 6 doubles),
@@ -151,19 +157,23 @@ int mjrl_policy_eval(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_eval,
                      const float* out_shift, const float* out_scale,
                      const mjrl_scratch* sc, double* sums, void* stream);
 
-/* The three launches behind the composites above, for callers that time or
- * overlap them separately: the per-row chain (rows_*) writes gu0/gu1/gp (and the
- * caches / log-std partials for vpg); weight_grads reduces them into gsum
- * (with_log_std = 1 after rows_vpg). */
-int mjrl_rows_vpg(const mjrl_shape* s, const mjrl_rows* rows, const float* packed_theta,
-                  const float* out_shift, const float* out_scale, const mjrl_scratch* sc,
-                  void* stream);
-int mjrl_rows_fvp(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_fvp,
-                  const float* packed_theta, const float* packed_v, const float* out_scale,
-                  const int32_t* done, void* stream);
-int mjrl_weight_grads(const mjrl_shape* s, const mjrl_rows* rows, int64_t T,
+/* The two steps behind the composites above, for callers that time or overlap
+ * them separately.  *_accumulate writes per-slice partial sums of every weight /
+ * bias gradient ("slabs" in sc->wpart); gather_grads folds the slabs in slice
+ * order into gsum[d] (with_log_std = 1 after vpg_accumulate).  For hidden widths
+ * 32 / 64 (m <= 32, n <= 383) accumulate is ONE persistent fused kernel (row chain
+ * + register-resident weight-gradient sums); otherwise the row-chain kernel plus
+ * the split-K weight-gradient kernel.  mjrl_fused_path(s) reports which. */
+int mjrl_vpg_accumulate(const mjrl_shape* s, const mjrl_rows* rows, const float* packed_theta,
+                        const float* out_shift, const float* out_scale, const mjrl_scratch* sc,
+                        void* stream);
+int mjrl_fvp_accumulate(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_fvp,
+                        const float* packed_theta, const float* packed_v, const float* out_scale,
+                        const int32_t* done, const mjrl_scratch* sc, void* stream);
+int mjrl_gather_grads(const mjrl_shape* s, const mjrl_rows* rows, int64_t T,
                       const mjrl_scratch* sc, int32_t with_log_std, const int32_t* done,
                       float* gsum, void* stream);
+int mjrl_fused_path(const mjrl_shape* s);
 
 /* ---- conjugate gradient on device (cg_solve.py:3-22) ----
  * State cg[8] (f32 scalars, device): [rdotr, v, mu, pz, done_flag(as int bits), iters, ...].

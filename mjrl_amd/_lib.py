@@ -48,6 +48,7 @@ SIGNATURES = {
     "mjrl_scratch_size": [SP, I64, C.POINTER(I64), C.POINTER(I64), C.POINTER(I32)],
     "mjrl_pack_batch": [P, P, I64, SP, P, P, P, P, P],
     "mjrl_gae": [P, P, P, P, I64, F64, F64, I32, P, P, P, P],
+    "mjrl_linear_baseline": [P, I64, I32, P, I64, P, P, P],
     "mjrl_moments": [P, I64, P, P, P, P],
     "mjrl_moments_f32": [P, I64, P, P, P, P],
     "mjrl_whiten": [P, I64, P, P, F64, P, P, P],
@@ -56,9 +57,10 @@ SIGNATURES = {
     "mjrl_policy_vpg": [SP, C.POINTER(Rows), P, P, P, C.POINTER(Scratch), P, P],
     "mjrl_policy_fvp": [SP, C.POINTER(Rows), I64, P, P, P, C.POINTER(Scratch), P, P, P],
     "mjrl_policy_eval": [SP, C.POINTER(Rows), I64, P, P, P, P, C.POINTER(Scratch), P, P],
-    "mjrl_rows_vpg": [SP, C.POINTER(Rows), P, P, P, C.POINTER(Scratch), P],
-    "mjrl_rows_fvp": [SP, C.POINTER(Rows), I64, P, P, P, P, P],
-    "mjrl_weight_grads": [SP, C.POINTER(Rows), I64, C.POINTER(Scratch), I32, P, P, P],
+    "mjrl_vpg_accumulate": [SP, C.POINTER(Rows), P, P, P, C.POINTER(Scratch), P],
+    "mjrl_fvp_accumulate": [SP, C.POINTER(Rows), I64, P, P, P, P, C.POINTER(Scratch), P],
+    "mjrl_gather_grads": [SP, C.POINTER(Rows), I64, C.POINTER(Scratch), I32, P, P, P],
+    "mjrl_fused_path": [SP],
     "mjrl_cg_init": [SP, P, P, P, P, P, P, P, P],
     "mjrl_cg_step": [SP, P, F64, F32, P, P, P, P, P, P, P, P, F32, P],
     "mjrl_cg_init_vec": [I32, P, P, P, P, P, P, P],

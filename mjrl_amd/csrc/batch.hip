@@ -43,41 +43,87 @@ __global__ void __launch_bounds__(256) k_pack_batch(const double* __restrict__ o
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < na; i += stride) act32[i] = (float)act[i];
 }
 
-// One lane per path; reverse recurrences in fp64 with separate multiply and add
-// (__dmul_rn / __dadd_rn cannot be contracted) — bit-identical to discount_sum.
+// Two lanes per path: the even lane runs the reverse recurrences (returns and GAE
+// advantages), the odd lane the forward path-return sum.  fp64 with separate
+// multiply and add (__dmul_rn / __dadd_rn cannot be contracted): bit-identical
+// to discount_sum.  The serial chain is short (a dependent mul+add per step);
+// what costs is memory latency, so each lane streams its path in 16-step chunks
+// through registers, the next chunk's loads in flight while this one is scanned.
+constexpr int GCH = 16;
+
 __global__ void __launch_bounds__(64) k_gae(const double* __restrict__ rew, const double* __restrict__ base,
                                             const int64_t* __restrict__ off, const uint8_t* __restrict__ term,
                                             int64_t P, double gamma, double gl, int use_gae,
                                             double* __restrict__ ret, double* __restrict__ adv,
                                             double* __restrict__ path_ret) {
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t lane_id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t p = lane_id >> 1;
     if (p >= P) return;
     const int64_t b = off[p], e = off[p + 1];
-    // sum(p["rewards"]) — Python's builtin sum, front to back (npg_cg.py:97)
-    double s = 0.0;
-    for (int64_t t = b; t < e; ++t) s = __dadd_rn(s, rew[t]);
-    path_ret[p] = s;
-    if (e <= b) return;
-    // returns: discount_sum(rewards, gamma) (process_samples.py:3-5, 37-44)
-    double acc = 0.0;
-    for (int64_t t = e - 1; t >= b; --t) {
-        acc = __dadd_rn(rew[t], __dmul_rn(gamma, acc));
-        ret[t] = acc;
-    }
-    if (!use_gae) {   // process_samples.py:10-13
-        for (int64_t t = b; t < e; ++t) adv[t] = __dsub_rn(ret[t], base[t]);
+    if (lane_id & 1) {
+        // sum(p["rewards"]) — Python's builtin sum, front to back (npg_cg.py:97)
+        double s = 0.0;
+        double x[GCH];
+        for (int64_t t0 = b; t0 < e; t0 += GCH) {
+            const int cnt = e - t0 < GCH ? (int)(e - t0) : GCH;
+#pragma unroll
+            for (int i = 0; i < GCH; ++i) x[i] = i < cnt ? rew[t0 + i] : 0.0;
+#pragma unroll
+            for (int i = 0; i < GCH; ++i)
+                if (i < cnt) s = __dadd_rn(s, x[i]);
+        }
+        path_ret[p] = s;
         return;
     }
+    if (e <= b) return;
+    // returns: discount_sum(rewards, gamma) (process_samples.py:3-5, 37-44)
     // GAE (process_samples.py:21-29): b1 = append(b, 0 if terminated else b[-1]),
-    // td = r + gamma*b1[1:] - b1[:-1], adv = discount_sum(td, gamma*lambda)
+    // td = r + gamma*b1[1:] - b1[:-1], adv = discount_sum(td, gamma*lambda);
+    // plain advantages (process_samples.py:10-13): ret - baseline.
+    double acc_r = 0.0, acc_a = 0.0;
     double bnext = term[p] ? 0.0 : base[e - 1];
-    acc = 0.0;
-    for (int64_t t = e - 1; t >= b; --t) {
-        const double bt = base[t];
-        const double td = __dsub_rn(__dadd_rn(rew[t], __dmul_rn(gamma, bnext)), bt);
-        acc = __dadd_rn(td, __dmul_rn(gl, acc));
-        adv[t] = acc;
-        bnext = bt;
+    double rc[GCH], bc[GCH], rn[GCH], bn[GCH];
+    int64_t t1 = e;                                   // current chunk is [t0, t1)
+    int64_t t0 = t1 - GCH > b ? t1 - GCH : b;
+#pragma unroll
+    for (int i = 0; i < GCH; ++i) {
+        const int64_t t = t0 + i;
+        rc[i] = t < t1 ? rew[t] : 0.0;
+        bc[i] = t < t1 ? base[t] : 0.0;
+    }
+    while (true) {
+        const int64_t n1 = t0, n0 = n1 - GCH > b ? n1 - GCH : b;   // next chunk [n0, n1)
+#pragma unroll
+        for (int i = 0; i < GCH; ++i) {
+            const int64_t t = n0 + i;
+            rn[i] = t < n1 ? rew[t] : 0.0;
+            bn[i] = t < n1 ? base[t] : 0.0;
+        }
+        const int cnt = (int)(t1 - t0);
+#pragma unroll
+        for (int i = GCH - 1; i >= 0; --i) {
+            if (i < cnt) {
+                const int64_t t = t0 + i;
+                acc_r = __dadd_rn(rc[i], __dmul_rn(gamma, acc_r));
+                ret[t] = acc_r;
+                if (use_gae) {
+                    const double td = __dsub_rn(__dadd_rn(rc[i], __dmul_rn(gamma, bnext)), bc[i]);
+                    acc_a = __dadd_rn(td, __dmul_rn(gl, acc_a));
+                    adv[t] = acc_a;
+                    bnext = bc[i];
+                } else {
+                    adv[t] = __dsub_rn(acc_r, bc[i]);
+                }
+            }
+        }
+        if (t0 <= b) break;
+        t1 = n1;
+        t0 = n0;
+#pragma unroll
+        for (int i = 0; i < GCH; ++i) {
+            rc[i] = rn[i];
+            bc[i] = bn[i];
+        }
     }
 }
 
@@ -171,6 +217,38 @@ __global__ void __launch_bounds__(256) k_dapg_adv(const double* __restrict__ w64
         adv_vpg[i] = i < T ? (float)(1e-2 * (w64[i] / den)) : dv;
 }
 
+// LinearBaseline.predict for every path (baselines/linear_baseline.py:10-18,46-49):
+// b_t = clip(o_t, -10, 10) . c[0:n] + (t/1000) c[n] + (t/1000)^2 c[n+1]
+//       + (t/1000)^3 c[n+2] + c[n+3], t = index within the path.
+// One wave per row (lanes across the observation, coalesced f64 loads), a
+// grid-stride over rows; the row's path comes from a binary search of path_off.
+__global__ void __launch_bounds__(256) k_linear_baseline(const double* __restrict__ obs, int64_t T, int n,
+                                                         const int64_t* __restrict__ off, int64_t P,
+                                                         const double* __restrict__ coef, double* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t row = wave; row < T; row += nw) {
+        double acc = 0.0;
+        for (int j = lane; j < n; j += 64) {
+            double o = obs[row * n + j];
+            o = o < -10.0 ? -10.0 : (o > 10.0 ? 10.0 : o);
+            acc += o * coef[j];
+        }
+        acc = wave_sum(acc);
+        if (lane == 0) {
+            int64_t lo = 0, hi = P;   // largest p with off[p] <= row
+            while (hi - lo > 1) {
+                const int64_t mid = (lo + hi) >> 1;
+                if (off[mid] <= row) lo = mid; else hi = mid;
+            }
+            const double al = (double)(row - off[lo]) / 1000.0;
+            acc += al * coef[n] + (al * al) * coef[n + 1] + pow(al, 3.0) * coef[n + 2] + coef[n + 3];
+            out[row] = acc;
+        }
+    }
+}
+
 __global__ void __launch_bounds__(256) k_scale_vec(const float* __restrict__ gsum, int d, double scale,
                                                    float* __restrict__ g) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -208,7 +286,7 @@ int mjrl_gae(const double* rew, const double* base, const int64_t* path_off, con
         return MJRL_EINVAL;
     if (P == 0) return MJRL_OK;
     const double gl = gamma * gae_lambda;   // python: gamma*gae_lambda (process_samples.py:29)
-    hipLaunchKernelGGL(k_gae, dim3((unsigned)((P + 63) / 64)), dim3(64), 0, (hipStream_t)stream, rew, base, path_off,
+    hipLaunchKernelGGL(k_gae, dim3((unsigned)((2 * P + 63) / 64)), dim3(64), 0, (hipStream_t)stream, rew, base, path_off,
                        terminated, P, gamma, gl, use_gae, ret, adv, path_ret);
     return err(hipGetLastError());
 }
@@ -250,6 +328,16 @@ int mjrl_dapg_adv(const double* w64, int64_t T, const double* mw1, const double*
     if (T + T_demo == 0) return MJRL_OK;
     hipLaunchKernelGGL(k_dapg_adv, dim3(grid_for(T + T_demo, 256, 2048)), dim3(256), 0, (hipStream_t)stream, w64,
                        T, mw1, mw2, T_demo, demo_coef, adv_vpg);
+    return err(hipGetLastError());
+}
+
+int mjrl_linear_baseline(const double* obs, int64_t T, int32_t n, const int64_t* path_off, int64_t P,
+                         const double* coeffs, double* out, void* stream) {
+    if (T < 0 || n <= 0 || P < 0 || (T > 0 && (!obs || !path_off || !coeffs || !out))) return MJRL_EINVAL;
+    if (T == 0) return MJRL_OK;
+    const int g = grid_for(T * 64, 256, 4096);
+    hipLaunchKernelGGL(k_linear_baseline, dim3(g), dim3(256), 0, (hipStream_t)stream, obs, T, n, path_off, P,
+                       coeffs, out);
     return err(hipGetLastError());
 }
 

@@ -1,0 +1,465 @@
+// fused.h — persistent fused VPG / FVP kernel for hidden widths <= 64
+// (included by policy.hip: shares RowArgs, gemm_tile and the k_gather slab layout).
+//
+// One 512-thread workgroup (8 waves) per CU walks 64-row tiles of timesteps.
+// Per tile everything stays on chip:
+//   phase 1   xhat tile streamed in 64-column chunks through LDS (double
+//             buffered through registers) x W0 (or the tangent dW0) -> [64 x H0]
+//   phase 2-5 the row chain of k_rows (JVP / forward, GN weight / log-lik,
+//             backprop) with every intermediate in LDS
+//   grads     gW2 += gp^T a1, gW1 += gu1^T a0, gb1 / gb2 column sums, and
+//             gW0 += gu0^T xhat with the tile re-streamed (L2-hot) — all
+//             accumulated in REGISTERS across the workgroup's tiles
+// and each workgroup writes one [H0][NP] / [H1][H0] / [MP][H1] (+ bias) slab
+// at the end, in exactly the layout k_wgrad writes, so k_gather folds them.
+// Replaces k_rows<FWD|FVP> + k_wgrad: the gu0 / gu1 / gp round trip through HBM
+// and k_wgrad's re-reads disappear.
+#pragma once
+
+namespace {
+
+constexpr int FT = 512;          // threads per workgroup (8 waves)
+constexpr int FGRID_CAP = 256;   // one persistent workgroup per CU
+
+// Output tiles [RB x CB] (16x16 each) over 8 waves: each wave owns NRW row
+// blocks x NCW col blocks; waves sharing a col block reuse its B fragment.
+template <int RB, int CB>
+struct Split8 {
+    static constexpr int WPC = CB >= 8 ? 1 : 8 / CB;   // waves per col block
+    static constexpr int NCW = CB >= 8 ? CB / 8 : 1;
+    static constexpr int NRW = CB >= 8 ? RB : (RB / WPC > 0 ? RB / WPC : 1);
+    static constexpr int CBS = CB >= 8 ? 8 : 1;
+    static constexpr int RBS = CB >= 8 ? 1 : WPC;
+    __device__ static int cb0(int w) { return CB >= 8 ? w : w % CB; }
+    __device__ static int rb0(int w) { return CB >= 8 ? 0 : w / CB; }
+};
+
+template <int H0, int H1, int MP>
+struct FLayout {
+    static constexpr int BT = 64;
+    static constexpr int LD0 = H0 + 4, LD1 = H1 + 4, LDP = MP + 4, KC = 64, LDX = KC + 4;
+    static constexpr int oD0 = 0;
+    static constexpr int oA0 = oD0 + BT * LD0;
+    static constexpr int oD1 = oA0 + BT * LD0;
+    static constexpr int oA1 = oD1 + BT * LD1;
+    static constexpr int oGP = oA1 + BT * LD1;
+    static constexpr int oXS = oGP + BT * LDP;
+    static constexpr int total = oXS + 2 * BT * LDX;
+    static constexpr int bytes = total * 4;
+    static_assert(LD0 >= MP, "log-std scratch lives in D0");
+};
+
+struct FOut {
+    float* wpart;
+    int64_t off0, off1, boff1, off2, boff2;   // slab offsets (k_gather layout, S = gridDim.x)
+};
+
+// acc[i][j] += sum_{t<64} G[t][n-block] * A[t][k-block], both row-major in LDS.
+template <int NRW, int NCW>
+__device__ __forceinline__ void wgrad_lds(floatx4 (&acc)[NRW][NCW], const float* G, int ldg, const float* A,
+                                          int lda, int nb0, int nbs, int nb_lim, int kb0, int kbs, int kb_lim,
+                                          int lane) {
+    const int r = lane & 15, q = lane >> 4;
+#pragma unroll 4
+    for (int t = 0; t < 64; t += 4) {
+        float ga[NRW], ab[NCW];
+#pragma unroll
+        for (int i = 0; i < NRW; ++i) {
+            const int nb = nb0 + i * nbs;
+            ga[i] = nb < nb_lim ? G[(t + q) * ldg + nb * 16 + r] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < NCW; ++j) {
+            const int kb = kb0 + j * kbs;
+            ab[j] = kb < kb_lim ? A[(t + q) * lda + kb * 16 + r] : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < NRW; ++i)
+#pragma unroll
+            for (int j = 0; j < NCW; ++j) acc[i][j] = mfma4(ga[i], ab[j], acc[i][j]);
+    }
+}
+
+template <int H0, int H1, int MP, int NCH, int MODE>
+__global__ void __launch_bounds__(FT, 1) k_fused(RowArgs a, FOut o) {
+    using L = FLayout<H0, H1, MP>;
+    constexpr int BT = L::BT, RB = 4, KC = L::KC;
+    using S1 = Split8<RB, H0 / 16>;
+    using S2 = Split8<RB, H1 / 16>;
+    using S3 = Split8<RB, MP / 16>;
+    using W0S = Split8<H0 / 16, KC / 16>;
+    using W1S = Split8<H1 / 16, H0 / 16>;
+    using W2S = Split8<MP / 16, H1 / 16>;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* D0 = smem + L::oD0;
+    float* A0s = smem + L::oA0;
+    float* D1 = smem + L::oD1;
+    float* A1s = smem + L::oA1;
+    float* GPs = smem + L::oGP;
+    float* XS = smem + L::oXS;
+    float* LSs = D0;   // FWD only: [BT][MP] log-std terms, consumed before phase 5 writes D0
+
+    if (MODE == FVP && a.done && *a.done) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int r16 = lane & 15, q = lane >> 4;
+    const int np = a.np, m = a.m;
+    const int64_t T = a.T;
+    const int64_t ntiles = (T + BT - 1) / BT;
+    const float* P = a.P;
+    const float* V = MODE == FVP ? a.V : a.P;   // weights of the first-layer GEMM / biases
+    const Packed pk(H0, H1, np, MP);
+
+    floatx4 g0[NCH][W0S::NRW][W0S::NCW];
+    floatx4 g1[W1S::NRW][W1S::NCW];
+    floatx4 g2[W2S::NRW][W2S::NCW];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) zero_acc(g0[c]);
+    zero_acc(g1);
+    zero_acc(g2);
+    float b1acc = 0.f, b2acc = 0.f;
+    double lsacc = 0.0;
+
+    constexpr int PER = BT * (KC / 4) / FT;   // float4 per thread per chunk
+    float4 st[PER];
+    auto gload = [&](int64_t row_base, int c) {
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int idx = tid + u * FT;
+            const int row = idx / (KC / 4), c4 = idx % (KC / 4);
+            const int col = c * KC + c4 * 4;
+            const int64_t gr = row_base + row;
+            st[u] = (gr < T && col < np) ? *reinterpret_cast<const float4*>(a.xhat + gr * np + col)
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto lstore = [&](float* xs) {
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int idx = tid + u * FT;
+            const int row = idx / (KC / 4), c4 = idx % (KC / 4);
+            *reinterpret_cast<float4*>(xs + row * L::LDX + c4 * 4) = st[u];
+        }
+    };
+
+    bool pre = false;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t row_base = tile * BT;
+
+        // FVP: this lane's cached activations for epilogues 1 / 2, fetched up front
+        float pa0[S1::NRW][S1::NCW][4], pa1[S2::NRW][S2::NCW][4];
+        if (MODE == FVP) {
+#pragma unroll
+            for (int i = 0; i < S1::NRW; ++i)
+#pragma unroll
+                for (int j = 0; j < S1::NCW; ++j)
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) {
+                        const int rb = S1::rb0(w) + i * S1::RBS;
+                        const int64_t gr = row_base + rb * 16 + 4 * q + rr;
+                        const int col = (S1::cb0(w) + j * S1::CBS) * 16 + r16;
+                        pa0[i][j][rr] = (rb < RB && gr < T) ? a.a0[gr * H0 + col] : 0.f;
+                    }
+#pragma unroll
+            for (int i = 0; i < S2::NRW; ++i)
+#pragma unroll
+                for (int j = 0; j < S2::NCW; ++j)
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) {
+                        const int rb = S2::rb0(w) + i * S2::RBS;
+                        const int64_t gr = row_base + rb * 16 + 4 * q + rr;
+                        const int col = (S2::cb0(w) + j * S2::CBS) * 16 + r16;
+                        pa1[i][j][rr] = (rb < RB && gr < T) ? a.a1[gr * H1 + col] : 0.f;
+                    }
+        }
+
+        // ---------------- phase 1: [64 x H0] = xhat * W0^T (or dW0^T) ----------------
+        floatx4 acc1[S1::NRW][S1::NCW];
+        zero_acc(acc1);
+        if (!pre) gload(row_base, 0);
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            float* xs = XS + (c & 1) * BT * L::LDX;
+            lstore(xs);
+            __syncthreads();
+            if (c + 1 < NCH) gload(row_base, c + 1);
+            const int kb = c * KC;
+            const int ke = kb + KC < np ? kb + KC : np;
+            gemm_tile(acc1, xs, L::LDX, kb, S1::rb0(w), S1::RBS, RB, V + pk.W0, np, S1::cb0(w), S1::CBS, kb, ke,
+                      lane);
+        }
+        // epilogue 1
+#pragma unroll
+        for (int i = 0; i < S1::NRW; ++i) {
+            const int rb = S1::rb0(w) + i * S1::RBS;
+            if (rb >= RB) continue;
+#pragma unroll
+            for (int j = 0; j < S1::NCW; ++j) {
+                const int col = (S1::cb0(w) + j * S1::CBS) * 16 + r16;
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    const int row = rb * 16 + 4 * q + rr;
+                    const int64_t gr = row_base + row;
+                    const float v = acc1[i][j][rr];
+                    if (MODE == FVP) {
+                        const float av = pa0[i][j][rr];
+                        D0[row * L::LD0 + col] = (1.f - av * av) * v;
+                        A0s[row * L::LD0 + col] = av;
+                    } else {
+                        const float av = tanhf(v);
+                        A0s[row * L::LD0 + col] = av;
+                        if (gr < T) a.a0[gr * H0 + col] = av;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+
+        // ---------------- phase 2: [64 x H1], K = H0 ----------------
+        {
+            floatx4 acc2[S2::NRW][S2::NCW];
+            zero_acc(acc2);
+            if (MODE == FVP) {
+                gemm_tile(acc2, D0, L::LD0, 0, S2::rb0(w), S2::RBS, RB, P + pk.W1, H0, S2::cb0(w), S2::CBS, 0, H0,
+                          lane);
+                gemm_tile(acc2, A0s, L::LD0, 0, S2::rb0(w), S2::RBS, RB, V + pk.W1, H0, S2::cb0(w), S2::CBS, 0,
+                          H0, lane);
+            } else {
+                gemm_tile(acc2, A0s, L::LD0, 0, S2::rb0(w), S2::RBS, RB, P + pk.W1, H0, S2::cb0(w), S2::CBS, 0, H0,
+                          lane);
+            }
+#pragma unroll
+            for (int i = 0; i < S2::NRW; ++i) {
+                const int rb = S2::rb0(w) + i * S2::RBS;
+                if (rb >= RB) continue;
+#pragma unroll
+                for (int j = 0; j < S2::NCW; ++j) {
+                    const int col = (S2::cb0(w) + j * S2::CBS) * 16 + r16;
+                    const float bias = V[pk.b1 + col];
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) {
+                        const int row = rb * 16 + 4 * q + rr;
+                        const int64_t gr = row_base + row;
+                        const float v = acc2[i][j][rr] + bias;
+                        if (MODE == FVP) {
+                            const float av = pa1[i][j][rr];
+                            D1[row * L::LD1 + col] = (1.f - av * av) * v;
+                            A1s[row * L::LD1 + col] = av;
+                        } else {
+                            const float av = tanhf(v);
+                            A1s[row * L::LD1 + col] = av;
+                            if (gr < T) a.a1[gr * H1 + col] = av;
+                        }
+                    }
+                }
+            }
+        }
+        __syncthreads();
+
+        // ---------------- phase 3: [64 x MP], K = H1 ----------------
+        {
+            floatx4 acc3[S3::NRW][S3::NCW];
+            zero_acc(acc3);
+            if (MODE == FVP) {
+                gemm_tile(acc3, D1, L::LD1, 0, S3::rb0(w), S3::RBS, RB, P + pk.W2, H1, S3::cb0(w), S3::CBS, 0, H1,
+                          lane);
+                gemm_tile(acc3, A1s, L::LD1, 0, S3::rb0(w), S3::RBS, RB, V + pk.W2, H1, S3::cb0(w), S3::CBS, 0,
+                          H1, lane);
+            } else {
+                gemm_tile(acc3, A1s, L::LD1, 0, S3::rb0(w), S3::RBS, RB, P + pk.W2, H1, S3::cb0(w), S3::CBS, 0, H1,
+                          lane);
+            }
+#pragma unroll
+            for (int i = 0; i < S3::NRW; ++i) {
+                const int rb = S3::rb0(w) + i * S3::RBS;
+                if (rb >= RB) continue;
+#pragma unroll
+                for (int j = 0; j < S3::NCW; ++j) {
+                    const int col = (S3::cb0(w) + j * S3::CBS) * 16 + r16;
+                    const float bias = V[pk.b2 + col];
+                    const float os = a.out_scale ? (col < m ? a.out_scale[col] : 1.f) : 1.f;
+                    const float osh = a.out_shift ? (col < m ? a.out_shift[col] : 0.f) : 0.f;
+                    float wq = 0.f;
+                    if (MODE == FVP) {
+                        const float sg = expf(P[pk.ls + col]);
+                        wq = os * os * (2.f / (2.f * sg * sg + 1e-8f));
+                    }
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) {
+                        const int row = rb * 16 + 4 * q + rr;
+                        const bool valid = row_base + row < T;
+                        const float v = acc3[i][j][rr] + bias;
+                        if (MODE == FVP)
+                            GPs[row * L::LDP + col] = (col < m && valid) ? wq * v : 0.f;
+                        else
+                            GPs[row * L::LDP + col] = col < m ? v * os + osh : 0.f;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+
+        // ---------------- FWD: log-likelihood, caches, VPG upstream ----------------
+        if (MODE == FWD) {
+            if (tid < BT) {
+                const int row = tid;
+                const int64_t gr = row_base + row;
+                float* gpr = GPs + row * L::LDP;
+                if (gr < T) {
+                    const float adv = a.adv_vpg[gr];
+                    float s2 = 0.f, sls = 0.f;
+                    for (int j = 0; j < m; ++j) {
+                        const float ls = P[pk.ls + j];
+                        const float sg = expf(ls);
+                        const float mu = gpr[j];
+                        const float zs = (a.act[gr * m + j] - mu) / sg;
+                        s2 += zs * zs;
+                        sls += ls;
+                        a.mu0[gr * m + j] = mu;
+                        LSs[row * MP + j] = adv * (zs * zs - 1.f);
+                        const float os = a.out_scale ? a.out_scale[j] : 1.f;
+                        gpr[j] = adv * (zs / sg) * os;
+                    }
+                    for (int j = m; j < MP; ++j) LSs[row * MP + j] = 0.f;
+                    a.ll0[gr] = ((-0.5f * s2) + (-sls)) + a.llc;
+                } else {
+                    for (int j = 0; j < MP; ++j) {
+                        gpr[j] = 0.f;
+                        LSs[row * MP + j] = 0.f;
+                    }
+                }
+            }
+            __syncthreads();
+            if (tid < MP) {
+                double s = 0.0;
+                for (int row = 0; row < BT; ++row) s += (double)LSs[row * MP + tid];
+                lsacc += s;
+            }
+            __syncthreads();
+        }
+
+        // ---------------- phase 4: gu1 = (1 - a1^2) (g W2) ----------------
+        {
+            floatx4 acc4[S2::NRW][S2::NCW];
+            zero_acc(acc4);
+            gemm_tile(acc4, GPs, L::LDP, 0, S2::rb0(w), S2::RBS, RB, P + pk.W2T, MP, S2::cb0(w), S2::CBS, 0, MP,
+                      lane);
+#pragma unroll
+            for (int i = 0; i < S2::NRW; ++i) {
+                const int rb = S2::rb0(w) + i * S2::RBS;
+                if (rb >= RB) continue;
+#pragma unroll
+                for (int j = 0; j < S2::NCW; ++j) {
+                    const int col = (S2::cb0(w) + j * S2::CBS) * 16 + r16;
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) {
+                        const int row = rb * 16 + 4 * q + rr;
+                        const float av = A1s[row * L::LD1 + col];
+                        D1[row * L::LD1 + col] = row_base + row < T ? (1.f - av * av) * acc4[i][j][rr] : 0.f;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+
+        // ---------------- phase 5: gu0 = (1 - a0^2) (gu1 W1) ----------------
+        {
+            floatx4 acc5[S1::NRW][S1::NCW];
+            zero_acc(acc5);
+            gemm_tile(acc5, D1, L::LD1, 0, S1::rb0(w), S1::RBS, RB, P + pk.W1T, H1, S1::cb0(w), S1::CBS, 0, H1,
+                      lane);
+#pragma unroll
+            for (int i = 0; i < S1::NRW; ++i) {
+                const int rb = S1::rb0(w) + i * S1::RBS;
+                if (rb >= RB) continue;
+#pragma unroll
+                for (int j = 0; j < S1::NCW; ++j) {
+                    const int col = (S1::cb0(w) + j * S1::CBS) * 16 + r16;
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) {
+                        const int row = rb * 16 + 4 * q + rr;
+                        const float av = A0s[row * L::LD0 + col];
+                        D0[row * L::LD0 + col] = row_base + row < T ? (1.f - av * av) * acc5[i][j][rr] : 0.f;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+
+        // ---------------- weight gradients, accumulated in registers ----------------
+        wgrad_lds(g2, GPs, L::LDP, A1s, L::LD1, W2S::rb0(w), W2S::RBS, MP / 16, W2S::cb0(w), W2S::CBS, H1 / 16,
+                  lane);
+        wgrad_lds(g1, D1, L::LD1, A0s, L::LD0, W1S::rb0(w), W1S::RBS, H1 / 16, W1S::cb0(w), W1S::CBS, H0 / 16,
+                  lane);
+        if (tid < H1) {
+            float s = 0.f;
+            for (int row = 0; row < BT; ++row) s += D1[row * L::LD1 + tid];
+            b1acc += s;
+        } else if (tid < H1 + MP) {
+            float s = 0.f;
+            for (int row = 0; row < BT; ++row) s += GPs[row * L::LDP + tid - H1];
+            b2acc += s;
+        }
+        // gW0 += gu0^T xhat: re-stream the tile's chunks (L2-hot); the last chunk
+        // prefetches the next tile's first chunk
+        const int64_t next = tile + gridDim.x;
+        gload(row_base, 0);
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            float* xs = XS + (c & 1) * BT * L::LDX;
+            lstore(xs);
+            __syncthreads();
+            if (c + 1 < NCH) {
+                gload(row_base, c + 1);
+            } else if (next < ntiles) {
+                gload(next * BT, 0);
+            }
+            const int kb_lim = (np - c * KC) / 16 < KC / 16 ? (np - c * KC) / 16 : KC / 16;
+            wgrad_lds(g0[c], D0, L::LD0, xs, L::LDX, W0S::rb0(w), W0S::RBS, H0 / 16, W0S::cb0(w), W0S::CBS,
+                      kb_lim, lane);
+        }
+        pre = next < ntiles;
+        __syncthreads();
+    }
+
+    // ---------------- this workgroup's slabs (k_gather layout, slice = blockIdx.x) ----------------
+    const int64_t blk = blockIdx.x;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+        for (int i = 0; i < W0S::NRW; ++i)
+#pragma unroll
+            for (int j = 0; j < W0S::NCW; ++j)
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    const int n = (W0S::rb0(w) + i * W0S::RBS) * 16 + 4 * q + rr;
+                    const int k = c * KC + (W0S::cb0(w) + j * W0S::CBS) * 16 + r16;
+                    if (n < H0 && k < np) o.wpart[o.off0 + (blk * H0 + n) * np + k] = g0[c][i][j][rr];
+                }
+#pragma unroll
+    for (int i = 0; i < W1S::NRW; ++i)
+#pragma unroll
+        for (int j = 0; j < W1S::NCW; ++j)
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int n = (W1S::rb0(w) + i * W1S::RBS) * 16 + 4 * q + rr;
+                const int k = (W1S::cb0(w) + j * W1S::CBS) * 16 + r16;
+                if (n < H1 && k < H0) o.wpart[o.off1 + (blk * H1 + n) * H0 + k] = g1[i][j][rr];
+            }
+#pragma unroll
+    for (int i = 0; i < W2S::NRW; ++i)
+#pragma unroll
+        for (int j = 0; j < W2S::NCW; ++j)
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int n = (W2S::rb0(w) + i * W2S::RBS) * 16 + 4 * q + rr;
+                const int k = (W2S::cb0(w) + j * W2S::CBS) * 16 + r16;
+                if (n < MP && k < H1) o.wpart[o.off2 + (blk * MP + n) * H1 + k] = g2[i][j][rr];
+            }
+    if (tid < H1)
+        o.wpart[o.boff1 + blk * H1 + tid] = b1acc;
+    else if (tid < H1 + MP)
+        o.wpart[o.boff2 + blk * MP + tid - H1] = b2acc;
+    if (MODE == FWD && tid < MP) a.rpart[blk * MP + tid] = lsacc;
+}
+
+}  // namespace

@@ -611,6 +611,12 @@ __global__ void __launch_bounds__(64) k_eval_final(const double* __restrict__ rp
     sums[1] = k;
 }
 
+}  // namespace
+
+#include "fused.h"
+
+namespace {
+
 // ---------------------------------------------------------------------------
 // host side: dispatch, grids, scratch sizes
 // ---------------------------------------------------------------------------
@@ -706,9 +712,91 @@ RowArgs row_args(const mjrl_shape* s, const mjrl_rows* r, int64_t T) {
     return ra;
 }
 
-int run_wgrad_gather(const mjrl_shape* s, const mjrl_rows* r, int64_t T, const mjrl_scratch* sc,
-                     const double* lspart, int G, const int32_t* done, float* gsum, hipStream_t st) {
-    const int S = sc->slices;
+bool fused_supported(const mjrl_shape* s) {
+    if (s->h0 != s->h1 || (s->h0 != 32 && s->h0 != 64)) return false;
+    if (s->mp != 16 && s->mp != 32) return false;
+    const int nch = (s->np + 63) / 64;
+    return nch >= 1 && nch <= 6;
+}
+
+inline int fused_grid(int64_t T) {
+    int64_t nt = (T + 63) / 64;
+    if (nt < 1) nt = 1;
+    return (int)(nt < FGRID_CAP ? nt : FGRID_CAP);
+}
+
+// slices of the weight-gradient slabs the accumulate step produces for (shape, T)
+inline int grad_slices(const mjrl_shape* s, int64_t T) {
+    return fused_supported(s) && T > 0 ? fused_grid(T) : wgrad_slices(T);
+}
+
+template <int H, int MP, int NCH, int MODE>
+int launch_fused_t(const RowArgs& ra, const FOut& fo, int grid, hipStream_t st) {
+    using L = FLayout<H, H, MP>;
+    auto fn = k_fused<H, H, MP, NCH, MODE>;
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, L::bytes);
+        if (e != hipSuccess) return (int)e;
+        attr = true;
+    }
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(FT), L::bytes, st, ra, fo);
+    return (int)hipGetLastError();
+}
+
+template <int MODE>
+int launch_fused(const mjrl_shape* s, const RowArgs& ra, const FOut& fo, int grid, hipStream_t st) {
+    const int nch = (s->np + 63) / 64;
+#define MJRL_F(H_, MP_, N_) \
+    if (s->h0 == H_ && s->mp == MP_ && nch == N_) return launch_fused_t<H_, MP_, N_, MODE>(ra, fo, grid, st);
+#define MJRL_FN(H_, MP_) MJRL_F(H_, MP_, 1) MJRL_F(H_, MP_, 2) MJRL_F(H_, MP_, 3) MJRL_F(H_, MP_, 4) \
+    MJRL_F(H_, MP_, 5) MJRL_F(H_, MP_, 6)
+    MJRL_FN(64, 16)
+    MJRL_FN(64, 32)
+    MJRL_FN(32, 16)
+    MJRL_FN(32, 32)
+#undef MJRL_FN
+#undef MJRL_F
+    return MJRL_ESHAPE;
+}
+
+int run_fused(int mode, const mjrl_shape* s, const mjrl_rows* r, int64_t T, const RowArgs& ra,
+              const mjrl_scratch* sc, hipStream_t st) {
+    const int G = fused_grid(T);
+    JobSet js = make_jobs(s, r, G);
+    FOut fo{};
+    fo.wpart = sc->wpart;
+    fo.off0 = js.job[0].off;
+    fo.off1 = js.job[1].off;
+    fo.boff1 = js.job[1].boff;
+    fo.off2 = js.job[2].off;
+    fo.boff2 = js.job[2].boff;
+    return mode == FWD ? launch_fused<FWD>(s, ra, fo, G, st) : launch_fused<FVP>(s, ra, fo, G, st);
+}
+
+int run_gather(const mjrl_shape* s, const mjrl_rows* r, int64_t T, const mjrl_scratch* sc, const double* lspart,
+               const int32_t* done, float* gsum, hipStream_t st) {
+    const int S = grad_slices(s, T);
+    JobSet js = make_jobs(s, r, S);
+    GArgs ga{};
+    ga.n = s->n; ga.m = s->m; ga.h0 = s->h0; ga.h1 = s->h1; ga.np = s->np; ga.mp = s->mp; ga.d = s->d; ga.S = S;
+    ga.off0 = js.job[0].off;
+    if (s->h0) {
+        ga.off1 = js.job[1].off; ga.boff1 = js.job[1].boff;
+        ga.off2 = js.job[2].off; ga.boff2 = js.job[2].boff;
+    }
+    ga.wpart = sc->wpart;
+    ga.lspart = lspart;
+    ga.G = fused_supported(s) && T > 0 ? fused_grid(T) : row_grid(s, T);
+    ga.gsum = gsum;
+    ga.done = done;
+    hipLaunchKernelGGL(k_gather, dim3((s->d + 255) / 256), dim3(256), 0, st, ga);
+    return (int)hipGetLastError();
+}
+
+int run_wgrad_only(const mjrl_shape* s, const mjrl_rows* r, int64_t T, const mjrl_scratch* sc, const int32_t* done,
+                   hipStream_t st) {
+    const int S = wgrad_slices(T);
     JobSet js = make_jobs(s, r, S);
     WArgs wa{};
     wa.njobs = js.njobs;
@@ -730,19 +818,6 @@ int run_wgrad_gather(const mjrl_shape* s, const mjrl_rows* r, int64_t T, const m
     } else {
         hipMemsetAsync(sc->wpart, 0, js.floats * sizeof(float), st);
     }
-    GArgs ga{};
-    ga.n = s->n; ga.m = s->m; ga.h0 = s->h0; ga.h1 = s->h1; ga.np = s->np; ga.mp = s->mp; ga.d = s->d; ga.S = S;
-    ga.off0 = js.job[0].off;
-    if (s->h0) {
-        ga.off1 = js.job[1].off; ga.boff1 = js.job[1].boff;
-        ga.off2 = js.job[2].off; ga.boff2 = js.job[2].boff;
-    }
-    ga.wpart = sc->wpart;
-    ga.lspart = lspart;
-    ga.G = G;
-    ga.gsum = gsum;
-    ga.done = done;
-    hipLaunchKernelGGL(k_gather, dim3((s->d + 255) / 256), dim3(256), 0, st, ga);
     return (int)hipGetLastError();
 }
 
@@ -775,7 +850,7 @@ int mjrl_shape_init(mjrl_shape* s, int32_t n, int32_t m, int32_t h0, int32_t h1)
 int mjrl_scratch_size(const mjrl_shape* s, int64_t T, int64_t* wpart_floats, int64_t* rpart_doubles,
                       int32_t* slices) {
     if (!s || T < 0 || !wpart_floats || !rpart_doubles || !slices) return MJRL_EINVAL;
-    const int S = wgrad_slices(T);
+    const int S = wgrad_slices(T) > fused_grid(T) ? wgrad_slices(T) : fused_grid(T);
     *slices = S;
     *wpart_floats = make_jobs(s, nullptr, S).floats;
     const int64_t rp = (int64_t)ROW_GRID_CAP * (s->mp > 2 ? s->mp : 2);
@@ -783,59 +858,74 @@ int mjrl_scratch_size(const mjrl_shape* s, int64_t T, int64_t* wpart_floats, int
     return MJRL_OK;
 }
 
-int mjrl_rows_vpg(const mjrl_shape* s, const mjrl_rows* rows, const float* packed_theta, const float* out_shift,
-                  const float* out_scale, const mjrl_scratch* sc, void* stream) {
+int mjrl_vpg_accumulate(const mjrl_shape* s, const mjrl_rows* rows, const float* packed_theta,
+                        const float* out_shift, const float* out_scale, const mjrl_scratch* sc, void* stream) {
     if (!rows_ok(s, rows) || !packed_theta || !sc || !rows->act || !rows->adv_vpg || !rows->mu0 || !rows->ll0)
         return MJRL_EINVAL;
     if (!shape_supported(s->h0, s->h1, s->mp)) return MJRL_ESHAPE;
     hipStream_t st = (hipStream_t)stream;
-    RowArgs ra = row_args(s, rows, rows->T);
+    const int64_t T = rows->T;
+    RowArgs ra = row_args(s, rows, T);
     ra.P = packed_theta;
     ra.out_shift = out_shift;
     ra.out_scale = out_scale;
     ra.rpart = sc->rpart;
-    const int G = row_grid(s, rows->T);
-    if (rows->T > 0) return launch_rows<FWD>(s, ra, G, st);
-    hipMemsetAsync(sc->rpart, 0, sizeof(double) * G * s->mp, st);
-    return (int)hipGetLastError();
+    if (T == 0) {
+        hipMemsetAsync(sc->wpart, 0, make_jobs(s, rows, grad_slices(s, 0)).floats * sizeof(float), st);
+        hipMemsetAsync(sc->rpart, 0, sizeof(double) * row_grid(s, 0) * s->mp, st);
+        return (int)hipGetLastError();
+    }
+    if (fused_supported(s)) return run_fused(FWD, s, rows, T, ra, sc, st);
+    int e = launch_rows<FWD>(s, ra, row_grid(s, T), st);
+    if (e) return e;
+    return run_wgrad_only(s, rows, T, sc, nullptr, st);
 }
 
-int mjrl_rows_fvp(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_fvp, const float* packed_theta,
-                  const float* packed_v, const float* out_scale, const int32_t* done, void* stream) {
-    if (!rows_ok(s, rows) || !packed_theta || !packed_v || T_fvp < 0 || T_fvp > rows->T) return MJRL_EINVAL;
+int mjrl_fvp_accumulate(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_fvp, const float* packed_theta,
+                        const float* packed_v, const float* out_scale, const int32_t* done, const mjrl_scratch* sc,
+                        void* stream) {
+    if (!rows_ok(s, rows) || !packed_theta || !packed_v || !sc || T_fvp < 0 || T_fvp > rows->T) return MJRL_EINVAL;
     if (!shape_supported(s->h0, s->h1, s->mp)) return MJRL_ESHAPE;
+    hipStream_t st = (hipStream_t)stream;
     RowArgs ra = row_args(s, rows, T_fvp);
     ra.P = packed_theta;
     ra.V = packed_v;
     ra.out_scale = out_scale;
     ra.done = done;
-    if (T_fvp > 0) return launch_rows<FVP>(s, ra, row_grid(s, T_fvp), (hipStream_t)stream);
-    return MJRL_OK;
+    if (T_fvp == 0) {
+        hipMemsetAsync(sc->wpart, 0, make_jobs(s, rows, grad_slices(s, 0)).floats * sizeof(float), st);
+        return (int)hipGetLastError();
+    }
+    if (fused_supported(s)) return run_fused(FVP, s, rows, T_fvp, ra, sc, st);
+    int e = launch_rows<FVP>(s, ra, row_grid(s, T_fvp), st);
+    if (e) return e;
+    return run_wgrad_only(s, rows, T_fvp, sc, done, st);
 }
 
-int mjrl_weight_grads(const mjrl_shape* s, const mjrl_rows* rows, int64_t T, const mjrl_scratch* sc,
+int mjrl_gather_grads(const mjrl_shape* s, const mjrl_rows* rows, int64_t T, const mjrl_scratch* sc,
                       int32_t with_log_std, const int32_t* done, float* gsum, void* stream) {
     if (!rows_ok(s, rows) || !sc || !gsum || T < 0 || T > rows->T) return MJRL_EINVAL;
     if (!shape_supported(s->h0, s->h1, s->mp)) return MJRL_ESHAPE;
-    return run_wgrad_gather(s, rows, T, sc, with_log_std ? sc->rpart : nullptr, row_grid(s, T), done, gsum,
-                            (hipStream_t)stream);
+    return run_gather(s, rows, T, sc, with_log_std ? sc->rpart : nullptr, done, gsum, (hipStream_t)stream);
 }
 
 int mjrl_policy_vpg(const mjrl_shape* s, const mjrl_rows* rows, const float* packed_theta, const float* out_shift,
                     const float* out_scale, const mjrl_scratch* sc, float* gsum, void* stream) {
-    int e = mjrl_rows_vpg(s, rows, packed_theta, out_shift, out_scale, sc, stream);
+    int e = mjrl_vpg_accumulate(s, rows, packed_theta, out_shift, out_scale, sc, stream);
     if (e) return e;
-    return mjrl_weight_grads(s, rows, rows->T, sc, 1, nullptr, gsum, stream);
+    return mjrl_gather_grads(s, rows, rows->T, sc, 1, nullptr, gsum, stream);
 }
 
 int mjrl_policy_fvp(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_fvp, const float* packed_theta,
                     const float* packed_v, const float* out_scale, const mjrl_scratch* sc, const int32_t* done,
                     float* gsum, void* stream) {
     if (!sc || !gsum) return MJRL_EINVAL;
-    int e = mjrl_rows_fvp(s, rows, T_fvp, packed_theta, packed_v, out_scale, done, stream);
+    int e = mjrl_fvp_accumulate(s, rows, T_fvp, packed_theta, packed_v, out_scale, done, sc, stream);
     if (e) return e;
-    return mjrl_weight_grads(s, rows, T_fvp, sc, 0, done, gsum, stream);
+    return mjrl_gather_grads(s, rows, T_fvp, sc, 0, done, gsum, stream);
 }
+
+int mjrl_fused_path(const mjrl_shape* s) { return s && fused_supported(s) ? 1 : 0; }
 
 int mjrl_policy_eval(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_eval, const float* packed_theta_new,
                      const float* packed_theta_old, const float* out_shift, const float* out_scale,

@@ -25,6 +25,18 @@ S_M1, S_M2, S_PM1, S_PM2, S_MS, S_MW1, S_MW2, S_EVAL = 0, 8, 16, 24, 32, 40, 48,
 N_STATS = 64
 
 
+def _linear_coeffs(baseline, n):
+    """Coefficients when `baseline` is a LinearBaseline (mjrl's or ours: same
+    features, baselines/linear_baseline.py:10-18) — None before its first fit —
+    or False when predict must run on the host."""
+    if baseline is None or type(baseline).__name__ != "LinearBaseline" or not hasattr(baseline, "_coeffs"):
+        return False
+    c = baseline._coeffs
+    if c is None:
+        return None
+    return c if len(c) == n + 4 else False
+
+
 class DeviceBatch:
     """One shard of trajectories in HBM — the hot path's input.
 
@@ -68,14 +80,23 @@ class DeviceBatch:
                     (T + T_demo, n))
         act = stage([p["actions"] for p in paths] + [p["actions"] for p in demo_paths or []], (T + T_demo, m))
         rew = stage([p["rewards"] for p in paths], (T,))
+        off = torch.from_numpy(np.concatenate([[0], np.cumsum(lengths)]).astype(np.int64)).to(device)
         if use_advantages:
             base = None
             adv = stage([p["advantages"] for p in paths], (T,))
+        elif _linear_coeffs(baseline, n) is not False:
+            # LinearBaseline.predict on the device (a4), reading the staged obs
+            coeffs = _linear_coeffs(baseline, n)
+            base = torch.zeros(T, dtype=torch.float64, device=device)
+            if coeffs is not None and T > 0:
+                c = torch.from_numpy(np.ascontiguousarray(coeffs, dtype=np.float64)).to(device)
+                _lib.check(_lib.lib().mjrl_linear_baseline(_lib.ptr(obs), T, n, _lib.ptr(off), len(paths), _lib.ptr(c),
+                                                           _lib.ptr(base), _lib.stream_ptr()), "mjrl_linear_baseline")
+            adv = None
         else:
             base = stage([baseline.predict(p) if baseline is not None else np.zeros(len(p["rewards"]))
                           for p in paths], (T,))
             adv = None
-        off = torch.from_numpy(np.concatenate([[0], np.cumsum(lengths)]).astype(np.int64)).to(device)
         term = torch.tensor([bool(p.get("terminated", False)) for p in paths], dtype=torch.uint8).to(device)
         b = cls(obs, act, rew, base, off, term, advantages=adv, T_demo=T_demo)
         b.lengths = lengths
@@ -107,7 +128,8 @@ class UpdateEngine:
         self.stats = torch.zeros(N_STATS, dtype=torch.float64, device=dev)
         self.mom_part = torch.zeros(4 * 256 + 16, dtype=torch.float64, device=dev)
         self.transforms = (None, None, None, None)
-        self.kernel_timing = None   # list -> (start, rows done, grads done) events per FVP
+        self.kernel_timing = None   # list -> (start, accumulate done, gather done) events per FVP
+        self.fused = bool(self.lib.mjrl_fused_path(C.byref(self.shape)))
 
     # ------------------------------------------------------------------
     def set_transformations(self, in_shift=None, in_scale=None, out_shift=None, out_scale=None):
@@ -306,13 +328,13 @@ class UpdateEngine:
                 if prof is not None:
                     e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
                     e0.record()
-                _lib.check(L.mjrl_rows_fvp(sp, C.byref(rows_fvp), T, _lib.ptr(self.packed_theta),
-                                           _lib.ptr(self.packed_p), _lib.ptr(osc), _lib.ptr(self.done), st),
-                           "mjrl_rows_fvp")
+                _lib.check(L.mjrl_fvp_accumulate(sp, C.byref(rows_fvp), T, _lib.ptr(self.packed_theta),
+                                                 _lib.ptr(self.packed_p), _lib.ptr(osc), _lib.ptr(self.done),
+                                                 C.byref(sc_fvp), st), "mjrl_fvp_accumulate")
                 if prof is not None:
                     e1.record()
-                _lib.check(L.mjrl_weight_grads(sp, C.byref(rows_fvp), T, C.byref(sc_fvp), 0, _lib.ptr(self.done),
-                                               _lib.ptr(v["gsum"]), st), "mjrl_weight_grads")
+                _lib.check(L.mjrl_gather_grads(sp, C.byref(rows_fvp), T, C.byref(sc_fvp), 0, _lib.ptr(self.done),
+                                               _lib.ptr(v["gsum"]), st), "mjrl_gather_grads")
                 if prof is not None:
                     e2.record()
                     prof.append((e0, e1, e2))

@@ -51,7 +51,7 @@ def test_shape_padding(lib, n, m, h, np_, mp, d):
     assert s.np >= n + 1 and s.np % 16 == 0        # bias column always present
     wf, rd, sl = C.c_int64(), C.c_int64(), C.c_int32()
     assert lib.mjrl_scratch_size(C.byref(s), 1000000, C.byref(wf), C.byref(rd), C.byref(sl)) == 0
-    assert 1 <= sl.value <= 128 and wf.value > 0 and rd.value > 0
+    assert 1 <= sl.value <= 256 and wf.value > 0 and rd.value > 0
 
 
 def test_unsupported_shape_is_rejected(lib):

@@ -112,9 +112,17 @@ def test_train_from_samples_fused_gae(name):
     paths = paths_of(c, with_adv=False)
     lam = None if np.isnan(c["gae_lambda"]) else float(c["gae_lambda"])
     stats = agent.train_from_samples(paths, float(c["gamma"]), lam)
+    from oracle import npg_cpu as O
     assert np.array_equal(np.concatenate([p["returns"] for p in paths]), c["returns"])
-    assert np.array_equal(np.concatenate([p["baseline"] for p in paths]), c["baseline"])
-    assert np.array_equal(np.concatenate([p["advantages"] for p in paths]), c["advantages"])
+    # the LinearBaseline prediction now runs on the device (rtol 1e-12 vs numpy's
+    # dgemv order); the GAE scan is bit-exact given those predictions
+    bl = np.concatenate([p["baseline"] for p in paths])
+    np.testing.assert_allclose(bl, c["baseline"], rtol=1e-12, atol=1e-12)
+    _, adv_ref = O.returns_and_advantages(c["rewards"], bl, c["lengths"], c["terminated"].astype(bool),
+                                          float(c["gamma"]), lam)
+    assert np.array_equal(np.concatenate([p["advantages"] for p in paths]), adv_ref)
+    np.testing.assert_allclose(np.concatenate([p["advantages"] for p in paths]), c["advantages"], rtol=1e-9,
+                               atol=1e-12)
     np.testing.assert_allclose(stats, c["base_stats"], rtol=1e-12)
     assert nrel(pol.get_param_values(), c["theta1"]) < tol(c, "theta", 1e-3)
 
@@ -272,3 +280,18 @@ def test_edge_cases_tiny_and_ragged():
         g = pol.flat_vpg(obs, act, O.whiten(adv))
         assert nrel(eng.vec["g"].cpu().numpy(), g) < 1e-5
         np.testing.assert_allclose(res["base_stats"], O.path_return_stats(rew, lengths), rtol=1e-12)
+
+
+def test_linear_baseline_predict_on_device():
+    """a4: LinearBaseline.predict computed on the device from the staged obs."""
+    from mjrl_amd.baselines.linear_baseline import LinearBaseline
+    from mjrl_amd.engine import DeviceBatch
+    from mjrl_amd.utils.gym_env import EnvSpec
+    c = load("c2_ragged")
+    base = LinearBaseline(EnvSpec(8, 2, 10, 1))
+    base._coeffs = c["baseline_coeffs"]
+    b = DeviceBatch.from_paths(paths_of(c, with_adv=False), torch.device("cuda:0"), baseline=base)
+    np.testing.assert_allclose(b.baseline.cpu().numpy(), c["baseline"], rtol=1e-12, atol=1e-12)
+    base._coeffs = None
+    b = DeviceBatch.from_paths(paths_of(c, with_adv=False), torch.device("cuda:0"), baseline=base)
+    assert np.array_equal(b.baseline.cpu().numpy(), np.zeros(c["baseline"].shape))

@@ -1,0 +1,466 @@
+// ks.h — persistent fused FWD / FVP / EVAL kernel for the MLP(64,64) policy with a
+// wide observation (NP = 32*KG, up to 384: Humanoid), included by policy.hip.
+//
+// One 512-thread workgroup (8 waves) per CU walks 32-row tiles of timesteps with
+// NO global load inside the tile loop except the next tile's xhat prefetch (and,
+// for FVP, the cached activations):
+//   - wave w owns hidden block cb = w&3 and observation half kh = w>>2: its slice of
+//     W0 (FWD / EVAL) or of the tangent dW0 (FVP) — 16 x NP/2 floats — lives in
+//     REGISTERS as MFMA B fragments for the whole launch, and so does its slice of
+//     the gW0 accumulator;
+//   - W1 / dW1 / W2 / dW2 live in LDS for the whole launch;
+//   - the 32-row xhat tile sits in LDS for both the first-layer GEMM and the gW0
+//     update; the next tile is prefetched into registers meanwhile.
+// Phase 1 computes per-half partial sums, folded through LDS; phases 2-5 are the
+// row chain of k_rows; gW1 / gW2 / biases accumulate in registers too.  Slabs
+// are written at the end in k_gather's layout.
+#pragma once
+
+namespace {
+
+constexpr int KT = 512;
+
+template <int MP, int KG>
+struct KLayout {
+    static constexpr int H = 64, BT = 32, RB = 2;
+    static constexpr int NP = 32 * KG, KH = NP / 2;
+    static constexpr int LDX = NP + 16;   // rows 4 apart fall 16 banks apart for the b32 gW0 reads
+    static constexpr int LD = H + 4, LDP = MP + 4;
+    static constexpr int oXT = 0;
+    static constexpr int oD0 = oXT + BT * LDX;
+    static constexpr int oA0 = oD0 + BT * LD;
+    static constexpr int oD1 = oA0 + BT * LD;
+    static constexpr int oA1 = oD1 + BT * LD;
+    static constexpr int oGP = oA1 + BT * LD;
+    static constexpr int oW1 = oGP + BT * LDP;     // [64][LD]  W1  (out x in)
+    static constexpr int odW1 = oW1 + H * LD;      // [64][LD]  dW1 (FVP)
+    static constexpr int oW2 = odW1 + H * LD;      // [MP][LD]  W2p
+    static constexpr int odW2 = oW2 + MP * LD;     // [MP][LD]  dW2p (FVP)
+    static constexpr int total = odW2 + MP * LD;
+    static constexpr int bytes = total * 4;
+    static_assert(bytes <= 160 * 1024, "LDS");
+    static constexpr int XPER = BT * NP / 4 / KT;  // float4 of the xhat tile per thread
+    static_assert(XPER * KT * 4 == BT * NP, "NP must be a multiple of 64");
+};
+
+// acc += A[rows][k] (LDS, row-major) x B where B(k, n) = Bs[n][k] (LDS, row-major by n)
+template <int NR>
+__device__ __forceinline__ void mm_lds_nk(floatx4 (&acc)[NR], const float* As, int lda, int rb0, int rbs,
+                                          const float* Bs, int ldb, int cb, int K, int lane) {
+    const int r = lane & 15, q = lane >> 4;
+#pragma unroll
+    for (int k = 0; k < K; k += 16) {
+        const float4 b = *reinterpret_cast<const float4*>(Bs + (cb * 16 + r) * ldb + k + 4 * q);
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+            const float4 a = *reinterpret_cast<const float4*>(As + ((rb0 + i * rbs) * 16 + r) * lda + k + 4 * q);
+            acc[i] = mfma_k16(a, b, acc[i]);
+        }
+    }
+}
+
+// acc += A[rows][k] (LDS) x B where B(k, n) = Bt[k][n] (LDS, row-major by k)
+template <int NR>
+__device__ __forceinline__ void mm_lds_kn(floatx4 (&acc)[NR], const float* As, int lda, int rb0, int rbs,
+                                          const float* Bt, int ldb, int cb, int K, int lane) {
+    const int r = lane & 15, q = lane >> 4;
+#pragma unroll
+    for (int k = 0; k < K; k += 16) {
+        float4 b;
+        b.x = Bt[(k + 4 * q + 0) * ldb + cb * 16 + r];
+        b.y = Bt[(k + 4 * q + 1) * ldb + cb * 16 + r];
+        b.z = Bt[(k + 4 * q + 2) * ldb + cb * 16 + r];
+        b.w = Bt[(k + 4 * q + 3) * ldb + cb * 16 + r];
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+            const float4 a = *reinterpret_cast<const float4*>(As + ((rb0 + i * rbs) * 16 + r) * lda + k + 4 * q);
+            acc[i] = mfma_k16(a, b, acc[i]);
+        }
+    }
+}
+
+template <int MP, int KG, int MODE>
+__global__ void __launch_bounds__(KT, 1) k_ks(RowArgs a, FOut o) {
+    using L = KLayout<MP, KG>;
+    constexpr int H = 64, BT = L::BT, NP = L::NP, KH = L::KH;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* XT = smem + L::oXT;
+    float* D0 = smem + L::oD0;
+    float* A0s = smem + L::oA0;
+    float* D1 = smem + L::oD1;
+    float* A1s = smem + L::oA1;
+    float* GPs = smem + L::oGP;
+    float* sW1 = smem + L::oW1;
+    float* sdW1 = smem + L::odW1;
+    float* sW2 = smem + L::oW2;
+    float* sdW2 = smem + L::odW2;
+    double* RED = reinterpret_cast<double*>(D0);   // EVAL: [2][BT] doubles (D0 unused in EVAL)
+    float* LSs = D1;                              // FWD: [BT][MP] (D1 unused before phase 4)
+
+    if (MODE == FVP && a.done && *a.done) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int r16 = lane & 15, q = lane >> 4;
+    const int cb = w & 3, kh = w >> 2;
+    const int m = a.m;
+    const int64_t T = a.T;
+    const int64_t ntiles = (T + BT - 1) / BT;
+    const float* P = a.P;
+    const Packed pk(H, H, NP, MP);
+    const float* W0src = (MODE == FVP ? a.V : P) + pk.W0;
+
+    // ---- launch preamble: weights to LDS, this wave's W0 / dW0 slice to registers ----
+    for (int i = tid; i < H * H; i += KT) {
+        const int row = i / H, col = i % H;
+        sW1[row * L::LD + col] = P[pk.W1 + i];
+        if (MODE == FVP) sdW1[row * L::LD + col] = a.V[pk.W1 + i];
+    }
+    for (int i = tid; i < MP * H; i += KT) {
+        const int row = i / H, col = i % H;
+        sW2[row * L::LD + col] = P[pk.W2 + i];
+        if (MODE == FVP) sdW2[row * L::LD + col] = a.V[pk.W2 + i];
+    }
+    float4 wb[KG];   // B fragments: W0[cb*16 + r][kh*KH + 16g + 4q .. +3]
+#pragma unroll
+    for (int g = 0; g < KG; ++g)
+        wb[g] = *reinterpret_cast<const float4*>(W0src + (cb * 16 + r16) * NP + kh * KH + 16 * g + 4 * q);
+
+    // accumulators (FWD / FVP)
+    floatx4 g0[KG];   // gW0[cb*16 ..][kh*KH + 16g ..]
+#pragma unroll
+    for (int g = 0; g < KG; ++g) g0[g] = zero4();
+    floatx4 g1[2];    // gW1 tiles (nb = cb, kb = kh + 2j)
+    g1[0] = zero4();
+    g1[1] = zero4();
+    floatx4 g2 = zero4();   // gW2 tile (nb = w>>2 < MP/16, kb = w&3)
+    float b1acc = 0.f, b2acc = 0.f;
+    double lsacc = 0.0, surr_acc = 0.0, kl_acc = 0.0;
+
+    // tile-invariant per-lane constants of the epilogues
+    const float bias1 = (MODE == FVP ? a.V : P)[pk.b1 + cb * 16 + r16];
+    const int cbo3 = w % (MP / 16), rb3 = w / (MP / 16);
+    const int col3 = cbo3 * 16 + r16;
+    const float bias3 = (MODE == FVP ? a.V : P)[pk.b2 + col3];
+    const float os3 = a.out_scale ? (col3 < m ? a.out_scale[col3] : 1.f) : 1.f;
+    const float osh3 = a.out_shift ? (col3 < m ? a.out_shift[col3] : 0.f) : 0.f;
+    float wq3 = 0.f;
+    if (MODE == FVP) {
+        const float sg = expf(P[pk.ls + col3]);
+        wq3 = os3 * os3 * (2.f / (2.f * sg * sg + 1e-8f));
+    }
+
+    float touch = 0.f;
+    float4 xr[L::XPER];
+    auto xload = [&](int64_t tile) {
+#pragma unroll
+        for (int u = 0; u < L::XPER; ++u) {
+            const int idx = tid + u * KT;
+            const int row = idx / (NP / 4), c4 = idx % (NP / 4);
+            const int64_t gr = tile * BT + row;
+            xr[u] = gr < T ? *reinterpret_cast<const float4*>(a.xhat + gr * NP + c4 * 4)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    __syncthreads();   // weights in LDS
+
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t row_base = tile * BT;
+        // ---- publish this tile's xhat (L2-warm from the previous tile's touch) ----
+        asm volatile("" ::"v"(touch));
+        xload(tile);
+#pragma unroll
+        for (int u = 0; u < L::XPER; ++u) {
+            const int idx = tid + u * KT;
+            const int row = idx / (NP / 4), c4 = idx % (NP / 4);
+            *reinterpret_cast<float4*>(XT + row * L::LDX + c4 * 4) = xr[u];
+        }
+        // FVP: cached activations for this lane's epilogue-1 / -2 elements
+        float pa0[2][4], pa1[4];
+        if (MODE == FVP) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    const int64_t gr = row_base + i * 16 + 4 * q + rr;
+                    pa0[i][rr] = (kh == 0 && gr < T) ? a.a0[gr * H + cb * 16 + r16] : 0.f;
+                }
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int64_t gr = row_base + kh * 16 + 4 * q + rr;
+                pa1[rr] = gr < T ? a.a1[gr * H + cb * 16 + r16] : 0.f;
+            }
+        }
+        __syncthreads();
+        // pull the next tile's xhat lines into L2 (one dword per 128-B line; the
+        // value is only kept alive until the next publish, 1 VGPR)
+        {
+            const int64_t nt = tile + gridDim.x;
+            constexpr int LPR = NP * 4 / 128;   // lines per row
+            if (nt < ntiles && tid < BT * LPR) {
+                const int64_t gr = nt * BT + tid / LPR;
+                if (gr < T) touch = a.xhat[gr * NP + (tid % LPR) * 32];
+            }
+        }
+
+        // ---- phase 1: partial [32 x 16] over this wave's observation half ----
+        floatx4 acc1[2] = {zero4(), zero4()};
+#pragma unroll
+        for (int g = 0; g < KG; ++g) {
+            const int k = kh * KH + 16 * g + 4 * q;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const float4 x = *reinterpret_cast<const float4*>(XT + (i * 16 + r16) * L::LDX + k);
+                acc1[i] = mfma_k16(x, wb[g], acc1[i]);
+            }
+            if ((g & 3) == 3) __builtin_amdgcn_sched_barrier(0);   // bound the hoisting of LDS reads
+        }
+        // fold the two halves: kh = 1 publishes, kh = 0 finishes
+        if (kh == 1) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) D0[(i * 16 + 4 * q + rr) * L::LD + cb * 16 + r16] = acc1[i][rr];
+        }
+        __syncthreads();
+        if (kh == 0) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    const int row = i * 16 + 4 * q + rr;
+                    const int col = cb * 16 + r16;
+                    const float v = acc1[i][rr] + D0[row * L::LD + col];
+                    const int64_t gr = row_base + row;
+                    if (MODE == FVP) {
+                        const float av = pa0[i][rr];
+                        D0[row * L::LD + col] = (1.f - av * av) * v;
+                        A0s[row * L::LD + col] = av;
+                    } else {
+                        const float av = tanhf(v);
+                        A0s[row * L::LD + col] = av;
+                        if (MODE == FWD && gr < T) a.a0[gr * H + col] = av;
+                    }
+                }
+        }
+        __syncthreads();
+
+        // ---- phase 2: [32 x 64], K = 64; wave -> (rb = kh, cb) ----
+        {
+            floatx4 acc[1] = {zero4()};
+            if (MODE == FVP) {
+                mm_lds_nk(acc, D0, L::LD, kh, 1, sW1, L::LD, cb, H, lane);
+                mm_lds_nk(acc, A0s, L::LD, kh, 1, sdW1, L::LD, cb, H, lane);
+            } else {
+                mm_lds_nk(acc, A0s, L::LD, kh, 1, sW1, L::LD, cb, H, lane);
+            }
+            const int col = cb * 16 + r16;
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int row = kh * 16 + 4 * q + rr;
+                const int64_t gr = row_base + row;
+                const float v = acc[0][rr] + bias1;
+                if (MODE == FVP) {
+                    const float av = pa1[rr];
+                    D1[row * L::LD + col] = (1.f - av * av) * v;
+                    A1s[row * L::LD + col] = av;
+                } else {
+                    const float av = tanhf(v);
+                    A1s[row * L::LD + col] = av;
+                    if (MODE == FWD && gr < T) a.a1[gr * H + col] = av;
+                }
+            }
+        }
+        __syncthreads();
+
+        // ---- phase 3: [32 x MP], K = 64; tiles (rb, cbo) over the first 2*MP/16 waves ----
+        if (w < 2 * (MP / 16)) {
+            floatx4 acc[1] = {zero4()};
+            if (MODE == FVP) {
+                mm_lds_nk(acc, D1, L::LD, rb3, 1, sW2, L::LD, cbo3, H, lane);
+                mm_lds_nk(acc, A1s, L::LD, rb3, 1, sdW2, L::LD, cbo3, H, lane);
+            } else {
+                mm_lds_nk(acc, A1s, L::LD, rb3, 1, sW2, L::LD, cbo3, H, lane);
+            }
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int row = rb3 * 16 + 4 * q + rr;
+                const bool valid = row_base + row < T;
+                const float v = acc[0][rr] + bias3;
+                if (MODE == FVP)
+                    GPs[row * L::LDP + col3] = (col3 < m && valid) ? wq3 * v : 0.f;
+                else
+                    GPs[row * L::LDP + col3] = col3 < m ? v * os3 + osh3 : 0.f;
+            }
+        }
+        __syncthreads();
+
+        // ---- per-row pass (FWD: log-lik, caches, VPG upstream; EVAL: LR, KL) ----
+        if (MODE != FVP) {
+            if (tid < BT) {
+                const int row = tid;
+                const int64_t gr = row_base + row;
+                float* gpr = GPs + row * L::LDP;
+                if (gr < T) {
+                    float s2 = 0.f, sls = 0.f;
+                    if (MODE == FWD) {
+                        const float adv = a.adv_vpg[gr];
+                        for (int j = 0; j < m; ++j) {
+                            const float ls = P[pk.ls + j];
+                            const float sg = expf(ls);
+                            const float mu = gpr[j];
+                            const float zs = (a.act[gr * m + j] - mu) / sg;
+                            s2 += zs * zs;
+                            sls += ls;
+                            a.mu0[gr * m + j] = mu;
+                            LSs[row * MP + j] = adv * (zs * zs - 1.f);
+                            const float os = a.out_scale ? a.out_scale[j] : 1.f;
+                            gpr[j] = adv * (zs / sg) * os;
+                        }
+                        for (int j = m; j < MP; ++j) LSs[row * MP + j] = 0.f;
+                        a.ll0[gr] = ((-0.5f * s2) + (-sls)) + a.llc;
+                    } else {
+                        float kl = 0.f;
+                        for (int j = 0; j < m; ++j) {
+                            const float lsn = P[pk.ls + j], lso = a.V[pk.ls + j];
+                            const float sn = expf(lsn), so = expf(lso);
+                            const float mun = gpr[j], muo = a.mu0[gr * m + j];
+                            const float zs = (a.act[gr * m + j] - mun) / sn;
+                            s2 += zs * zs;
+                            sls += lsn;
+                            const float dm = muo - mun;
+                            const float nr = (dm * dm + so * so) - sn * sn;
+                            const float dr = 2.f * sn * sn + 1e-8f;
+                            kl += (nr / dr + lsn) - lso;
+                        }
+                        const float lln = ((-0.5f * s2) + (-sls)) + a.llc;
+                        const float lr = expf(lln - a.ll0[gr]);
+                        RED[row] = (double)(lr * a.adv[gr]);
+                        RED[BT + row] = (double)kl;
+                    }
+                } else {
+                    if (MODE == FWD) {
+                        for (int j = 0; j < MP; ++j) {
+                            gpr[j] = 0.f;
+                            LSs[row * MP + j] = 0.f;
+                        }
+                    } else {
+                        RED[row] = 0.0;
+                        RED[BT + row] = 0.0;
+                    }
+                }
+            }
+            __syncthreads();
+            if (MODE == FWD) {
+                if (tid < MP) {
+                    double s = 0.0;
+                    for (int row = 0; row < BT; ++row) s += (double)LSs[row * MP + tid];
+                    lsacc += s;
+                }
+            } else if (tid == 0) {
+                double s = 0.0, k = 0.0;
+                for (int row = 0; row < BT; ++row) {
+                    s += RED[row];
+                    k += RED[BT + row];
+                }
+                surr_acc += s;
+                kl_acc += k;
+            }
+            __syncthreads();
+        }
+
+        if (MODE != EVAL) {
+            // ---- phase 4: gu1 = (1 - a1^2) (g W2); wave -> (rb = kh, cb) ----
+            {
+                floatx4 acc[1] = {zero4()};
+                mm_lds_kn(acc, GPs, L::LDP, kh, 1, sW2, L::LD, cb, MP, lane);
+                const int col = cb * 16 + r16;
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    const int row = kh * 16 + 4 * q + rr;
+                    const float av = A1s[row * L::LD + col];
+                    D1[row * L::LD + col] = row_base + row < T ? (1.f - av * av) * acc[0][rr] : 0.f;
+                }
+            }
+            __syncthreads();
+            // ---- phase 5: gu0 = (1 - a0^2) (gu1 W1) ----
+            {
+                floatx4 acc[1] = {zero4()};
+                mm_lds_kn(acc, D1, L::LD, kh, 1, sW1, L::LD, cb, H, lane);
+                const int col = cb * 16 + r16;
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    const int row = kh * 16 + 4 * q + rr;
+                    const float av = A0s[row * L::LD + col];
+                    D0[row * L::LD + col] = row_base + row < T ? (1.f - av * av) * acc[0][rr] : 0.f;
+                }
+            }
+            __syncthreads();
+            // ---- weight gradients (registers) ----
+#pragma unroll 1
+            for (int t = 0; t < BT; t += 4) {
+                const float gu = D0[(t + q) * L::LD + cb * 16 + r16];
+#pragma unroll
+                for (int g = 0; g < KG; ++g) {
+                    g0[g] = mfma4(gu, XT[(t + q) * L::LDX + kh * KH + 16 * g + r16], g0[g]);
+                    if ((g & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+                }
+                const float gu1 = D1[(t + q) * L::LD + cb * 16 + r16];
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    g1[j] = mfma4(gu1, A0s[(t + q) * L::LD + (kh + 2 * j) * 16 + r16], g1[j]);
+                if ((w >> 2) < MP / 16)
+                    g2 = mfma4(GPs[(t + q) * L::LDP + (w >> 2) * 16 + r16], A1s[(t + q) * L::LD + (w & 3) * 16 + r16],
+                               g2);
+            }
+            if (tid < H) {
+                float s = 0.f;
+                for (int row = 0; row < BT; ++row) s += D1[row * L::LD + tid];
+                b1acc += s;
+            } else if (tid < H + MP) {
+                float s = 0.f;
+                for (int row = 0; row < BT; ++row) s += GPs[row * L::LDP + tid - H];
+                b2acc += s;
+            }
+        }
+        __syncthreads();
+    }
+
+    const int64_t blk = blockIdx.x;
+    if (MODE == EVAL) {
+        if (tid == 0) {
+            a.rpart[blk * 2 + 0] = surr_acc;
+            a.rpart[blk * 2 + 1] = kl_acc;
+        }
+        return;
+    }
+#pragma unroll
+    for (int g = 0; g < KG; ++g)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            const int n = cb * 16 + 4 * q + rr;
+            const int k = kh * KH + 16 * g + r16;
+            o.wpart[o.off0 + (blk * H + n) * NP + k] = g0[g][rr];
+        }
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            const int n = cb * 16 + 4 * q + rr;
+            const int k = (kh + 2 * j) * 16 + r16;
+            o.wpart[o.off1 + (blk * H + n) * H + k] = g1[j][rr];
+        }
+    if ((w >> 2) < MP / 16) {
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            const int n = (w >> 2) * 16 + 4 * q + rr;
+            const int k = (w & 3) * 16 + r16;
+            o.wpart[o.off2 + (blk * MP + n) * H + k] = g2[rr];
+        }
+    }
+    if (tid < H)
+        o.wpart[o.boff1 + blk * H + tid] = b1acc;
+    else if (tid < H + MP)
+        o.wpart[o.boff2 + blk * MP + tid - H] = b2acc;
+    if (MODE == FWD && tid < MP) a.rpart[blk * MP + tid] = lsacc;
+}
+
+}  // namespace

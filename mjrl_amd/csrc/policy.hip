@@ -614,6 +614,7 @@ __global__ void __launch_bounds__(64) k_eval_final(const double* __restrict__ rp
 }  // namespace
 
 #include "fused.h"
+#include "ks.h"
 
 namespace {
 
@@ -725,9 +726,57 @@ inline int fused_grid(int64_t T) {
     return (int)(nt < FGRID_CAP ? nt : FGRID_CAP);
 }
 
+// the K-split kernel (ks.h): MLP(64,64), m <= 32, NP = 32 * KG, NP a multiple of 64
+bool ks_supported(const mjrl_shape* s) {
+    if (s->h0 != 64 || s->h1 != 64 || (s->mp != 16 && s->mp != 32) || s->np % 32) return false;
+    const int kg = s->np / 32;
+    return kg == 2 || kg == 4 || kg == 6 || kg == 8 || kg == 12;
+}
+
+inline int ks_grid(int64_t T) {
+    int64_t nt = (T + 31) / 32;
+    if (nt < 1) nt = 1;
+    return (int)(nt < FGRID_CAP ? nt : FGRID_CAP);
+}
+
+// which accumulate kernel runs for (shape, T): 2 = K-split, 1 = fused, 0 = rows + wgrad
+inline int acc_path(const mjrl_shape* s, int64_t T) {
+    if (T <= 0) return 0;
+    if (ks_supported(s)) return 2;
+    return fused_supported(s) ? 1 : 0;
+}
+
 // slices of the weight-gradient slabs the accumulate step produces for (shape, T)
 inline int grad_slices(const mjrl_shape* s, int64_t T) {
-    return fused_supported(s) && T > 0 ? fused_grid(T) : wgrad_slices(T);
+    const int p = acc_path(s, T);
+    return p == 2 ? ks_grid(T) : (p == 1 ? fused_grid(T) : wgrad_slices(T));
+}
+
+template <int MP, int KG, int MODE>
+int launch_ks_t(const RowArgs& ra, const FOut& fo, int grid, hipStream_t st) {
+    using L = KLayout<MP, KG>;
+    auto fn = k_ks<MP, KG, MODE>;
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, L::bytes);
+        if (e != hipSuccess) return (int)e;
+        attr = true;
+    }
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(KT), L::bytes, st, ra, fo);
+    return (int)hipGetLastError();
+}
+
+template <int MODE>
+int launch_ks(const mjrl_shape* s, const RowArgs& ra, const FOut& fo, int grid, hipStream_t st) {
+    const int kg = s->np / 32;
+#define MJRL_K(MP_, KG_) \
+    if (s->mp == MP_ && kg == KG_) return launch_ks_t<MP_, KG_, MODE>(ra, fo, grid, st);
+#define MJRL_KN(MP_) MJRL_K(MP_, 2) MJRL_K(MP_, 4) MJRL_K(MP_, 6) MJRL_K(MP_, 8) MJRL_K(MP_, 12)
+    MJRL_KN(16)
+    MJRL_KN(32)
+#undef MJRL_KN
+#undef MJRL_K
+    return MJRL_ESHAPE;
 }
 
 template <int H, int MP, int NCH, int MODE>
@@ -762,7 +811,8 @@ int launch_fused(const mjrl_shape* s, const RowArgs& ra, const FOut& fo, int gri
 
 int run_fused(int mode, const mjrl_shape* s, const mjrl_rows* r, int64_t T, const RowArgs& ra,
               const mjrl_scratch* sc, hipStream_t st) {
-    const int G = fused_grid(T);
+    const bool ks = acc_path(s, T) == 2;
+    const int G = ks ? ks_grid(T) : fused_grid(T);
     JobSet js = make_jobs(s, r, G);
     FOut fo{};
     fo.wpart = sc->wpart;
@@ -771,6 +821,11 @@ int run_fused(int mode, const mjrl_shape* s, const mjrl_rows* r, int64_t T, cons
     fo.boff1 = js.job[1].boff;
     fo.off2 = js.job[2].off;
     fo.boff2 = js.job[2].boff;
+    if (ks) {
+        if (mode == FWD) return launch_ks<FWD>(s, ra, fo, G, st);
+        if (mode == FVP) return launch_ks<FVP>(s, ra, fo, G, st);
+        return launch_ks<EVAL>(s, ra, fo, G, st);
+    }
     return mode == FWD ? launch_fused<FWD>(s, ra, fo, G, st) : launch_fused<FVP>(s, ra, fo, G, st);
 }
 
@@ -787,7 +842,10 @@ int run_gather(const mjrl_shape* s, const mjrl_rows* r, int64_t T, const mjrl_sc
     }
     ga.wpart = sc->wpart;
     ga.lspart = lspart;
-    ga.G = fused_supported(s) && T > 0 ? fused_grid(T) : row_grid(s, T);
+    {
+        const int p = acc_path(s, T);
+        ga.G = p == 2 ? ks_grid(T) : (p == 1 ? fused_grid(T) : row_grid(s, T));
+    }
     ga.gsum = gsum;
     ga.done = done;
     hipLaunchKernelGGL(k_gather, dim3((s->d + 255) / 256), dim3(256), 0, st, ga);
@@ -850,7 +908,8 @@ int mjrl_shape_init(mjrl_shape* s, int32_t n, int32_t m, int32_t h0, int32_t h1)
 int mjrl_scratch_size(const mjrl_shape* s, int64_t T, int64_t* wpart_floats, int64_t* rpart_doubles,
                       int32_t* slices) {
     if (!s || T < 0 || !wpart_floats || !rpart_doubles || !slices) return MJRL_EINVAL;
-    const int S = wgrad_slices(T) > fused_grid(T) ? wgrad_slices(T) : fused_grid(T);
+    int S = wgrad_slices(T) > fused_grid(T) ? wgrad_slices(T) : fused_grid(T);
+    if (ks_grid(T) > S) S = ks_grid(T);
     *slices = S;
     *wpart_floats = make_jobs(s, nullptr, S).floats;
     const int64_t rp = (int64_t)ROW_GRID_CAP * (s->mp > 2 ? s->mp : 2);
@@ -875,7 +934,7 @@ int mjrl_vpg_accumulate(const mjrl_shape* s, const mjrl_rows* rows, const float*
         hipMemsetAsync(sc->rpart, 0, sizeof(double) * row_grid(s, 0) * s->mp, st);
         return (int)hipGetLastError();
     }
-    if (fused_supported(s)) return run_fused(FWD, s, rows, T, ra, sc, st);
+    if (acc_path(s, T)) return run_fused(FWD, s, rows, T, ra, sc, st);
     int e = launch_rows<FWD>(s, ra, row_grid(s, T), st);
     if (e) return e;
     return run_wgrad_only(s, rows, T, sc, nullptr, st);
@@ -896,7 +955,7 @@ int mjrl_fvp_accumulate(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_fv
         hipMemsetAsync(sc->wpart, 0, make_jobs(s, rows, grad_slices(s, 0)).floats * sizeof(float), st);
         return (int)hipGetLastError();
     }
-    if (fused_supported(s)) return run_fused(FVP, s, rows, T_fvp, ra, sc, st);
+    if (acc_path(s, T_fvp)) return run_fused(FVP, s, rows, T_fvp, ra, sc, st);
     int e = launch_rows<FVP>(s, ra, row_grid(s, T_fvp), st);
     if (e) return e;
     return run_wgrad_only(s, rows, T_fvp, sc, done, st);
@@ -925,7 +984,7 @@ int mjrl_policy_fvp(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_fvp, c
     return mjrl_gather_grads(s, rows, T_fvp, sc, 0, done, gsum, stream);
 }
 
-int mjrl_fused_path(const mjrl_shape* s) { return s && fused_supported(s) ? 1 : 0; }
+int mjrl_fused_path(const mjrl_shape* s) { return s ? acc_path(s, 1) : 0; }
 
 int mjrl_policy_eval(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_eval, const float* packed_theta_new,
                      const float* packed_theta_old, const float* out_shift, const float* out_scale,
@@ -941,9 +1000,10 @@ int mjrl_policy_eval(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_eval,
     ra.out_shift = out_shift;
     ra.out_scale = out_scale;
     ra.rpart = sc->rpart;
-    const int G = row_grid(s, T_eval);
+    const bool ks = acc_path(s, T_eval) == 2;
+    const int G = ks ? ks_grid(T_eval) : row_grid(s, T_eval);
     if (T_eval > 0) {
-        int e = launch_rows<EVAL>(s, ra, G, st);
+        int e = ks ? run_fused(EVAL, s, rows, T_eval, ra, sc, st) : launch_rows<EVAL>(s, ra, G, st);
         if (e) return e;
     } else {
         hipMemsetAsync(sc->rpart, 0, sizeof(double) * 2 * G, st);

@@ -196,24 +196,35 @@ def main():
 
     # dominant-kernel roofline from the live events of the timed region
     ev = eng.kernel_timing
-    t_rows = np.mean([a.elapsed_time(b) for a, b, _ in ev]) / 1e3
-    t_grad = np.mean([b.elapsed_time(c) for _, b, c in ev]) / 1e3
+    t_acc = np.mean([a.elapsed_time(b) for a, b, _ in ev]) / 1e3
+    t_gat = np.mean([b.elapsed_time(c) for _, b, c in ev]) / 1e3
     fl = flops_per_row(N_OBS, N_ACT, *HIDDEN)
     rows_rank = batch.T
-    kern = {"rows_fvp": dict(avg_ms=t_rows * 1e3, tflops=fl["rows_fvp"] * rows_rank / t_rows / 1e12),
-            "weight_grads": dict(avg_ms=t_grad * 1e3, tflops=fl["weight_grads"] * rows_rank / t_grad / 1e12)}
+    path = eng.accumulate_path()
+    np_ = eng.shape.np
+    if path == 0:   # rows kernel then split-K weight-gradient kernel: time each
+        acc_name, acc_key, acc_fl = "k_rows<64,64,32,FVP>", "k_rows<64, 64, 32, 1>", fl["rows_fvp"]
+        gat_name, gat_key, gat_fl = "k_wgrad", "k_wgrad", fl["weight_grads"]
+    else:           # one persistent kernel does both; the gather is a pure slab reduction
+        mp = eng.shape.mp
+        acc_name = ("k_ks<%d,%d,FVP>" % (mp, np_ // 32)) if path == 2 else "k_fused<64,64,%d,FVP>" % mp
+        acc_key = ("k_ks<%d, %d, 1>" % (mp, np_ // 32)) if path == 2 else "k_fused<"
+        acc_fl = fl["rows_fvp"] + fl["weight_grads"]
+        gat_name, gat_key, gat_fl = "k_gather", "k_gather", 0
+    kern = {acc_name: dict(avg_ms=t_acc * 1e3, tflops=acc_fl * rows_rank / t_acc / 1e12),
+            gat_name: dict(avg_ms=t_gat * 1e3, tflops=gat_fl * rows_rank / t_gat / 1e12)}
     dom = max(kern, key=lambda k: kern[k]["avg_ms"])
-    traffic, tsrc = pmc_traffic("k_rows<64, 64, 32, 1>" if dom == "rows_fvp" else "k_wgrad")
+    traffic, tsrc = pmc_traffic(acc_key if dom == acc_name else gat_key)
     if traffic is not None and world > 1:
         traffic = traffic * rows_rank / T_total    # the committed PMC pass is the 1-GPU (1M-row) launch
-    roof = dict(bound="mfma", kernel="k_rows<64,64,32,FVP>" if dom == "rows_fvp" else "k_wgrad",
+    roof = dict(bound="mfma", kernel=dom,
                 achieved=round(kern[dom]["tflops"], 3), peak=PEAK_F32_MFMA, unit="TFLOP/s",
                 frac=round(kern[dom]["tflops"] / PEAK_F32_MFMA, 4),
                 traffic=None if traffic is None else round(traffic),
                 traffic_unit="bytes/launch (HBM, PMC)", traffic_source=tsrc,
                 traffic_GBps=None if traffic is None else round(traffic / (kern[dom]["avg_ms"] * 1e-3) / 1e9, 1),
-                flops_per_timestep=fl[dom], rows_per_launch=rows_rank, launches=len(ev),
-                kernels={k: {kk: round(vv, 4) for kk, vv in v.items()} for k, v in kern.items()})
+                flops_per_timestep=acc_fl if dom == acc_name else gat_fl, rows_per_launch=rows_rank,
+                launches=len(ev), kernels={k: {kk: round(vv, 4) for kk, vv in v.items()} for k, v in kern.items()})
 
     if rank == 0:
         ms = elapsed / args.steps * 1e3

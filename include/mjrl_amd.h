@@ -173,6 +173,10 @@ int mjrl_fvp_accumulate(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_fv
 int mjrl_gather_grads(const mjrl_shape* s, const mjrl_rows* rows, int64_t T,
                       const mjrl_scratch* sc, int32_t with_log_std, const int32_t* done,
                       float* gsum, void* stream);
+/* Which accumulate kernel mjrl_{vpg,fvp}_accumulate run for this shape:
+ * 2 = K-split persistent (MLP(64,64), act_dim <= 32, np % 32 == 0),
+ * 1 = fused persistent (hidden 32/64), 0 = row kernel + split-K weight gradients.
+ * The gather and the results do not depend on it. */
 int mjrl_fused_path(const mjrl_shape* s);
 
 /* ---- conjugate gradient on device (cg_solve.py:3-22) ----

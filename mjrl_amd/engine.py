@@ -426,6 +426,11 @@ class UpdateEngine:
         return result
 
     # ------------------------------------------------------------------
+    def accumulate_path(self):
+        """Accumulate kernel the dispatcher runs for this shape: 2 = K-split
+        persistent (k_ks), 1 = fused persistent (k_fused), 0 = k_rows + k_wgrad."""
+        return int(self.lib.mjrl_fused_path(C.byref(self.shape)))
+
     def fvp(self, v, damping=1e-4, T=None):
         """F v + damping v at the parameters of the last update's forward pass
         (the caches a0/a1/mu0 and packed_theta of that pass) — NPG.HVP

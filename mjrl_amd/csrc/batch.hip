@@ -43,86 +43,136 @@ __global__ void __launch_bounds__(256) k_pack_batch(const double* __restrict__ o
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < na; i += stride) act32[i] = (float)act[i];
 }
 
-// Two lanes per path: the even lane runs the reverse recurrences (returns and GAE
-// advantages), the odd lane the forward path-return sum.  fp64 with separate
-// multiply and add (__dmul_rn / __dadd_rn cannot be contracted): bit-identical
-// to discount_sum.  The serial chain is short (a dependent mul+add per step);
-// what costs is memory latency, so each lane streams its path in 16-step chunks
-// through registers, the next chunk's loads in flight while this one is scanned.
-constexpr int GCH = 16;
+// One wave per path.  The path's rewards and baselines come into LDS with
+// coalesced loads, in windows of GW steps; lane 0 runs the serial fp64 chains out
+// of LDS (separate multiply and add, __dmul_rn / __dadd_rn cannot be contracted:
+// bit-identical to discount_sum), writing returns / advantages back in place; the
+// wave then stores the window with coalesced writes.  Paths longer than a window
+// are walked window by window (forward for the path-return sum, backward for the
+// recurrences), carrying the chain state across windows.
+constexpr int GW = 1024;           // steps per LDS window
 
-__global__ void __launch_bounds__(64) k_gae(const double* __restrict__ rew, const double* __restrict__ base,
-                                            const int64_t* __restrict__ off, const uint8_t* __restrict__ term,
-                                            int64_t P, double gamma, double gl, int use_gae,
-                                            double* __restrict__ ret, double* __restrict__ adv,
-                                            double* __restrict__ path_ret) {
-    const int64_t lane_id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t p = lane_id >> 1;
-    if (p >= P) return;
-    const int64_t b = off[p], e = off[p + 1];
-    if (lane_id & 1) {
+// LDS written by some lanes of a wave and read by others: order the accesses
+// (waitcnt + compiler barrier) without a workgroup barrier.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+constexpr int GAE_WAVES = 4;       // waves (paths in flight) per workgroup
+constexpr int GU = 8;              // serial steps per batch of LDS reads
+
+__global__ void __launch_bounds__(64 * GAE_WAVES) k_gae(const double* __restrict__ rew,
+                                                        const double* __restrict__ base,
+                                                        const int64_t* __restrict__ off,
+                                                        const uint8_t* __restrict__ term, int64_t P, double gamma,
+                                                        double gl, int use_gae, double* __restrict__ ret,
+                                                        double* __restrict__ adv, double* __restrict__ path_ret) {
+    __shared__ double sr[GAE_WAVES][GW];
+    __shared__ double sb[GAE_WAVES][GW];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    double* R = sr[w];
+    double* B = sb[w];
+    for (int64_t p = (int64_t)blockIdx.x * GAE_WAVES + w; p < P; p += (int64_t)gridDim.x * GAE_WAVES) {
+        const int64_t b = off[p], e = off[p + 1];
         // sum(p["rewards"]) — Python's builtin sum, front to back (npg_cg.py:97)
         double s = 0.0;
-        double x[GCH];
-        for (int64_t t0 = b; t0 < e; t0 += GCH) {
-            const int cnt = e - t0 < GCH ? (int)(e - t0) : GCH;
+        for (int64_t w0 = b; w0 < e; w0 += GW) {
+            const int cnt = e - w0 < GW ? (int)(e - w0) : GW;
+            {
+                double x[GW / 64];   // all of the lane's loads in flight at once
 #pragma unroll
-            for (int i = 0; i < GCH; ++i) x[i] = i < cnt ? rew[t0 + i] : 0.0;
+                for (int k = 0; k < GW / 64; ++k) x[k] = lane + 64 * k < cnt ? rew[w0 + lane + 64 * k] : 0.0;
 #pragma unroll
-            for (int i = 0; i < GCH; ++i)
-                if (i < cnt) s = __dadd_rn(s, x[i]);
+                for (int k = 0; k < GW / 64; ++k)
+                    if (lane + 64 * k < cnt) R[lane + 64 * k] = x[k];
+            }
+            wave_sync();
+            if (lane == 0) {
+                int i = 0;
+                for (; i + GU <= cnt; i += GU) {
+                    double x[GU];
+#pragma unroll
+                    for (int u = 0; u < GU; ++u) x[u] = R[i + u];
+#pragma unroll
+                    for (int u = 0; u < GU; ++u) s = __dadd_rn(s, x[u]);
+                }
+                for (; i < cnt; ++i) s = __dadd_rn(s, R[i]);
+            }
+            wave_sync();
         }
-        path_ret[p] = s;
-        return;
-    }
-    if (e <= b) return;
-    // returns: discount_sum(rewards, gamma) (process_samples.py:3-5, 37-44)
-    // GAE (process_samples.py:21-29): b1 = append(b, 0 if terminated else b[-1]),
-    // td = r + gamma*b1[1:] - b1[:-1], adv = discount_sum(td, gamma*lambda);
-    // plain advantages (process_samples.py:10-13): ret - baseline.
-    double acc_r = 0.0, acc_a = 0.0;
-    double bnext = term[p] ? 0.0 : base[e - 1];
-    double rc[GCH], bc[GCH], rn[GCH], bn[GCH];
-    int64_t t1 = e;                                   // current chunk is [t0, t1)
-    int64_t t0 = t1 - GCH > b ? t1 - GCH : b;
+        if (lane == 0) path_ret[p] = s;
+        if (e <= b) continue;
+        // returns: discount_sum(rewards, gamma) (process_samples.py:3-5, 37-44)
+        // GAE (process_samples.py:21-29): b1 = append(b, 0 if terminated else b[-1]),
+        // td = r + gamma*b1[1:] - b1[:-1], adv = discount_sum(td, gamma*lambda);
+        // plain advantages (process_samples.py:10-13): ret - baseline.
+        double acc_r = 0.0, acc_a = 0.0;
+        double bnext = term[p] ? 0.0 : base[e - 1];
+        for (int64_t w1 = e; w1 > b; w1 -= GW) {
+            const int64_t w0 = w1 - GW > b ? w1 - GW : b;
+            const int cnt = (int)(w1 - w0);
+            {
+                // a one-window path still has its rewards in R from the sum above
+                const bool reload = e - b > GW;
+                double x[GW / 64], y[GW / 64];
 #pragma unroll
-    for (int i = 0; i < GCH; ++i) {
-        const int64_t t = t0 + i;
-        rc[i] = t < t1 ? rew[t] : 0.0;
-        bc[i] = t < t1 ? base[t] : 0.0;
-    }
-    while (true) {
-        const int64_t n1 = t0, n0 = n1 - GCH > b ? n1 - GCH : b;   // next chunk [n0, n1)
+                for (int k = 0; k < GW / 64; ++k) {
+                    const bool in = lane + 64 * k < cnt;
+                    x[k] = in && reload ? rew[w0 + lane + 64 * k] : 0.0;
+                    y[k] = in ? base[w0 + lane + 64 * k] : 0.0;
+                }
 #pragma unroll
-        for (int i = 0; i < GCH; ++i) {
-            const int64_t t = n0 + i;
-            rn[i] = t < n1 ? rew[t] : 0.0;
-            bn[i] = t < n1 ? base[t] : 0.0;
-        }
-        const int cnt = (int)(t1 - t0);
+                for (int k = 0; k < GW / 64; ++k)
+                    if (lane + 64 * k < cnt) {
+                        if (reload) R[lane + 64 * k] = x[k];
+                        B[lane + 64 * k] = y[k];
+                    }
+            }
+            wave_sync();
+            if (lane == 0) {
+                int i = cnt;
+                for (; i >= GU; i -= GU) {   // steps i-1 .. i-GU
+                    double r[GU], bb[GU];
 #pragma unroll
-        for (int i = GCH - 1; i >= 0; --i) {
-            if (i < cnt) {
-                const int64_t t = t0 + i;
-                acc_r = __dadd_rn(rc[i], __dmul_rn(gamma, acc_r));
-                ret[t] = acc_r;
-                if (use_gae) {
-                    const double td = __dsub_rn(__dadd_rn(rc[i], __dmul_rn(gamma, bnext)), bc[i]);
-                    acc_a = __dadd_rn(td, __dmul_rn(gl, acc_a));
-                    adv[t] = acc_a;
-                    bnext = bc[i];
-                } else {
-                    adv[t] = __dsub_rn(acc_r, bc[i]);
+                    for (int u = 0; u < GU; ++u) {
+                        r[u] = R[i - 1 - u];
+                        bb[u] = B[i - 1 - u];
+                    }
+#pragma unroll
+                    for (int u = 0; u < GU; ++u) {
+                        acc_r = __dadd_rn(r[u], __dmul_rn(gamma, acc_r));
+                        R[i - 1 - u] = acc_r;
+                        if (use_gae) {
+                            const double td = __dsub_rn(__dadd_rn(r[u], __dmul_rn(gamma, bnext)), bb[u]);
+                            acc_a = __dadd_rn(td, __dmul_rn(gl, acc_a));
+                            B[i - 1 - u] = acc_a;
+                            bnext = bb[u];
+                        } else {
+                            B[i - 1 - u] = __dsub_rn(acc_r, bb[u]);
+                        }
+                    }
+                }
+                for (; i > 0; --i) {
+                    const double r = R[i - 1], bb = B[i - 1];
+                    acc_r = __dadd_rn(r, __dmul_rn(gamma, acc_r));
+                    R[i - 1] = acc_r;
+                    if (use_gae) {
+                        const double td = __dsub_rn(__dadd_rn(r, __dmul_rn(gamma, bnext)), bb);
+                        acc_a = __dadd_rn(td, __dmul_rn(gl, acc_a));
+                        B[i - 1] = acc_a;
+                        bnext = bb;
+                    } else {
+                        B[i - 1] = __dsub_rn(acc_r, bb);
+                    }
                 }
             }
-        }
-        if (t0 <= b) break;
-        t1 = n1;
-        t0 = n0;
-#pragma unroll
-        for (int i = 0; i < GCH; ++i) {
-            rc[i] = rn[i];
-            bc[i] = bn[i];
+            wave_sync();
+            for (int i = lane; i < cnt; i += 64) {
+                ret[w0 + i] = R[i];
+                adv[w0 + i] = B[i];
+            }
+            wave_sync();
         }
     }
 }
@@ -170,23 +220,33 @@ __global__ void __launch_bounds__(MOM_THREADS) k_moments_part(const T* __restric
     }
 }
 
-// Moments pass 2: one workgroup folds the block partials in block order.
+// Moments pass 2: one wave folds the block partials — lane l takes blocks
+// l, l+64, ... in order, then a fixed shuffle tree (deterministic).
 __global__ void __launch_bounds__(64) k_moments_final(const double* __restrict__ part, int nb, int64_t N,
                                                       double* __restrict__ out) {
-    if (threadIdx.x != 0) return;
+    const int lane = threadIdx.x;
     double s1 = 0.0, s2 = 0.0, mn = __builtin_inf(), mx = -__builtin_inf();
-    for (int b = 0; b < nb; ++b) {
+    for (int b = lane; b < nb; b += 64) {
         s1 += part[b * 4 + 0];
         s2 += part[b * 4 + 1];
         mn = fmin(mn, part[b * 4 + 2]);
         mx = fmax(mx, part[b * 4 + 3]);
     }
-    out[0] = s1;
-    out[1] = s2;
-    out[2] = (double)N;
-    out[3] = mn;
-    out[4] = mx;
-    out[5] = -mn;   // so one MAX all-reduce over out[4..5] gives the global extrema
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mn = fmin(mn, __shfl_xor(mn, o, 64));
+        mx = fmax(mx, __shfl_xor(mx, o, 64));
+    }
+    if (lane == 0) {
+        out[0] = s1;
+        out[1] = s2;
+        out[2] = (double)N;
+        out[3] = mn;
+        out[4] = mx;
+        out[5] = -mn;   // so one MAX all-reduce over out[4..5] gives the global extrema
+    }
 }
 
 // adv32 = float((adv - mean) / (std + 1e-6)) (npg_cg.py:91; .float() at batch_reinforce.py:38)
@@ -286,8 +346,9 @@ int mjrl_gae(const double* rew, const double* base, const int64_t* path_off, con
         return MJRL_EINVAL;
     if (P == 0) return MJRL_OK;
     const double gl = gamma * gae_lambda;   // python: gamma*gae_lambda (process_samples.py:29)
-    hipLaunchKernelGGL(k_gae, dim3((unsigned)((2 * P + 63) / 64)), dim3(64), 0, (hipStream_t)stream, rew, base, path_off,
-                       terminated, P, gamma, gl, use_gae, ret, adv, path_ret);
+    const int64_t g = (P + GAE_WAVES - 1) / GAE_WAVES;
+    hipLaunchKernelGGL(k_gae, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(64 * GAE_WAVES), 0, (hipStream_t)stream, rew,
+                       base, path_off, terminated, P, gamma, gl, use_gae, ret, adv, path_ret);
     return err(hipGetLastError());
 }
 

@@ -15,6 +15,7 @@ using namespace mjrl;
 namespace {
 
 constexpr int CG_THREADS = 1024;
+constexpr int CG_U = 8;   // elements per thread per chunk of a pass
 
 struct PackMap {
     int n, m, h0, h1, np, mp;
@@ -109,39 +110,80 @@ __global__ void __launch_bounds__(CG_THREADS) k_cg_step(mjrl_shape s, const floa
     __shared__ double red[CG_THREADS / 64];
     if (*done) return;
     const PackMap pm(s);
-    const int ls0 = s.d - s.m;
+    const int ls0 = s.d - s.m, d = s.d, tid = threadIdx.x;
+    constexpr int CH = CG_THREADS * CG_U;
+    // each pass walks d in chunks of CG_U elements per thread, all loads of a
+    // chunk issued before use (the single workgroup is latency-bound otherwise)
     double acc = 0.0;
-    for (int f = threadIdx.x; f < s.d; f += CG_THREADS) {
-        const float pf = p[f];
-        float hv;
-        if (f >= ls0) {
-            const float sg = expf(packed_theta[pm.pk.ls + (f - ls0)]);
-            const double u = (double)sg * (double)sg;
-            const double c = 4.0 * u * (2.0 * u - 1e-8) / ((2.0 * u + 1e-8) * (2.0 * u + 1e-8));
-            hv = (float)(c * (double)pf);
-        } else {
-            hv = (float)((double)gsum[f] * inv_T);
+    for (int f0 = 0; f0 < d; f0 += CH) {
+        float pf[CG_U], gv[CG_U];
+#pragma unroll
+        for (int u = 0; u < CG_U; ++u) {
+            const int f = f0 + u * CG_THREADS + tid;
+            pf[u] = f < d ? p[f] : 0.f;
+            gv[u] = f < ls0 ? gsum[f] : (f < d ? packed_theta[pm.pk.ls + (f - ls0)] : 0.f);
         }
-        const float zf = __fadd_rn(hv, __fmul_rn(damping, pf));   // hvp_flat + regu_coef*vector
-        z[f] = zf;
-        acc += (double)pf * (double)zf;
+#pragma unroll
+        for (int u = 0; u < CG_U; ++u) {
+            const int f = f0 + u * CG_THREADS + tid;
+            if (f >= d) continue;
+            float hv;
+            if (f >= ls0) {
+                const float sg = expf(gv[u]);
+                const double uu = (double)sg * (double)sg;
+                const double c = 4.0 * uu * (2.0 * uu - 1e-8) / ((2.0 * uu + 1e-8) * (2.0 * uu + 1e-8));
+                hv = (float)(c * (double)pf[u]);
+            } else {
+                hv = (float)((double)gv[u] * inv_T);
+            }
+            const float zf = __fadd_rn(hv, __fmul_rn(damping, pf[u]));   // hvp_flat + regu_coef*vector
+            z[f] = zf;
+            acc += (double)pf[u] * (double)zf;
+        }
     }
     const float pz = (float)block_sum1024(acc, red);
     const float rdotr = cg[0];
     const float v = rdotr / pz;
     acc = 0.0;
-    for (int f = threadIdx.x; f < s.d; f += CG_THREADS) {
-        x[f] = __fadd_rn(x[f], __fmul_rn(v, p[f]));
-        const float rf = __fsub_rn(r[f], __fmul_rn(v, z[f]));
-        r[f] = rf;
-        acc += (double)rf * (double)rf;
+    for (int f0 = 0; f0 < d; f0 += CH) {
+        float xv[CG_U], pv[CG_U], rv[CG_U], zv[CG_U];
+#pragma unroll
+        for (int u = 0; u < CG_U; ++u) {
+            const int f = f0 + u * CG_THREADS + tid;
+            const bool in = f < d;
+            xv[u] = in ? x[f] : 0.f;
+            pv[u] = in ? p[f] : 0.f;
+            rv[u] = in ? r[f] : 0.f;
+            zv[u] = in ? z[f] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < CG_U; ++u) {
+            const int f = f0 + u * CG_THREADS + tid;
+            if (f >= d) continue;
+            x[f] = __fadd_rn(xv[u], __fmul_rn(v, pv[u]));
+            const float rf = __fsub_rn(rv[u], __fmul_rn(v, zv[u]));
+            r[f] = rf;
+            acc += (double)rf * (double)rf;
+        }
     }
     const float rr = (float)block_sum1024(acc, red);
     const float mu = rr / rdotr;
-    for (int f = threadIdx.x; f < s.d; f += CG_THREADS) {
-        const float pf = __fadd_rn(r[f], __fmul_rn(mu, p[f]));
-        p[f] = pf;
-        pack_one(pm, f, pf, packed_p, false, 0.f);
+    for (int f0 = 0; f0 < d; f0 += CH) {
+        float pv[CG_U], rv[CG_U];
+#pragma unroll
+        for (int u = 0; u < CG_U; ++u) {
+            const int f = f0 + u * CG_THREADS + tid;
+            pv[u] = f < d ? p[f] : 0.f;
+            rv[u] = f < d ? r[f] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < CG_U; ++u) {
+            const int f = f0 + u * CG_THREADS + tid;
+            if (f >= d) continue;
+            const float pf = __fadd_rn(rv[u], __fmul_rn(mu, pv[u]));
+            p[f] = pf;
+            pack_one(pm, f, pf, packed_p, false, 0.f);
+        }
     }
     __syncthreads();
     if (threadIdx.x == 0) {

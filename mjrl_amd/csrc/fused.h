@@ -97,7 +97,6 @@ __global__ void __launch_bounds__(FT, 1) k_fused(RowArgs a, FOut o) {
     float* A1s = smem + L::oA1;
     float* GPs = smem + L::oGP;
     float* XS = smem + L::oXS;
-    float* LSs = D0;   // FWD only: [BT][MP] log-std terms, consumed before phase 5 writes D0
 
     if (MODE == FVP && a.done && *a.done) return;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -117,7 +116,8 @@ __global__ void __launch_bounds__(FT, 1) k_fused(RowArgs a, FOut o) {
     zero_acc(g1);
     zero_acc(g2);
     float b1acc = 0.f, b2acc = 0.f;
-    double lsacc = 0.0;
+    double racc0 = 0.0, racc1 = 0.0;   // row-pass partials (FWD), folded at the end
+    const float sls = MODE == FWD ? ls_sum(P + pk.ls, m) : 0.f;
 
     constexpr int PER = BT * (KC / 4) / FT;   // float4 per thread per chunk
     float4 st[PER];
@@ -300,40 +300,7 @@ __global__ void __launch_bounds__(FT, 1) k_fused(RowArgs a, FOut o) {
 
         // ---------------- FWD: log-likelihood, caches, VPG upstream ----------------
         if (MODE == FWD) {
-            if (tid < BT) {
-                const int row = tid;
-                const int64_t gr = row_base + row;
-                float* gpr = GPs + row * L::LDP;
-                if (gr < T) {
-                    const float adv = a.adv_vpg[gr];
-                    float s2 = 0.f, sls = 0.f;
-                    for (int j = 0; j < m; ++j) {
-                        const float ls = P[pk.ls + j];
-                        const float sg = expf(ls);
-                        const float mu = gpr[j];
-                        const float zs = (a.act[gr * m + j] - mu) / sg;
-                        s2 += zs * zs;
-                        sls += ls;
-                        a.mu0[gr * m + j] = mu;
-                        LSs[row * MP + j] = adv * (zs * zs - 1.f);
-                        const float os = a.out_scale ? a.out_scale[j] : 1.f;
-                        gpr[j] = adv * (zs / sg) * os;
-                    }
-                    for (int j = m; j < MP; ++j) LSs[row * MP + j] = 0.f;
-                    a.ll0[gr] = ((-0.5f * s2) + (-sls)) + a.llc;
-                } else {
-                    for (int j = 0; j < MP; ++j) {
-                        gpr[j] = 0.f;
-                        LSs[row * MP + j] = 0.f;
-                    }
-                }
-            }
-            __syncthreads();
-            if (tid < MP) {
-                double s = 0.0;
-                for (int row = 0; row < BT; ++row) s += (double)LSs[row * MP + tid];
-                lsacc += s;
-            }
+            row_pass<MODE, BT, MP, FT, false>(a, P + pk.ls, sls, row_base, GPs, L::LDP, racc0, racc1, tid);
             __syncthreads();
         }
 
@@ -459,7 +426,11 @@ __global__ void __launch_bounds__(FT, 1) k_fused(RowArgs a, FOut o) {
         o.wpart[o.boff1 + blk * H1 + tid] = b1acc;
     else if (tid < H1 + MP)
         o.wpart[o.boff2 + blk * MP + tid - H1] = b2acc;
-    if (MODE == FWD && tid < MP) a.rpart[blk * MP + tid] = lsacc;
+    if (MODE == FWD) {
+        static_assert(L::total >= 2 * FT, "row_pass_final scratch");
+        __syncthreads();
+        row_pass_final<MODE, MP, FT>(racc0, racc1, reinterpret_cast<double*>(smem), a.rpart, blk, tid);
+    }
 }
 
 }  // namespace

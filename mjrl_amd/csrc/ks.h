@@ -1,11 +1,11 @@
-// ks.h — persistent fused FWD / FVP / EVAL kernel for the MLP(64,64) policy with a
+// ks.h — persistent fused FWD / FVP kernel for the MLP(64,64) policy with a
 // wide observation (NP = 32*KG, up to 384: Humanoid), included by policy.hip.
 //
 // One 512-thread workgroup (8 waves) per CU walks 32-row tiles of timesteps with
 // NO global load inside the tile loop except the next tile's xhat prefetch (and,
 // for FVP, the cached activations):
 //   - wave w owns hidden block cb = w&3 and observation half kh = w>>2: its slice of
-//     W0 (FWD / EVAL) or of the tangent dW0 (FVP) — 16 x NP/2 floats — lives in
+//     W0 (FWD) or of the tangent dW0 (FVP) — 16 x NP/2 floats — lives in
 //     REGISTERS as MFMA B fragments for the whole launch, and so does its slice of
 //     the gW0 accumulator;
 //   - W1 / dW1 / W2 / dW2 live in LDS for the whole launch;
@@ -26,6 +26,7 @@ struct KLayout {
     static constexpr int NP = 32 * KG, KH = NP / 2;
     static constexpr int LDX = NP + 16;   // rows 4 apart fall 16 banks apart for the b32 gW0 reads
     static constexpr int LD = H + 4, LDP = MP + 4;
+    static_assert(KT == BT * H / 4, "tanh_tile: one float4 per thread");
     static constexpr int oXT = 0;
     static constexpr int oD0 = oXT + BT * LDX;
     static constexpr int oA0 = oD0 + BT * LD;
@@ -79,8 +80,22 @@ __device__ __forceinline__ void mm_lds_kn(floatx4 (&acc)[NR], const float* As, i
     }
 }
 
+// FWD activation of one [32][64] tile: A = tanh(U) in LDS and the a0 / a1 cache
+// rows in HBM, one float4 per thread (row-contiguous, coalesced stores).
+__device__ __forceinline__ void tanh_tile(const float* U, float* A, float* cache, int64_t row_base, int64_t T,
+                                          int tid) {
+    constexpr int LD = 68;
+    const int row = tid >> 4, c = (tid & 15) * 4;
+    const float4 u = *reinterpret_cast<const float4*>(U + row * LD + c);
+    const float4 v = make_float4(tanhf(u.x), tanhf(u.y), tanhf(u.z), tanhf(u.w));
+    *reinterpret_cast<float4*>(A + row * LD + c) = v;
+    const int64_t gr = row_base + row;
+    if (gr < T) *reinterpret_cast<float4*>(cache + gr * 64 + c) = v;
+}
+
 template <int MP, int KG, int MODE>
 __global__ void __launch_bounds__(KT, 1) k_ks(RowArgs a, FOut o) {
+    static_assert(MODE == FWD || MODE == FVP, "k_ks runs the gradient modes");
     using L = KLayout<MP, KG>;
     constexpr int H = 64, BT = L::BT, NP = L::NP, KH = L::KH;
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -94,8 +109,6 @@ __global__ void __launch_bounds__(KT, 1) k_ks(RowArgs a, FOut o) {
     float* sdW1 = smem + L::odW1;
     float* sW2 = smem + L::oW2;
     float* sdW2 = smem + L::odW2;
-    double* RED = reinterpret_cast<double*>(D0);   // EVAL: [2][BT] doubles (D0 unused in EVAL)
-    float* LSs = D1;                              // FWD: [BT][MP] (D1 unused before phase 4)
 
     if (MODE == FVP && a.done && *a.done) return;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -133,7 +146,8 @@ __global__ void __launch_bounds__(KT, 1) k_ks(RowArgs a, FOut o) {
     g1[1] = zero4();
     floatx4 g2 = zero4();   // gW2 tile (nb = w>>2 < MP/16, kb = w&3)
     float b1acc = 0.f, b2acc = 0.f;
-    double lsacc = 0.0, surr_acc = 0.0, kl_acc = 0.0;
+    double racc0 = 0.0, racc1 = 0.0;   // row-pass partials (FWD), folded at the end
+    const float sls = MODE == FWD ? ls_sum(P + pk.ls, m) : 0.f;
 
     // tile-invariant per-lane constants of the epilogues
     const float bias1 = (MODE == FVP ? a.V : P)[pk.b1 + cb * 16 + r16];
@@ -229,19 +243,20 @@ __global__ void __launch_bounds__(KT, 1) k_ks(RowArgs a, FOut o) {
                     const int row = i * 16 + 4 * q + rr;
                     const int col = cb * 16 + r16;
                     const float v = acc1[i][rr] + D0[row * L::LD + col];
-                    const int64_t gr = row_base + row;
                     if (MODE == FVP) {
                         const float av = pa0[i][rr];
                         D0[row * L::LD + col] = (1.f - av * av) * v;
                         A0s[row * L::LD + col] = av;
                     } else {
-                        const float av = tanhf(v);
-                        A0s[row * L::LD + col] = av;
-                        if (MODE == FWD && gr < T) a.a0[gr * H + col] = av;
+                        D0[row * L::LD + col] = v;   // pre-activation; tanh below
                     }
                 }
         }
         __syncthreads();
+        if (MODE == FWD) {
+            tanh_tile(D0, A0s, a.a0, row_base, T, tid);
+            __syncthreads();
+        }
 
         // ---- phase 2: [32 x 64], K = 64; wave -> (rb = kh, cb) ----
         {
@@ -256,20 +271,21 @@ __global__ void __launch_bounds__(KT, 1) k_ks(RowArgs a, FOut o) {
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr) {
                 const int row = kh * 16 + 4 * q + rr;
-                const int64_t gr = row_base + row;
                 const float v = acc[0][rr] + bias1;
                 if (MODE == FVP) {
                     const float av = pa1[rr];
                     D1[row * L::LD + col] = (1.f - av * av) * v;
                     A1s[row * L::LD + col] = av;
                 } else {
-                    const float av = tanhf(v);
-                    A1s[row * L::LD + col] = av;
-                    if (MODE == FWD && gr < T) a.a1[gr * H + col] = av;
+                    D1[row * L::LD + col] = v;
                 }
             }
         }
         __syncthreads();
+        if (MODE == FWD) {
+            tanh_tile(D1, A1s, a.a1, row_base, T, tid);
+            __syncthreads();
+        }
 
         // ---- phase 3: [32 x MP], K = 64; tiles (rb, cbo) over the first 2*MP/16 waves ----
         if (w < 2 * (MP / 16)) {
@@ -293,81 +309,13 @@ __global__ void __launch_bounds__(KT, 1) k_ks(RowArgs a, FOut o) {
         }
         __syncthreads();
 
-        // ---- per-row pass (FWD: log-lik, caches, VPG upstream; EVAL: LR, KL) ----
-        if (MODE != FVP) {
-            if (tid < BT) {
-                const int row = tid;
-                const int64_t gr = row_base + row;
-                float* gpr = GPs + row * L::LDP;
-                if (gr < T) {
-                    float s2 = 0.f, sls = 0.f;
-                    if (MODE == FWD) {
-                        const float adv = a.adv_vpg[gr];
-                        for (int j = 0; j < m; ++j) {
-                            const float ls = P[pk.ls + j];
-                            const float sg = expf(ls);
-                            const float mu = gpr[j];
-                            const float zs = (a.act[gr * m + j] - mu) / sg;
-                            s2 += zs * zs;
-                            sls += ls;
-                            a.mu0[gr * m + j] = mu;
-                            LSs[row * MP + j] = adv * (zs * zs - 1.f);
-                            const float os = a.out_scale ? a.out_scale[j] : 1.f;
-                            gpr[j] = adv * (zs / sg) * os;
-                        }
-                        for (int j = m; j < MP; ++j) LSs[row * MP + j] = 0.f;
-                        a.ll0[gr] = ((-0.5f * s2) + (-sls)) + a.llc;
-                    } else {
-                        float kl = 0.f;
-                        for (int j = 0; j < m; ++j) {
-                            const float lsn = P[pk.ls + j], lso = a.V[pk.ls + j];
-                            const float sn = expf(lsn), so = expf(lso);
-                            const float mun = gpr[j], muo = a.mu0[gr * m + j];
-                            const float zs = (a.act[gr * m + j] - mun) / sn;
-                            s2 += zs * zs;
-                            sls += lsn;
-                            const float dm = muo - mun;
-                            const float nr = (dm * dm + so * so) - sn * sn;
-                            const float dr = 2.f * sn * sn + 1e-8f;
-                            kl += (nr / dr + lsn) - lso;
-                        }
-                        const float lln = ((-0.5f * s2) + (-sls)) + a.llc;
-                        const float lr = expf(lln - a.ll0[gr]);
-                        RED[row] = (double)(lr * a.adv[gr]);
-                        RED[BT + row] = (double)kl;
-                    }
-                } else {
-                    if (MODE == FWD) {
-                        for (int j = 0; j < MP; ++j) {
-                            gpr[j] = 0.f;
-                            LSs[row * MP + j] = 0.f;
-                        }
-                    } else {
-                        RED[row] = 0.0;
-                        RED[BT + row] = 0.0;
-                    }
-                }
-            }
-            __syncthreads();
-            if (MODE == FWD) {
-                if (tid < MP) {
-                    double s = 0.0;
-                    for (int row = 0; row < BT; ++row) s += (double)LSs[row * MP + tid];
-                    lsacc += s;
-                }
-            } else if (tid == 0) {
-                double s = 0.0, k = 0.0;
-                for (int row = 0; row < BT; ++row) {
-                    s += RED[row];
-                    k += RED[BT + row];
-                }
-                surr_acc += s;
-                kl_acc += k;
-            }
+        // ---- per-row pass (FWD: log-lik, caches, VPG upstream) ----
+        if (MODE == FWD) {
+            row_pass<MODE, BT, MP, KT, false>(a, P + pk.ls, sls, row_base, GPs, L::LDP, racc0, racc1, tid);
             __syncthreads();
         }
 
-        if (MODE != EVAL) {
+        {
             // ---- phase 4: gu1 = (1 - a1^2) (g W2); wave -> (rb = kh, cb) ----
             {
                 floatx4 acc[1] = {zero4()};
@@ -425,13 +373,6 @@ __global__ void __launch_bounds__(KT, 1) k_ks(RowArgs a, FOut o) {
     }
 
     const int64_t blk = blockIdx.x;
-    if (MODE == EVAL) {
-        if (tid == 0) {
-            a.rpart[blk * 2 + 0] = surr_acc;
-            a.rpart[blk * 2 + 1] = kl_acc;
-        }
-        return;
-    }
 #pragma unroll
     for (int g = 0; g < KG; ++g)
 #pragma unroll
@@ -460,7 +401,11 @@ __global__ void __launch_bounds__(KT, 1) k_ks(RowArgs a, FOut o) {
         o.wpart[o.boff1 + blk * H + tid] = b1acc;
     else if (tid < H + MP)
         o.wpart[o.boff2 + blk * MP + tid - H] = b2acc;
-    if (MODE == FWD && tid < MP) a.rpart[blk * MP + tid] = lsacc;
+    if (MODE == FWD) {
+        static_assert(L::total >= 2 * KT, "row_pass_final scratch");
+        __syncthreads();
+        row_pass_final<MODE, MP, KT>(racc0, racc1, reinterpret_cast<double*>(smem), a.rpart, blk, tid);
+    }
 }
 
 }  // namespace

@@ -66,14 +66,125 @@ struct Layout {
     static constexpr bool XS_ALIAS = !LIN && 2 * BT * LD1 >= XS;
     static constexpr int oXS = XS_ALIAS ? oD1 : oGP + BT * LDP;
     static constexpr int end1 = XS_ALIAS ? oGP + BT * LDP : oXS + XS;
-    static constexpr int SCR = BT * MP + 4 * BT;   // log-std scratch [BT][MP] + 2*BT doubles
-    static constexpr bool SCR_IN_D0 = !LIN && BT * LD0 >= SCR;
-    static constexpr int oSCR = SCR_IN_D0 ? oD0 : end1;
-    static constexpr int total = SCR_IN_D0 ? end1 : end1 + SCR;
+    static constexpr int total = end1 > 2 * NTHREADS ? end1 : 2 * NTHREADS;   // >= row_pass_final's doubles
     static constexpr int bytes = total * 4;
 };
 
 __device__ __forceinline__ float tanh_f(float x) { return tanhf(x); }
+
+// sum_j log_std_j in action order (the -sum(log_std) term of log_likelihood)
+__device__ __forceinline__ float ls_sum(const float* __restrict__ P_ls, int m) {
+    float s = 0.f;
+    for (int j = 0; j < m; ++j) s += P_ls[j];
+    return s;
+}
+
+// Per-row pass of FWD / EVAL over a tile of BT rows whose output-layer values
+// sit in GPs[BT][ldp] (gaussian_mlp.py:100-140 log_likelihood, mean_LL,
+// likelihood_ratio, kl_old_new; batch_reinforce.py:37-55).
+// Element-parallel over (row, action): thread tid owns action j = tid % MP of
+// rows (tid + u NT) / MP, so the MP lanes of a row sit in one wave and the sums
+// over actions are a fixed shuffle tree inside the row's lanes (no barrier).
+//   FWD : mu0 <- mean; GPs <- adv z / sigma * out_scale (zero for j >= m and rows
+//         past T); ll0 <- log-likelihood; acc0 += adv (z^2 - 1) (log-std VPG, action j).
+//   EVAL: acc0 += exp(LL_new - LL_old) adv, acc1 += KL(old || new) (lanes j = 0).
+// The per-thread partials are folded once per launch by row_pass_final.
+template <int MODE, int BT, int MP, int NT, bool STORE_GP>
+__device__ __forceinline__ void row_pass(const RowArgs& a, const float* __restrict__ P_ls, float sls,
+                                         int64_t row_base, float* GPs, int ldp, double& acc0, double& acc1,
+                                         int tid) {
+    constexpr int PER = BT * MP / NT;
+    static_assert(NT % MP == 0 && PER * NT == BT * MP && MP <= 64, "row lanes in one wave");
+    const int m = a.m;
+    const int64_t T = a.T;
+    const int j = tid % MP;
+    const bool act_j = j < m;
+    const float lsn = act_j ? P_ls[j] : 0.f;
+    const float sn = expf(lsn);
+    float os = 1.f, lso = 0.f, so = 1.f;
+    if (MODE == FWD) {
+        if (a.out_scale && act_j) os = a.out_scale[j];
+    } else {
+        lso = act_j ? a.V[(P_ls - a.P) + j] : 0.f;
+        so = expf(lso);
+    }
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const int row = (tid + u * NT) / MP;
+        const int64_t gr = row_base + row;
+        const bool valid = gr < T && act_j;
+        float* g = GPs + row * ldp + j;
+        const float mu = *g;
+        const float av = valid ? a.act[gr * m + j] : 0.f;
+        float mo = 0.f, adv = 0.f;
+        if (MODE == EVAL) mo = valid ? a.mu0[gr * m + j] : 0.f;
+        if (MODE == FWD) adv = gr < T ? a.adv_vpg[gr] : 0.f;
+        const float zs = valid ? (av - mu) / sn : 0.f;
+        float z2 = zs * zs;
+        float kl = 0.f;
+        if (MODE == FWD) {
+            if (valid) {
+                a.mu0[gr * m + j] = mu;
+                acc0 += (double)(adv * (z2 - 1.f));
+            }
+            const float gv = valid ? adv * (zs / sn) * os : 0.f;
+            *g = gv;
+            if (STORE_GP && gr < T) a.gp[gr * MP + j] = gv;
+        } else if (valid) {
+            const float dm = mo - mu;
+            const float nr = (dm * dm + so * so) - sn * sn;
+            const float dr = 2.f * sn * sn + 1e-8f;
+            kl = (nr / dr + lsn) - lso;
+        }
+#pragma unroll
+        for (int o = MP / 2; o > 0; o >>= 1) {
+            z2 += __shfl_xor(z2, o, 64);
+            if (MODE == EVAL) kl += __shfl_xor(kl, o, 64);
+        }
+        if (j == 0 && gr < T) {
+            const float ll = ((-0.5f * z2) + (-sls)) + a.llc;
+            if (MODE == FWD) {
+                a.ll0[gr] = ll;
+            } else {
+                const float lr = expf(ll - a.ll0[gr]);
+                acc0 += (double)(lr * a.adv[gr]);
+                acc1 += (double)kl;
+            }
+        }
+    }
+}
+
+// Fold the launch's row-pass partials (fixed order): FWD -> rpart[blk][MP]
+// (log-std VPG sums), EVAL -> rpart[blk][2] (surrogate and KL sums).
+// red: LDS scratch of NT doubles; the caller has synchronised the block.
+template <int MODE, int MP, int NT>
+__device__ __forceinline__ void row_pass_final(double acc0, double acc1, double* red, double* __restrict__ rpart,
+                                               int64_t blk, int tid) {
+    if (MODE == FWD) {
+        red[tid] = acc0;
+        __syncthreads();
+        if (tid < MP) {
+            double s = 0.0;
+            for (int k = 0; k < NT / MP; ++k) s += red[k * MP + tid];
+            rpart[blk * MP + tid] = s;
+        }
+    } else {
+        if (tid % MP == 0) {
+            red[tid / MP] = acc0;
+            red[NT / MP + tid / MP] = acc1;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            double s = 0.0, k = 0.0;
+            for (int i = 0; i < NT / MP; ++i) {
+                s += red[i];
+                k += red[NT / MP + i];
+            }
+            rpart[blk * 2 + 0] = s;
+            rpart[blk * 2 + 1] = k;
+        }
+    }
+}
 
 template <int H0, int H1, int MP, int MODE>
 __global__ void __launch_bounds__(NTHREADS, (Layout<H0, H1, MP>::bytes > 81920 ? 1 : 2)) k_rows(RowArgs a) {
@@ -88,8 +199,6 @@ __global__ void __launch_bounds__(NTHREADS, (Layout<H0, H1, MP>::bytes > 81920 ?
     float* A1s = smem + L::oA1;
     float* GPs = smem + L::oGP;
     float* XS = smem + L::oXS;
-    float* LSs = smem + L::oSCR;                                   // [BT][MP]
-    double* RED = reinterpret_cast<double*>(smem + L::oSCR + BT * MP);   // [2][BT]
 
     if (MODE == FVP && a.done && *a.done) return;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -101,8 +210,9 @@ __global__ void __launch_bounds__(NTHREADS, (Layout<H0, H1, MP>::bytes > 81920 ?
     const float* P = a.P;
     const Packed pk(H0, H1, np, MP);
     // per-lane output-column constants for the output layer
-    double ls_acc = 0.0;             // FWD: log-std gradient partial (thread j < MP)
-    double surr_acc = 0.0, kl_acc = 0.0;   // EVAL partials (thread 0)
+    // FWD / EVAL row-pass partials (row_pass), folded at the end of the launch
+    double racc0 = 0.0, racc1 = 0.0;
+    const float sls = MODE == FVP ? 0.f : ls_sum(P + pk.ls, m);
 
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t row_base = tile * BT;
@@ -289,79 +399,7 @@ __global__ void __launch_bounds__(NTHREADS, (Layout<H0, H1, MP>::bytes > 81920 ?
 
         // ---------------- per-row pass: log-likelihood, VPG upstream, LR, KL -------------
         if (MODE != FVP) {
-            if (tid < BT) {
-                const int row = tid;
-                const int64_t gr = row_base + row;
-                float* gpr = GPs + row * L::LDP;
-                if (gr < T) {
-                    float s2 = 0.f, sls = 0.f;
-                    if (MODE == FWD) {
-                        const float adv = a.adv_vpg[gr];
-                        for (int j = 0; j < m; ++j) {
-                            const float ls = P[pk.ls + j];
-                            const float sg = expf(ls);
-                            const float mu = gpr[j];
-                            const float zs = (a.act[gr * m + j] - mu) / sg;
-                            s2 += zs * zs;
-                            sls += ls;
-                            a.mu0[gr * m + j] = mu;
-                            LSs[row * MP + j] = adv * (zs * zs - 1.f);
-                            const float os = a.out_scale ? a.out_scale[j] : 1.f;
-                            gpr[j] = adv * (zs / sg) * os;
-                        }
-                        for (int j = m; j < MP; ++j) LSs[row * MP + j] = 0.f;
-                        a.ll0[gr] = ((-0.5f * s2) + (-sls)) + a.llc;
-                        for (int j = 0; j < MP; ++j) a.gp[gr * MP + j] = gpr[j];
-                    } else {   // EVAL
-                        float kl = 0.f, slo = 0.f;
-                        for (int j = 0; j < m; ++j) {
-                            const float lsn = P[pk.ls + j], lso = a.V[pk.ls + j];
-                            const float sn = expf(lsn), so = expf(lso);
-                            const float mun = gpr[j], muo = a.mu0[gr * m + j];
-                            const float zs = (a.act[gr * m + j] - mun) / sn;
-                            s2 += zs * zs;
-                            sls += lsn;
-                            slo += lso;
-                            const float dm = muo - mun;
-                            const float nr = (dm * dm + so * so) - sn * sn;
-                            const float dr = 2.f * sn * sn + 1e-8f;
-                            kl += (nr / dr + lsn) - lso;
-                        }
-                        const float lln = ((-0.5f * s2) + (-sls)) + a.llc;
-                        const float lr = expf(lln - a.ll0[gr]);
-                        RED[row] = (double)(lr * a.adv[gr]);
-                        RED[BT + row] = (double)kl;
-                    }
-                } else {
-                    if (MODE == FWD) {
-                        for (int j = 0; j < MP; ++j) {
-                            gpr[j] = 0.f;
-                            LSs[row * MP + j] = 0.f;
-                        }
-                    } else {
-                        RED[row] = 0.0;
-                        RED[BT + row] = 0.0;
-                    }
-                }
-            }
-            __syncthreads();
-            if (MODE == FWD) {
-                if (tid < MP) {
-                    double s = 0.0;
-                    for (int row = 0; row < BT; ++row) s += (double)LSs[row * MP + tid];
-                    ls_acc += s;
-                }
-            } else if (MODE == EVAL) {
-                if (tid == 0) {
-                    double s = 0.0, k = 0.0;
-                    for (int row = 0; row < BT; ++row) {
-                        s += RED[row];
-                        k += RED[BT + row];
-                    }
-                    surr_acc += s;
-                    kl_acc += k;
-                }
-            }
+            row_pass<MODE, BT, MP, NTHREADS, true>(a, P + pk.ls, sls, row_base, GPs, L::LDP, racc0, racc1, tid);
             __syncthreads();
         }
 
@@ -418,13 +456,10 @@ __global__ void __launch_bounds__(NTHREADS, (Layout<H0, H1, MP>::bytes > 81920 ?
         }
     }
 
-    if (MODE == FWD) {
-        if (tid < MP) a.rpart[(int64_t)blockIdx.x * MP + tid] = ls_acc;
-    } else if (MODE == EVAL) {
-        if (tid == 0) {
-            a.rpart[(int64_t)blockIdx.x * 2 + 0] = surr_acc;
-            a.rpart[(int64_t)blockIdx.x * 2 + 1] = kl_acc;
-        }
+    if (MODE != FVP) {
+        static_assert(L::total >= 2 * NTHREADS, "row_pass_final scratch");
+        __syncthreads();
+        row_pass_final<MODE, MP, NTHREADS>(racc0, racc1, reinterpret_cast<double*>(smem), a.rpart, blockIdx.x, tid);
     }
 }
 
@@ -550,14 +585,21 @@ struct GArgs {
     const int32_t* done;
 };
 
-__global__ void __launch_bounds__(256) k_gather(GArgs a) {
+// Block = 8 waves over 64 consecutive flat parameters: lane -> parameter, wave w
+// sums its contiguous share of the slices in order, and wave 0 adds the eight
+// wave partials in order (deterministic, fp64).
+constexpr int GATHER_WAVES = 8;
+
+__global__ void __launch_bounds__(64 * GATHER_WAVES) k_gather(GArgs a) {
     if (a.done && *a.done) return;
-    const int f = blockIdx.x * blockDim.x + threadIdx.x;
-    if (f >= a.d) return;
+    __shared__ double part[GATHER_WAVES][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int f = blockIdx.x * 64 + lane;
     int64_t src = -1, stride = 0;
     int lsj = -1;
     int g = f;
-    if (a.h0 == 0) {
+    if (f >= a.d) {
+    } else if (a.h0 == 0) {
         if (g < a.m * a.n) {
             src = a.off0 + (int64_t)(g / a.n) * a.np + g % a.n;
             stride = (int64_t)a.mp * a.np;
@@ -593,22 +635,46 @@ __global__ void __launch_bounds__(256) k_gather(GArgs a) {
     }
     double acc = 0.0;
     if (src >= 0) {
-        for (int s = 0; s < a.S; ++s) acc += (double)a.wpart[src + s * stride];
-    } else if (a.lspart) {
-        for (int b = 0; b < a.G; ++b) acc += a.lspart[(int64_t)b * a.mp + lsj];
+        const int per = (a.S + GATHER_WAVES - 1) / GATHER_WAVES;
+        const int s0 = w * per, s1 = min(a.S, s0 + per);
+        const float* p = a.wpart + src;
+        int s = s0;
+        for (; s + 8 <= s1; s += 8) {
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = p[(int64_t)(s + j) * stride];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc += (double)v[j];
+        }
+        for (; s < s1; ++s) acc += (double)p[(int64_t)s * stride];
+    } else if (lsj >= 0 && a.lspart) {
+        const int per = (a.G + GATHER_WAVES - 1) / GATHER_WAVES;
+        const int b0 = w * per, b1 = min(a.G, b0 + per);
+        for (int b = b0; b < b1; ++b) acc += a.lspart[(int64_t)b * a.mp + lsj];
     }
-    a.gsum[f] = (float)acc;
+    part[w][lane] = acc;
+    __syncthreads();
+    if (w == 0 && f < a.d) {
+        double t = part[0][lane];
+#pragma unroll
+        for (int j = 1; j < GATHER_WAVES; ++j) t += part[j][lane];
+        a.gsum[f] = (float)t;
+    }
 }
 
 __global__ void __launch_bounds__(64) k_eval_final(const double* __restrict__ rpart, int G, double* __restrict__ sums) {
-    if (threadIdx.x != 0) return;
+    // one wave: lane l folds partials l, l+64, ... in order, then a fixed shuffle tree
     double s = 0.0, k = 0.0;
-    for (int b = 0; b < G; ++b) {
+    for (int b = threadIdx.x; b < G; b += 64) {
         s += rpart[2 * b];
         k += rpart[2 * b + 1];
     }
-    sums[0] = s;
-    sums[1] = k;
+    s = wave_sum(s);
+    k = wave_sum(k);
+    if (threadIdx.x == 0) {
+        sums[0] = s;
+        sums[1] = k;
+    }
 }
 
 }  // namespace
@@ -823,8 +889,7 @@ int run_fused(int mode, const mjrl_shape* s, const mjrl_rows* r, int64_t T, cons
     fo.boff2 = js.job[2].boff;
     if (ks) {
         if (mode == FWD) return launch_ks<FWD>(s, ra, fo, G, st);
-        if (mode == FVP) return launch_ks<FVP>(s, ra, fo, G, st);
-        return launch_ks<EVAL>(s, ra, fo, G, st);
+        return launch_ks<FVP>(s, ra, fo, G, st);
     }
     return mode == FWD ? launch_fused<FWD>(s, ra, fo, G, st) : launch_fused<FVP>(s, ra, fo, G, st);
 }
@@ -848,7 +913,7 @@ int run_gather(const mjrl_shape* s, const mjrl_rows* r, int64_t T, const mjrl_sc
     }
     ga.gsum = gsum;
     ga.done = done;
-    hipLaunchKernelGGL(k_gather, dim3((s->d + 255) / 256), dim3(256), 0, st, ga);
+    hipLaunchKernelGGL(k_gather, dim3((s->d + 63) / 64), dim3(64 * GATHER_WAVES), 0, st, ga);
     return (int)hipGetLastError();
 }
 
@@ -1000,10 +1065,10 @@ int mjrl_policy_eval(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_eval,
     ra.out_shift = out_shift;
     ra.out_scale = out_scale;
     ra.rpart = sc->rpart;
-    const bool ks = acc_path(s, T_eval) == 2;
-    const int G = ks ? ks_grid(T_eval) : row_grid(s, T_eval);
+    // forward-only: the row kernel (no weight-gradient state to keep resident)
+    const int G = row_grid(s, T_eval);
     if (T_eval > 0) {
-        int e = ks ? run_fused(EVAL, s, rows, T_eval, ra, sc, st) : launch_rows<EVAL>(s, ra, G, st);
+        int e = launch_rows<EVAL>(s, ra, G, st);
         if (e) return e;
     } else {
         hipMemsetAsync(sc->rpart, 0, sizeof(double) * 2 * G, st);

@@ -45,6 +45,25 @@ def flops_per_row(n, m, h0, h1):
     return dict(rows_fvp=jvp + vjp_act, weight_grads=wgrad)
 
 
+def update_flops_per_row(n, m, h0, h1, K):
+    """Algorithmic FLOPs of one whole update per timestep:
+    fwd F + VPG (F + 2I) + K FVPs K (2F + 4I) + post-update fwd F, with
+    F = 2(n h0 + h0 h1 + h1 m), I = h0 h1 + h1 m (1,563,136 at Humanoid / K = 10)."""
+    F = 2 * (n * h0 + h0 * h1 + h1 * m)
+    I = h0 * h1 + h1 * m
+    return 3 * F + 2 * I + K * (2 * F + 4 * I)
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def pmc_traffic(kernel_key):
     """HBM bytes per launch of a kernel from the newest committed PMC summary
     (profiles/r*/pmc_traffic.json, written from separate rocprofv3 --pmc passes
@@ -106,8 +125,9 @@ def stage_shard(p0, p1, device, base):
     return DeviceBatch(ho.to(device), ha.to(device), t(rw), t(bl), t(off), t(np.zeros(P, np.uint8)))
 
 
-def cpu_baseline(rows, base):
-    """The oracle (CPU restatement of the reference update) on `rows` timesteps."""
+def cpu_baseline(rows, base, reps=3):
+    """The oracle (CPU restatement of the reference update) on `rows` timesteps:
+    one warm-up update on a tenth of the sample, then the median of `reps`."""
     from oracle import npg_cpu as O
     P = rows // HORIZON
     obs, act, rew = make_paths(0, P)
@@ -117,19 +137,60 @@ def cpu_baseline(rows, base):
     lengths = np.full(P, HORIZON)
     bl = np.concatenate([base.predict(dict(observations=o, rewards=r))
                          for o, r in zip(O.split(obs, lengths), O.split(rew, lengths))])
-    torch.manual_seed(0)
     theta = np.concatenate([(np.random.RandomState(1).randn(int(np.prod(s))) * 0.05).ravel()
                             for s in O.param_shapes(N_OBS, N_ACT, HIDDEN)]).astype(np.float32)
     theta[-N_ACT:] = 0.0
-    pol = O.Policy(N_OBS, N_ACT, HIDDEN, theta.astype(np.float64), None)
-    t0 = time.perf_counter()
-    ret, adv = O.returns_and_advantages(rew, bl, lengths, np.zeros(P, bool), GAMMA, LAM)
-    O.update(pol, obs, act, adv, rew, lengths, algo="npg", n_step_size=DELTA, cg_iters=CG_ITERS, damping=DAMPING)
-    dt = time.perf_counter() - t0
-    return dict(value=rows / dt, unit="timesteps/s", cores=torch.get_num_threads(), kind="port",
+
+    def one(r):
+        pol = O.Policy(N_OBS, N_ACT, HIDDEN, theta.astype(np.float64), None)
+        Pr = r // HORIZON
+        t0 = time.perf_counter()
+        ret, adv = O.returns_and_advantages(rew[:r], bl[:r], lengths[:Pr], np.zeros(Pr, bool), GAMMA, LAM)
+        O.update(pol, obs[:r], act[:r], adv, rew[:r], lengths[:Pr], algo="npg", n_step_size=DELTA,
+                 cg_iters=CG_ITERS, damping=DAMPING)
+        return time.perf_counter() - t0
+
+    one(max(HORIZON, (rows // 10) // HORIZON * HORIZON))
+    ts = sorted(one(P * HORIZON) for _ in range(reps))
+    dt = ts[len(ts) // 2]
+    return dict(value=P * HORIZON / dt, unit="timesteps/s", cores=torch.get_num_threads(), kind="port",
+                cpu=cpu_model(),
                 sample="%d paths x %d steps (%d timesteps) of the same Humanoid-shape workload, one update "
-                       "(returns + GAE + train_from_paths), oracle/npg_cpu.py on %d torch threads: %.2f s"
-                       % (P, HORIZON, rows, torch.get_num_threads(), dt))
+                       "(returns + GAE + train_from_paths), oracle/npg_cpu.py on %d torch threads: median of %d "
+                       "updates %.2f s (all: %s)" % (P, HORIZON, P * HORIZON, torch.get_num_threads(), reps, dt,
+                                                    ", ".join("%.2f" % t for t in ts)))
+
+
+def e2e_from_host(paths_range, eng, th0, base, upd, device, reps=2):
+    """End-to-end update from numpy sampler paths (what train_agent sees):
+    pinned staging + H2D + device LinearBaseline predict + update + readback.
+    Reported beside `value` (never as it): SURVEY.md §8 d1."""
+    from mjrl_amd.engine import DeviceBatch
+    p0, p1 = paths_range
+    obs, act, rew = make_paths(p0, p1)
+    paths = [dict(observations=o.astype(np.float64), actions=a.astype(np.float64), rewards=r, terminated=False)
+             for o, a, r in zip(obs, act, rew)]
+    del obs, act
+    T = sum(len(p["rewards"]) for p in paths)
+    th = th0.clone()
+
+    def one():
+        nonlocal th
+        b = DeviceBatch.from_paths(paths, device, baseline=base)
+        eng.update(b, th, **upd)
+        th = eng.vec["theta_new"].clone()
+        torch.cuda.synchronize()
+
+    one()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        one()
+        ts.append(time.perf_counter() - t0)
+    dt = float(np.median(ts))
+    return dict(value=round(T / dt, 1), unit="timesteps/s", ms_per_step=round(dt * 1e3, 2),
+                note="numpy f64 paths -> pinned staging (reused) -> H2D -> device LinearBaseline.predict -> "
+                     "update -> readback; median of %d" % reps)
 
 
 def main():
@@ -138,8 +199,9 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--paths", type=int, default=N_PATHS)
-    ap.add_argument("--cpu-rows", type=int, default=100000)
+    ap.add_argument("--cpu-rows", type=int, default=200000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end-from-host-paths measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -225,6 +287,12 @@ def main():
                 traffic_GBps=None if traffic is None else round(traffic / (kern[dom]["avg_ms"] * 1e-3) / 1e9, 1),
                 flops_per_timestep=acc_fl if dom == acc_name else gat_fl, rows_per_launch=rows_rank,
                 launches=len(ev), kernels={k: {kk: round(vv, 4) for kk, vv in v.items()} for k, v in kern.items()})
+    # whole-update algorithmic FLOP rate, all kernels and gaps included
+    ufl = update_flops_per_row(N_OBS, N_ACT, HIDDEN[0], HIDDEN[1], CG_ITERS)
+    ut = ufl * T_total / (elapsed / args.steps) / 1e12
+    roof["update"] = dict(flops_per_timestep=ufl, achieved=round(ut, 3), unit="TFLOP/s",
+                          frac=round(ut / (PEAK_F32_MFMA * world), 4),
+                          note="algorithmic FLOPs of a whole update / wall time per update, vs n_gpus x peak")
 
     if rank == 0:
         ms = elapsed / args.steps * 1e3
@@ -236,6 +304,8 @@ def main():
                                timesteps=T_total, paths=args.paths, horizon=HORIZON, cg_iters=CG_ITERS,
                                parallelism="dp%d" % world),
                    roofline=roof)
+        if world == 1 and not args.no_e2e:
+            out["e2e_from_host"] = e2e_from_host((p0, p1), eng, th, base, upd, device)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_rows, base)
         print(json.dumps(out))

@@ -102,6 +102,13 @@ int mjrl_gae(const double* rew, const double* base, const int64_t* path_off,
 int mjrl_linear_baseline(const double* obs, int64_t T, int32_t n, const int64_t* path_off,
                          int64_t P, const double* coeffs, double* out, void* stream);
 
+/* ---- subsampled Fisher rows (npg_cg.py:58-62: obs[rand_idx], act[rand_idx]) ----
+ * dst row i = src row idx[i] for i < n, rows of row_bytes bytes (a multiple of 4);
+ * indices may repeat (np.random.choice draws with replacement).  Used to build
+ * the compact xhat / a0 / a1 rows one Fisher-vector product runs on. */
+int mjrl_gather_rows(const void* src, int64_t row_bytes, const int64_t* idx, int64_t n, void* dst,
+                     void* stream);
+
 /* ---- moments for whitening / stats (npg_cg.py:91, 97-102; dapg.py:70) ----
  * out[0] = sum(x - c), out[1] = sum((x - c)^2), out[2] = N, out[3] = min(x),
  * out[4] = max(x), out[5] = -min(x) over x[0..N-1] (out needs 6 doubles),

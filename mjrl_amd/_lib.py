@@ -66,6 +66,7 @@ SIGNATURES = {
     "mjrl_cg_init_vec": [I32, P, P, P, P, P, P, P],
     "mjrl_cg_update": [I32, P, P, P, P, P, P, F32, P],
     "mjrl_scale_vec": [P, I32, F64, P, P],
+    "mjrl_gather_rows": [P, I64, P, I64, P, P],
     "mjrl_npg_step": [SP, P, P, P, I32, F32, F32, I32, F32, P, P, P, P],
 }
 

@@ -38,9 +38,8 @@ class DAPG(NPG):
         return self.demo_paths if self._use_demos() else None
 
     def _update_args(self):
-        self._check_subsample()
         args = dict(algo="dapg", kl_dist=self.kl_dist, cg_iters=self.FIM_invert_args["iters"],
-                    damping=self.FIM_invert_args["damping"])
+                    damping=self.FIM_invert_args["damping"], hvp_sample_frac=self.hvp_subsample)
         if self._use_demos():
             args["demo_coef"] = self.lam_0 * (self.lam_1 ** self.iter_count)   # dapg.py:65
             self.iter_count += 1

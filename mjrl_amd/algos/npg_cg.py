@@ -30,15 +30,15 @@ class NPG(BatchREINFORCE):
         self._comm = comm
         self._engine = None
 
-    def _check_subsample(self):
-        if self.hvp_subsample is not None and self.hvp_subsample < 0.99:
-            raise NotImplementedError("hvp_sample_frac < 0.99 (npg_cg.py:58-62) is not implemented on the "
-                                      "device path yet; use the full batch (the reference default)")
-
     def HVP(self, observations, actions, vector, regu_coef=None):
-        """F v + damping v at the current (old == new) parameters (npg_cg.py:55-74)."""
-        self._check_subsample()
+        """F v + damping v at the current (old == new) parameters (npg_cg.py:55-74);
+        with hvp_sample_frac < 0.99 on np.random.choice(N, int(frac N)) rows drawn
+        from numpy's global RNG, as the reference does (npg_cg.py:58-62)."""
         regu_coef = self.FIM_invert_args["damping"] if regu_coef is None else regu_coef
+        if self.hvp_subsample is not None and self.hvp_subsample < 0.99:
+            num_samples = observations.shape[0]
+            rand_idx = np.random.choice(num_samples, size=int(self.hvp_subsample * num_samples))
+            observations, actions = observations[rand_idx], actions[rand_idx]
         eng = self.engine()
         T = eng.load_rows(observations, actions)
         eng.forward_pass(self._theta(), T)
@@ -51,9 +51,9 @@ class NPG(BatchREINFORCE):
         return eval
 
     def _update_args(self):
-        self._check_subsample()
         return dict(algo="npg", n_step_size=self.n_step_size, const_lr=self.alpha,
-                    cg_iters=self.FIM_invert_args["iters"], damping=self.FIM_invert_args["damping"])
+                    cg_iters=self.FIM_invert_args["iters"], damping=self.FIM_invert_args["damping"],
+                    hvp_sample_frac=self.hvp_subsample)
 
     def _log_update(self, res):
         self.logger.log_kv("alpha", res["alpha"])

@@ -28,6 +28,5 @@ class TRPO(NPG):
         self._engine = None
 
     def _update_args(self):
-        self._check_subsample()
         return dict(algo="trpo", kl_dist=self.kl_dist, cg_iters=self.FIM_invert_args["iters"],
-                    damping=self.FIM_invert_args["damping"])
+                    damping=self.FIM_invert_args["damping"], hvp_sample_frac=self.hvp_subsample)

@@ -6,8 +6,10 @@ quantities are sums over timesteps, so the only exchange is an all-reduce SUM of
   - the whitening moments (2 x 3 doubles) and the path-return moments,
   - the flat VPG sum (d floats) and every Fisher-vector-product sum (d floats),
   - the post-step surrogate / KL sums (2 doubles per line-search trial),
-plus one MAX of the path-return extrema.  Backend "nccl" is RCCL over xGMI on
-ROCm; the same code runs on "gloo" for the CPU tests.
+plus one MAX of the path-return extrema.  A subsampled Fisher
+(hvp_sample_frac < 1) adds one broadcast of rank 0's row draw per update.
+Backend "nccl" is RCCL over xGMI on ROCm; the same code runs on "gloo" for the
+CPU tests.
 """
 import numpy as np
 import torch
@@ -23,6 +25,13 @@ class LocalComm:
 
     def allreduce_max(self, t):
         return t
+
+    def broadcast(self, t, src=0):
+        return t
+
+    def row_offset(self, T, device=None):
+        """First global row of this rank's shard (ranks hold contiguous path ranges)."""
+        return 0
 
 
 class DistComm:
@@ -44,6 +53,17 @@ class DistComm:
         if self.world_size > 1:
             self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
         return t
+
+    def broadcast(self, t, src=0):
+        if self.world_size > 1:
+            self.dist.broadcast(t, src=src, group=self.group)
+        return t
+
+    def row_offset(self, T, device=None):
+        counts = torch.zeros(self.world_size, dtype=torch.float64, device=device)
+        counts[self.rank] = float(T)
+        self.allreduce_sum(counts)
+        return int(counts[:self.rank].sum().item())
 
 
 def default_comm():

@@ -315,6 +315,20 @@ __global__ void __launch_bounds__(256) k_scale_vec(const float* __restrict__ gsu
     if (i < d) g[i] = (float)((double)gsum[i] * scale);
 }
 
+// dst[i] = src[idx[i]] (row copies; one wave per row, 16-B lanes when aligned)
+template <typename V>
+__global__ void __launch_bounds__(256) k_gather_rows(const V* __restrict__ src, int64_t row_v,
+                                                     const int64_t* __restrict__ idx, int64_t n,
+                                                     V* __restrict__ dst) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < n; i += nw) {
+        const V* s = src + idx[i] * row_v;
+        V* d = dst + i * row_v;
+        for (int64_t c = lane; c < row_v; c += 64) d[c] = s[c];
+    }
+}
+
 inline int grid_for(int64_t work, int per_block, int cap) {
     int64_t g = (work + per_block - 1) / per_block;
     if (g < 1) g = 1;
@@ -399,6 +413,20 @@ int mjrl_linear_baseline(const double* obs, int64_t T, int32_t n, const int64_t*
     const int g = grid_for(T * 64, 256, 4096);
     hipLaunchKernelGGL(k_linear_baseline, dim3(g), dim3(256), 0, (hipStream_t)stream, obs, T, n, path_off, P,
                        coeffs, out);
+    return err(hipGetLastError());
+}
+
+int mjrl_gather_rows(const void* src, int64_t row_bytes, const int64_t* idx, int64_t n, void* dst, void* stream) {
+    if (n < 0 || row_bytes < 0 || row_bytes % 4 != 0 || (n > 0 && (!src || !idx || !dst))) return MJRL_EINVAL;
+    if (n == 0 || row_bytes == 0) return MJRL_OK;
+    const int g = grid_for(n, 4, 8192);   // 4 rows (waves) per workgroup
+    const bool v16 = row_bytes % 16 == 0 && ((uintptr_t)src | (uintptr_t)dst) % 16 == 0;
+    if (v16)
+        hipLaunchKernelGGL(k_gather_rows<float4>, dim3(g), dim3(256), 0, (hipStream_t)stream,
+                           (const float4*)src, row_bytes / 16, idx, n, (float4*)dst);
+    else
+        hipLaunchKernelGGL(k_gather_rows<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, (const float*)src,
+                           row_bytes / 4, idx, n, (float*)dst);
     return err(hipGetLastError());
 }
 

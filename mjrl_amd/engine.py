@@ -37,6 +37,39 @@ def _linear_coeffs(baseline, n):
     return c if len(c) == n + 4 else False
 
 
+class _PinnedStaging:
+    """Grow-only pinned host buffers reused across batches (one per slot), so a
+    training loop does not pay a multi-GB cudaHostAlloc per train_step.  A slot
+    is reused only after the H2D copy that last read it has completed."""
+
+    def __init__(self):
+        self._buf = {}
+        self._ev = {}
+
+    def stage(self, slot, arrs, shape, dtype, device):
+        nbytes = int(np.prod(shape)) * np.dtype(dtype).itemsize
+        ev = self._ev.get(slot)
+        if ev is not None:
+            ev.synchronize()
+        h = self._buf.get(slot)
+        if h is None or h.numel() < nbytes:
+            h = torch.empty(max(nbytes, 1), dtype=torch.uint8, pin_memory=True)
+            self._buf[slot] = h
+        view = h[:nbytes].numpy().view(dtype).reshape(shape)
+        if len(arrs):
+            np.concatenate(arrs, axis=0, out=view)
+        out = torch.empty(shape, dtype=torch.float64 if dtype == np.float64 else torch.int64, device=device)
+        if nbytes:
+            out.view(-1).view(torch.uint8).copy_(h[:nbytes], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._ev[slot] = ev
+        return out
+
+
+_STAGING = _PinnedStaging()
+
+
 class DeviceBatch:
     """One shard of trajectories in HBM — the hot path's input.
 
@@ -70,20 +103,18 @@ class DeviceBatch:
         dlen = [len(p["observations"]) for p in (demo_paths or [])]
         T_demo = int(sum(dlen))
 
-        def stage(arrs, shape, dtype=np.float64):
-            h = torch.empty(shape, dtype=torch.float64 if dtype == np.float64 else torch.int64, pin_memory=True)
-            if len(arrs):
-                np.concatenate(arrs, axis=0, out=h.numpy())
-            return h.to(device, non_blocking=True)
+        def stage(slot, arrs, shape, dtype=np.float64):
+            return _STAGING.stage(slot, arrs, shape, dtype, device)
 
-        obs = stage([p["observations"] for p in paths] + [p["observations"] for p in demo_paths or []],
+        obs = stage("obs", [p["observations"] for p in paths] + [p["observations"] for p in demo_paths or []],
                     (T + T_demo, n))
-        act = stage([p["actions"] for p in paths] + [p["actions"] for p in demo_paths or []], (T + T_demo, m))
-        rew = stage([p["rewards"] for p in paths], (T,))
+        act = stage("act", [p["actions"] for p in paths] + [p["actions"] for p in demo_paths or []],
+                    (T + T_demo, m))
+        rew = stage("rew", [p["rewards"] for p in paths], (T,))
         off = torch.from_numpy(np.concatenate([[0], np.cumsum(lengths)]).astype(np.int64)).to(device)
         if use_advantages:
             base = None
-            adv = stage([p["advantages"] for p in paths], (T,))
+            adv = stage("adv", [p["advantages"] for p in paths], (T,))
         elif _linear_coeffs(baseline, n) is not False:
             # LinearBaseline.predict on the device (a4), reading the staged obs
             coeffs = _linear_coeffs(baseline, n)
@@ -94,8 +125,8 @@ class DeviceBatch:
                                                            _lib.ptr(base), _lib.stream_ptr()), "mjrl_linear_baseline")
             adv = None
         else:
-            base = stage([baseline.predict(p) if baseline is not None else np.zeros(len(p["rewards"]))
-                          for p in paths], (T,))
+            base = stage("base", [baseline.predict(p) if baseline is not None else np.zeros(len(p["rewards"]))
+                                  for p in paths], (T,))
             adv = None
         term = torch.tensor([bool(p.get("terminated", False)) for p in paths], dtype=torch.uint8).to(device)
         b = cls(obs, act, rew, base, off, term, advantages=adv, T_demo=T_demo)
@@ -234,7 +265,8 @@ class UpdateEngine:
 
     def update(self, batch, theta, *, algo="npg", gamma=0.995, gae_lambda=0.98, n_step_size=0.01,
                const_lr=None, kl_dist=None, cg_iters=10, damping=1e-4, residual_tol=1e-10,
-               demo_coef=None, learn_rate=0.01, T_global=None, trpo_verbose=True, skip_gae=False):
+               demo_coef=None, learn_rate=0.01, T_global=None, trpo_verbose=True, skip_gae=False,
+               hvp_sample_frac=None):
         """One policy update.  `theta`: f32 device tensor [d] (flat params, reference
         order).  algo in {'npg', 'trpo', 'dapg', 'vpg'}.
 
@@ -242,13 +274,25 @@ class UpdateEngine:
         trpo: delta = 2 kl_dist + KL backtracking                              trpo.py:98-124
         dapg: g = (T_all/T) vpg(all rows), delta = 2 kl_dist                   dapg.py:62-121
         vpg:  theta + learn_rate * g (BatchREINFORCE)                          batch_reinforce.py:134-145
+        hvp_sample_frac < 0.99: each Fisher-vector product runs on its own draw of
+        np.random.choice(T_global, int(frac T_global)) rows from numpy's global RNG
+        (npg_cg.py:58-62); rank 0 draws, the draw is broadcast, and after the update
+        the RNG is left where the reference's early-exiting CG would leave it.
         Returns host scalars plus the new device theta (self.vec['theta_new'])."""
         L = self.lib
         s = self.shape
         self.st = st = _lib.stream_ptr()
         T, T_demo, P = batch.T, batch.T_demo, batch.P
         T_all = T + T_demo
-        self._ensure(T_all, P)
+        # global row count (all ranks): scales every mean
+        if T_global is None:
+            tg = torch.tensor([float(T)], dtype=torch.float64, device=self.device)
+            self.comm.allreduce_sum(tg)
+            T_global = float(tg.item()) if self.comm.world_size > 1 else float(T)
+        sub = None
+        if hvp_sample_frac is not None and hvp_sample_frac < 0.99 and algo != "vpg":
+            sub = self._hvp_draws(float(hvp_sample_frac), int(round(T_global)), T, int(cg_iters))
+        self._ensure(max(T_all, sub["max"]) if sub else T_all, P)
         w = self.ws
         v = self.vec
         sp = C.byref(s)
@@ -293,11 +337,6 @@ class UpdateEngine:
         else:
             adv_vpg = w["adv32"]
             T_vpg = T
-        # global row count (all ranks): scales every mean
-        if T_global is None:
-            tg = torch.tensor([float(T)], dtype=torch.float64, device=self.device)
-            self.comm.allreduce_sum(tg)
-            T_global = float(tg.item()) if self.comm.world_size > 1 else float(T)
         inv_T = 1.0 / T_global
         self.last_T, self.last_T_global = T, T_global
 
@@ -324,22 +363,27 @@ class UpdateEngine:
                                       _lib.ptr(self.packed_p), _lib.ptr(self.cg), _lib.ptr(self.done), st),
                        "mjrl_cg_init")
             prof = self.kernel_timing
-            for _ in range(int(cg_iters)):
+            inv_T_fvp = inv_T if sub is None else 1.0 / max(sub["Ts"], 1)
+            for k in range(int(cg_iters)):
+                rows_k, sc_k, T_k = rows_fvp, sc_fvp, T
+                if sub is not None:
+                    rows_k, sc_k, T_k = self._subsample_rows(sub, k, adv_vpg)
                 if prof is not None:
                     e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
                     e0.record()
-                _lib.check(L.mjrl_fvp_accumulate(sp, C.byref(rows_fvp), T, _lib.ptr(self.packed_theta),
+                _lib.check(L.mjrl_fvp_accumulate(sp, C.byref(rows_k), T_k, _lib.ptr(self.packed_theta),
                                                  _lib.ptr(self.packed_p), _lib.ptr(osc), _lib.ptr(self.done),
-                                                 C.byref(sc_fvp), st), "mjrl_fvp_accumulate")
+                                                 C.byref(sc_k), st), "mjrl_fvp_accumulate")
                 if prof is not None:
                     e1.record()
-                _lib.check(L.mjrl_gather_grads(sp, C.byref(rows_fvp), T, C.byref(sc_fvp), 0, _lib.ptr(self.done),
+                _lib.check(L.mjrl_gather_grads(sp, C.byref(rows_k), T_k, C.byref(sc_k), 0, _lib.ptr(self.done),
                                                _lib.ptr(v["gsum"]), st), "mjrl_gather_grads")
                 if prof is not None:
                     e2.record()
                     prof.append((e0, e1, e2))
                 self.comm.allreduce_sum(v["gsum"])
-                _lib.check(L.mjrl_cg_step(sp, _lib.ptr(v["gsum"]), inv_T, float(damping), _lib.ptr(self.packed_theta),
+                _lib.check(L.mjrl_cg_step(sp, _lib.ptr(v["gsum"]), inv_T_fvp, float(damping),
+                                          _lib.ptr(self.packed_theta),
                                           _lib.ptr(v["x"]), _lib.ptr(v["r"]), _lib.ptr(v["p"]), _lib.ptr(v["z"]),
                                           _lib.ptr(self.packed_p), _lib.ptr(self.cg), _lib.ptr(self.done),
                                           float(residual_tol), st), "mjrl_cg_step")
@@ -404,6 +448,12 @@ class UpdateEngine:
         stats = self.stats.cpu().numpy()
         out = self.out.cpu().numpy()
         cg = self.cg.cpu().numpy()
+        if sub is not None and sub["rng"] is not None:
+            # the reference stops drawing when its CG exits early: replay only the
+            # draws of the FVPs that ran, so numpy's global RNG ends in the same state
+            np.random.set_state(sub["rng"])
+            for _ in range(int(cg[1])):
+                np.random.choice(sub["N"], size=sub["Ts"])
         n_p = stats[S_PM1 + 2]
         base_stats = [stats[S_PM1] / n_p, math.sqrt(stats[S_PM2 + 1] / n_p), -stats[S_PM1 + 5], stats[S_PM1 + 4]]
         result = dict(
@@ -426,31 +476,89 @@ class UpdateEngine:
         return result
 
     # ------------------------------------------------------------------
+    def _hvp_draws(self, frac, N, T_local, K):
+        """K row draws np.random.choice(N, int(frac N)) (npg_cg.py:58-62) made on
+        rank 0, broadcast, and cut to this rank's rows (global index - row offset,
+        draw order kept).  One H2D / broadcast for the whole CG solve."""
+        Ts = int(frac * N)
+        comm = self.comm
+        rng = None
+        if comm.rank == 0:
+            rng = np.random.get_state()
+            d = np.stack([np.random.choice(N, size=Ts) for _ in range(K)]) if K else np.zeros((0, Ts))
+            idx = torch.from_numpy(np.ascontiguousarray(d, dtype=np.int64)).to(self.device)
+        else:
+            idx = torch.empty((K, Ts), dtype=torch.int64, device=self.device)
+        comm.broadcast(idx)
+        if comm.world_size > 1:
+            lo = comm.row_offset(T_local, self.device)
+            sel = (idx >= lo) & (idx < lo + T_local)
+            counts = sel.sum(1).cpu().numpy().astype(np.int64)
+            loc = (idx[sel] - lo).contiguous()
+        else:
+            counts = np.full(K, Ts, dtype=np.int64)
+            loc = idx.reshape(-1).contiguous()
+        offs = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+        mx = int(counts.max()) if K else 0
+        return dict(idx=loc, counts=counts, offs=offs, Ts=Ts, N=N, rng=rng, max=mx)
+
+    def _subsample_rows(self, sub, k, adv_vpg):
+        """Compact xhat / a0 / a1 rows of draw k (mjrl_gather_rows) and the Rows /
+        Scratch an FVP over them uses."""
+        s = self.shape
+        n_k = int(sub["counts"][k])
+        ip = C.c_void_p(sub["idx"].data_ptr() + 8 * int(sub["offs"][k]))
+        w = self.ws
+        cap = max(sub["max"], 1)
+        f32 = dict(dtype=torch.float32, device=self.device)
+        ws = self.__dict__.setdefault("ws_sub", {})
+        if "xs" not in ws or ws["xs"].shape[0] < cap:
+            ws["xs"] = torch.empty((cap, s.np), **f32)
+            if s.h0:
+                ws["a0s"] = torch.empty((cap, s.h0), **f32)
+                ws["a1s"] = torch.empty((cap, s.h1), **f32)
+        pairs = [("xhat", "xs", s.np)] + ([("a0", "a0s", s.h0), ("a1", "a1s", s.h1)] if s.h0 else [])
+        rows = self._rows(n_k, adv_vpg)
+        for src, dst, width in pairs:
+            _lib.check(self.lib.mjrl_gather_rows(_lib.ptr(w[src]), 4 * width, ip, n_k, _lib.ptr(ws[dst]), self.st),
+                       "mjrl_gather_rows")
+            setattr(rows, src, ws[dst].data_ptr())
+        return rows, self._scratch(n_k), n_k
+
     def accumulate_path(self):
         """Accumulate kernel the dispatcher runs for this shape: 2 = K-split
         persistent (k_ks), 1 = fused persistent (k_fused), 0 = k_rows + k_wgrad."""
         return int(self.lib.mjrl_fused_path(C.byref(self.shape)))
 
-    def fvp(self, v, damping=1e-4, T=None):
+    def fvp(self, v, damping=1e-4, T=None, idx=None):
         """F v + damping v at the parameters of the last update's forward pass
         (the caches a0/a1/mu0 and packed_theta of that pass) — NPG.HVP
         (npg_cg.py:55-74) as a standalone call, used by parity tests and
-        `NPG.HVP`.  `v`: f32 device tensor [d].  Returns a new device tensor."""
+        `NPG.HVP`.  `v`: f32 device tensor [d].  `idx` (int64 device tensor):
+        the rows of a subsampled Fisher (npg_cg.py:58-62), gathered as in the
+        update's CG loop.  Returns a new device tensor."""
         L = self.lib
         s = self.shape
         sp = C.byref(s)
         self.st = st = _lib.stream_ptr()
         T = self.last_T if T is None else T
         vv = self.vec
-        scratch = self._scratch(T)
-        rows = self._rows(T, self.ws["adv32"])
+        T_global = self.last_T_global
+        if idx is not None:
+            n = int(idx.numel())
+            sub = dict(idx=idx.contiguous(), counts=[n], offs=[0], max=n)
+            self._ensure(max(self.cap_T, n), self.cap_P)
+            rows, scratch, T = self._subsample_rows(sub, 0, self.ws["adv32"])
+            T_global = float(n)
+        else:
+            scratch = self._scratch(T)
+            rows = self._rows(T, self.ws["adv32"])
         _lib.check(L.mjrl_cg_init(sp, _lib.ptr(v), _lib.ptr(vv["x"]), _lib.ptr(vv["r"]), _lib.ptr(vv["p"]),
                                   _lib.ptr(self.packed_p), _lib.ptr(self.cg), _lib.ptr(self.done), st), "mjrl_cg_init")
         _lib.check(L.mjrl_policy_fvp(sp, C.byref(rows), T, _lib.ptr(self.packed_theta), _lib.ptr(self.packed_p),
                                      _lib.ptr(self.transforms[3]), C.byref(scratch), _lib.ptr(self.done),
                                      _lib.ptr(vv["gsum"]), st), "mjrl_policy_fvp")
         self.comm.allreduce_sum(vv["gsum"])
-        T_global = self.last_T_global
         _lib.check(L.mjrl_cg_step(sp, _lib.ptr(vv["gsum"]), 1.0 / T_global, float(damping),
                                   _lib.ptr(self.packed_theta), _lib.ptr(vv["x"]), _lib.ptr(vv["r"]), _lib.ptr(vv["p"]),
                                   _lib.ptr(vv["z"]), _lib.ptr(self.packed_p), _lib.ptr(self.cg), _lib.ptr(self.done),

@@ -245,13 +245,18 @@ def cg_solve(f_Ax, b, iters=10, tol=1e-10, trace=None):
 # --------------------------------------------------------------------------
 def update(policy, obs, act, adv_raw, rewards, lengths, algo="npg", *,
            n_step_size=0.01, const_lr=None, kl_dist=None, cg_iters=10, damping=1e-4,
-           demo_obs=None, demo_act=None, demo_coef=None, trace=None):
+           demo_obs=None, demo_act=None, demo_coef=None, trace=None, hvp_sample_frac=None, np_seed=None):
     """Runs the policy update on concatenated arrays and returns a result dict.
 
     algo: 'npg'  (npg_cg.py:84-165), 'trpo' (trpo.py:54-145), 'dapg' (dapg.py:54-141).
     For 'npg' with kl_dist set, n_step_size = 2*kl_dist (npg_cg.py:47).
     For 'dapg', demo_coef = lam_0 * lam_1**iter_count (dapg.py:65).
+    hvp_sample_frac < 0.99: every Fisher-vector product runs on
+    np.random.choice(N, int(frac N)) rows (with replacement) drawn from numpy's
+    global RNG (npg_cg.py:58-62); np_seed, if given, seeds it first.
     """
+    if np_seed is not None:
+        np.random.seed(np_seed)
     res = {}
     adv = whiten(adv_raw)
     res["adv_whitened"] = adv
@@ -269,7 +274,13 @@ def update(policy, obs, act, adv_raw, rewards, lengths, algo="npg", *,
     res["vpg_grad"] = g
 
     cg_trace = [] if trace else None
-    x = cg_solve(lambda v: policy.fvp(obs, act, v, damping), g, iters=cg_iters, trace=cg_trace)
+    def f_Ax(v):
+        if hvp_sample_frac is not None and hvp_sample_frac < 0.99:
+            idx = np.random.choice(obs.shape[0], size=int(hvp_sample_frac * obs.shape[0]))
+            return policy.fvp(obs[idx], act[idx], v, damping)
+        return policy.fvp(obs, act, v, damping)
+
+    x = cg_solve(f_Ax, g, iters=cg_iters, trace=cg_trace)
     res["npg_grad"] = x
     res["cg_trace"] = cg_trace
     gx = np.dot(g.T, x)
@@ -313,6 +324,31 @@ def update(policy, obs, act, adv_raw, rewards, lengths, algo="npg", *,
     return res
 
 
+def hvp_rows(c):
+    """Row indices of a fixture's standalone NPG.HVP call: all rows, or — for a
+    subsampled Fisher — the draw the reference made after np.random.seed(hvp_np_seed)
+    (npg_cg.py:58-62)."""
+    N = c["obs"].shape[0]
+    frac = float(c["kw_hvp_sample_frac"]) if "kw_hvp_sample_frac" in c else 1.0
+    if frac >= 0.99:
+        return np.arange(N)
+    np.random.seed(int(c["hvp_np_seed"]))
+    return np.random.choice(N, size=int(frac * N))
+
+
+def cg_rows(c):
+    """Row indices of each Fisher-vector product in the fixture's CG trace: the
+    k-th draw after np.random.seed(np_seed), the reference's only global-RNG use
+    in train_from_paths (npg_cg.py:58-62, cg_solve.py:10)."""
+    N = c["obs"].shape[0]
+    frac = float(c["kw_hvp_sample_frac"]) if "kw_hvp_sample_frac" in c else 1.0
+    k = int(c["cg_iters_run"])
+    if frac >= 0.99:
+        return [np.arange(N)] * k
+    np.random.seed(int(c["np_seed"]))
+    return [np.random.choice(N, size=int(frac * N)) for _ in range(k)]
+
+
 def load_case(path):
     """Loads a golden fixture into oracle-ready arrays."""
     z = np.load(path, allow_pickle=False)
@@ -332,6 +368,10 @@ def case_kwargs(c):
     """Algorithm kwargs of a fixture, in update()'s vocabulary."""
     algo = str(c["algo"])
     kw = dict(algo=algo)
+    if "kw_hvp_sample_frac" in c:
+        kw["hvp_sample_frac"] = float(c["kw_hvp_sample_frac"])
+    if "np_seed" in c:
+        kw["np_seed"] = int(c["np_seed"])
     if "kw_FIM_invert_args" in c:
         kw["cg_iters"] = int(c["kw_FIM_invert_args"][0])
         kw["damping"] = float(c["kw_FIM_invert_args"][1])

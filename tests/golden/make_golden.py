@@ -134,17 +134,23 @@ def concat(paths, key):
     return np.concatenate([p[key] for p in paths])
 
 
-def run_case(name, **kw):
+ONLY = set(sys.argv[1:])   # optional: regenerate only the named cases
+
+
+def run_case(name, reverse_alt=True, **kw):
     """Runs the reference at 1 torch thread (the fixture), again at 8 threads, and
     again at 1 thread with the path order reversed (the same batch, every sum over
     timesteps reordered).  The largest difference to the fixture (the reference's
     own reduction-order sensitivity) is stored as spread_*
     and calibrates the end-to-end tolerances of the GPU parity tests."""
+    if ONLY and name not in ONLY:
+        return None
     torch.set_num_threads(8)
-    alt8 = _run(None, **kw)
+    alts = [_run(None, **kw)]
     torch.set_num_threads(1)
-    altr = _run(None, reverse=True, **kw)
-    out = _run(name, alt=[alt8, altr], **kw)
+    if reverse_alt:   # (a subsampled Fisher draws other rows once reversed: no reversal there)
+        alts.append(_run(None, reverse=True, **kw))
+    out = _run(name, alt=alts, **kw)
     _err64(name, out)
     return out
 
@@ -185,7 +191,7 @@ def _nrel(a, b):
 def _run(name, *, n, m, hidden, lengths, terminated, algo, algo_kwargs,
          gamma=0.995, gae_lambda=0.97, seed=123, policy_seed=0,
          log_std=None, transforms=None, demo=None, linear=False,
-         baseline_fit=True, alt=None, reverse=False):
+         baseline_fit=True, alt=None, reverse=False, np_seed=None):
     rs = np.random.RandomState(seed)
     spec = EnvSpec(n, m, max(lengths), 1)
     if linear:
@@ -227,12 +233,16 @@ def _run(name, *, n, m, hidden, lengths, terminated, algo, algo_kwargs,
     mean0, ll0 = policy.mean_LL(obs, act)
     vrs = np.random.RandomState(seed + 7)
     hvp_v = vrs.randn(policy.d).astype(np.float32)
+    if np_seed is not None:   # the subsampled HVP draws from numpy's global RNG (npg_cg.py:58-62)
+        np.random.seed(np_seed + 1)
     hvp_out = agent.HVP(obs, act, hvp_v)
 
     # the update proper (batch_reinforce.py:86-91 minus sampling and fit)
     process_samples.compute_returns(paths, gamma)
     process_samples.compute_advantages(paths, baseline, gamma, gae_lambda)
     rec = Recorder(agent, [npg_mod, trpo_mod, dapg_mod])
+    if np_seed is not None:
+        np.random.seed(np_seed)
     try:
         base_stats = agent.train_from_paths(paths)
     finally:
@@ -271,6 +281,9 @@ def _run(name, *, n, m, hidden, lengths, terminated, algo, algo_kwargs,
         base_stats=np.array(base_stats, dtype=np.float64),
         running_score=agent.running_score,
     )
+    if np_seed is not None:
+        out["np_seed"] = np.int64(np_seed)
+        out["hvp_np_seed"] = np.int64(np_seed + 1)
     for k, v in agent.logger.log.items():
         out["log_" + k] = np.array(v[-1], dtype=np.float64)
     for k, v in algo_kwargs.items():
@@ -321,6 +334,11 @@ def main():
     run_case("c2_constlr", n=8, m=2, hidden=(64, 64), lengths=[100] * 10,
              terminated=[False] * 10, algo="npg",
              algo_kwargs=dict(const_learn_rate=0.05), seed=12)
+    # C2s: NPG with a subsampled Fisher (hvp_sample_frac = 0.5, npg_cg.py:58-62)
+    run_case("c2_hvp_sub", n=8, m=2, hidden=(64, 64), lengths=[200] * 20,
+             terminated=[False] * 20, algo="npg",
+             algo_kwargs=dict(normalized_step_size=0.1, hvp_sample_frac=0.5), seed=31, np_seed=2024,
+             reverse_alt=False)
     # C3: HalfCheetah shape, TRPO (reduced to 10 x 1000)
     run_case("c3_halfcheetah_trpo", n=17, m=6, hidden=(128, 128),
              lengths=[1000] * 10, terminated=[False] * 10, algo="trpo",
@@ -368,4 +386,5 @@ def baselines_case():
 
 if __name__ == "__main__":
     main()
-    baselines_case()
+    if not ONLY or "baselines" in ONLY:
+        baselines_case()

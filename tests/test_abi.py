@@ -70,6 +70,9 @@ def test_null_arguments_fail_loudly(lib):
     assert lib.mjrl_pack_batch(None, None, 10, C.byref(s), None, None, None, None, None) == _lib.MJRL_EINVAL
     assert lib.mjrl_gae(None, None, None, None, 5, 0.99, 0.97, 1, None, None, None, None) == _lib.MJRL_EINVAL
     assert lib.mjrl_policy_fvp(C.byref(s), None, 10, None, None, None, None, None, None, None) == _lib.MJRL_EINVAL
+    assert lib.mjrl_gather_rows(None, 16, None, 4, None, None) == _lib.MJRL_EINVAL
+    assert lib.mjrl_gather_rows(C.c_void_p(16), 6, C.c_void_p(16), 4, C.c_void_p(16), None) == _lib.MJRL_EINVAL
+    assert lib.mjrl_gather_rows(None, 16, None, 0, None, None) == _lib.MJRL_OK
 
 
 def test_no_gpu_means_no_compute():

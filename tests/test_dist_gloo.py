@@ -108,3 +108,48 @@ def test_sharded_schedule_equals_unsharded(name):
     assert np.array_equal(x0, x1)
     tol = max(1e-3, 3 * float(c["spread_x"]), 2 * float(c["err64_x"]))
     assert np.linalg.norm(x0 - c["cg_x"]) / np.linalg.norm(c["cg_x"]) < tol
+
+
+def _draw_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from types import SimpleNamespace
+        from mjrl_amd.comm import DistComm
+        from mjrl_amd.engine import UpdateEngine
+        T_local = [700, 300][rank]
+        np.random.seed(5 if rank == 0 else 77)   # only rank 0's RNG may matter
+        fake = SimpleNamespace(comm=DistComm(), device=torch.device("cpu"))
+        sub = UpdateEngine._hvp_draws(fake, 0.5, 1000, T_local, 4)
+        q.put((rank, sub["idx"].numpy(), sub["counts"], sub["offs"], sub["Ts"], np.random.rand()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_subsampled_fisher_draw_sharding():
+    """hvp_sample_frac < 1 on 2 ranks: rank 0's np.random.choice draws
+    (npg_cg.py:58-62) are broadcast and each rank keeps its own rows, in draw
+    order; together the shards hold exactly the reference's draw."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_draw_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(world):
+        r, *vals = q.get(timeout=300)
+        out[r] = vals
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    np.random.seed(5)
+    ref = [np.random.choice(1000, size=500) for _ in range(4)]
+    assert out[0][3] == out[1][3] == 500
+    for k in range(4):
+        i0 = out[0][0][out[0][2][k]:out[0][2][k + 1]]
+        i1 = out[1][0][out[1][2][k]:out[1][2][k + 1]] + 700
+        assert np.array_equal(i0, ref[k][ref[k] < 700])
+        assert np.array_equal(i1, ref[k][ref[k] >= 700])

@@ -69,6 +69,8 @@ def make_agent(name, c, pol, spec):
             args["normalized_step_size"] = float(c["kw_normalized_step_size"])
         if "kw_const_learn_rate" in c:
             args["const_learn_rate"] = float(c["kw_const_learn_rate"])
+        if "kw_hvp_sample_frac" in c:
+            args["hvp_sample_frac"] = float(c["kw_hvp_sample_frac"])
         return NPG(None, pol, base, save_logs=True, **args), base
     if kw["algo"] == "trpo":
         return TRPO(None, pol, base, kl_dist=kw["kl_dist"], save_logs=True), base
@@ -84,11 +86,13 @@ REF_KEYS = {"npg": {"alpha", "delta", "time_vpg", "time_npg", "kl_dist", "surr_i
 
 
 @pytest.mark.parametrize("name", ["c1_pointmass_linear", "c2_swimmer", "c3_trpo_backtrack", "c4_humanoid",
-                                  "c5_door_dapg", "c2_constlr"])
+                                  "c5_door_dapg", "c2_constlr", "c2_hvp_sub"])
 def test_train_from_paths(name):
     c = load(name)
     pol, spec = make_policy(c)
     agent, _ = make_agent(name, c, pol, spec)
+    if "np_seed" in c:
+        np.random.seed(int(c["np_seed"]))
     stats = agent.train_from_paths(paths_of(c))
     np.testing.assert_allclose(stats, c["base_stats"], rtol=1e-12)
     assert nrel(pol.get_param_values(), c["theta1"]) < tol(c, "theta", 1e-3)
@@ -333,3 +337,14 @@ def test_gae_kernel_multiwindow_bitexact(use_gae):
     pr = pret.cpu().numpy()
     assert np.array_equal(pr[keep], np.array([sum(r) for r in O.split(rew[m], lengths[keep])]))
     assert pr[~keep].tolist() == [0.0]
+
+
+def test_subsampled_hvp_api():
+    """NPG.HVP with hvp_sample_frac < 1 through the drop-in API: the reference's
+    np.random.choice draw from numpy's global RNG (npg_cg.py:58-62)."""
+    c = load("c2_hvp_sub")
+    pol, spec = make_policy(c)
+    agent, _ = make_agent("c2_hvp_sub", c, pol, spec)
+    np.random.seed(int(c["hvp_np_seed"]))
+    hv = agent.HVP(c["obs64"], c["act64"], c["hvp_v"])
+    assert nrel(hv, c["hvp_out"]) < 1e-5

@@ -50,13 +50,18 @@ def _worker(rank, world, port, name, q):
             args["n_step_size"] = kw.get("n_step_size", 0.01)
         else:
             args["kl_dist"] = kw["kl_dist"]
+        if "hvp_sample_frac" in kw:
+            # rank 0 draws (and must match the reference's draws); rank 1's RNG is
+            # deliberately different to show the broadcast is what it uses
+            args["hvp_sample_frac"] = kw["hvp_sample_frac"]
+            np.random.seed(kw["np_seed"] if rank == 0 else 99)
         res = eng.update(b, t(c["theta0"].astype(np.float32)), **args)
         q.put((rank, eng.vec["theta_new"].cpu().numpy(), res["base_stats"], res["kl_dist"], res["alpha"]))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name", ["c2_ragged", "c3_halfcheetah_trpo"])
+@pytest.mark.parametrize("name", ["c2_ragged", "c3_halfcheetah_trpo", "c2_hvp_sub"])
 def test_two_rank_update(name):
     from oracle import npg_cpu as O
     world = 2

@@ -86,6 +86,10 @@ def run_case(name):
         args.update(kl_dist=kw["kl_dist"])
     if algo == "dapg":
         args.update(demo_coef=kw["demo_coef"])
+    if "hvp_sample_frac" in kw:
+        args.update(hvp_sample_frac=kw["hvp_sample_frac"])
+    if "np_seed" in kw:   # subsampled Fisher: the reference's global-RNG draws (npg_cg.py:58-62)
+        np.random.seed(kw["np_seed"])
     res = eng.update(batch, theta, **args)
     return c, kw, eng, res
 
@@ -122,6 +126,11 @@ def test_update_matches_reference(name):
     np.testing.assert_allclose(res["surr_after"], surr_o, rtol=1e-4, atol=1e-7)
     if kw["algo"] == "trpo":
         assert len(res["trials"]) == len(c["kl_calls"]) - 1
+    if "np_seed" in kw:
+        # numpy's global RNG ends where the reference's CG left it
+        after = np.random.rand()
+        O.cg_rows(c)
+        assert after == np.random.rand()
 
 
 @pytest.mark.parametrize("name", CASES)
@@ -129,8 +138,11 @@ def test_fvp_and_teacher_forced_cg(name):
     c, kw, eng, res = run_case(name)
     dev = torch.device("cuda:0")
     damping = kw.get("damping", 1e-4)
-    fv = eng.fvp(torch.from_numpy(c["hvp_v"]).to(dev), damping=damping).cpu().numpy()
+    from oracle import npg_cpu as O
+    sub = "kw_hvp_sample_frac" in c
+    ix = lambda i: torch.from_numpy(np.asarray(i, np.int64)).to(dev) if sub else None
+    fv = eng.fvp(torch.from_numpy(c["hvp_v"]).to(dev), damping=damping, idx=ix(O.hvp_rows(c))).cpu().numpy()
     assert nrel(fv, c["hvp_out"]) < 1e-5, nrel(fv, c["hvp_out"])
-    for p, z in zip(c["cg_p"], c["cg_z"]):
-        zz = eng.fvp(torch.from_numpy(p.astype(np.float32)).to(dev), damping=damping).cpu().numpy()
+    for p, z, rows in zip(c["cg_p"], c["cg_z"], O.cg_rows(c)):
+        zz = eng.fvp(torch.from_numpy(p.astype(np.float32)).to(dev), damping=damping, idx=ix(rows)).cpu().numpy()
         assert nrel(zz, z) < 1e-5, nrel(zz, z)

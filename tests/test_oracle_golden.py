@@ -72,7 +72,8 @@ def test_policy_forward_and_grads(name):
     assert nrel(mu.detach().numpy(), c["mean0"]) < 1e-6
     assert nrel(ll.detach().numpy(), c["ll0"]) < 1e-6
     kw = O.case_kwargs(c)
-    fv = pol.fvp(c["obs64"], c["act64"], c["hvp_v"], kw.get("damping", 1e-4))
+    idx = O.hvp_rows(c)
+    fv = pol.fvp(c["obs64"][idx], c["act64"][idx], c["hvp_v"], kw.get("damping", 1e-4))
     assert nrel(fv, c["hvp_out"]) < 1e-5
     if kw["algo"] != "dapg":
         g = pol.flat_vpg(c["obs64"], c["act64"], c["adv_whitened"])
@@ -86,8 +87,8 @@ def test_cg_teacher_forced(name):
     torch.set_num_threads(1)
     pol = O.Policy(int(c["n"]), int(c["m"]), c["hidden_t"], c["theta0"], c["transforms"])
     damping = O.case_kwargs(c).get("damping", 1e-4)
-    for p, z in zip(c["cg_p"], c["cg_z"]):
-        assert nrel(pol.fvp(c["obs64"], c["act64"], p, damping), z) < 1e-5
+    for p, z, idx in zip(c["cg_p"], c["cg_z"], O.cg_rows(c)):
+        assert nrel(pol.fvp(c["obs64"][idx], c["act64"][idx], p, damping), z) < 1e-5
 
 
 @pytest.mark.parametrize("name", CASES)

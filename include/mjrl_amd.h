@@ -102,6 +102,23 @@ int mjrl_gae(const double* rew, const double* base, const int64_t* path_off,
 int mjrl_linear_baseline(const double* obs, int64_t T, int32_t n, const int64_t* path_off,
                          int64_t P, const double* coeffs, double* out, void* stream);
 
+/* ---- LinearBaseline.fit normal equations on device (baselines/linear_baseline.py:20-44) ----
+ * Gram matrix of the augmented rows [f_t, y_t], f_t = [clip(obs_t, +-10), a, a^2, a^3, 1]
+ * (a = (t - path start)/1000, as _features), y_t = returns: out[K][K] row-major fp64 with
+ * K = n + 5, so out[:k][:k] = F^T F, out[:k][k] = F^T y, out[k][k] = y^T y (k = n + 4).
+ * The (F^T F + reg I) c = F^T y lstsq retry loop stays with the caller (k x k, host).
+ * scratch: mjrl_linear_baseline_gram_scratch() doubles (split-K slabs + path times);
+ * deterministic (fixed slice order, no atomics). */
+int mjrl_linear_baseline_gram_scratch(int32_t n, int64_t T, int64_t* doubles);
+int mjrl_linear_baseline_gram(const double* obs, const double* returns, int64_t T, int32_t n,
+                              const int64_t* path_off, int64_t P, double* scratch, double* out,
+                              void* stream);
+/* out[t] = returns[t] - f_t . coeffs (fit(return_errors=True)'s residuals);
+ * scratch as for mjrl_linear_baseline_gram. */
+int mjrl_linear_baseline_residual(const double* obs, const double* returns, int64_t T, int32_t n,
+                                  const int64_t* path_off, int64_t P, const double* coeffs,
+                                  double* scratch, double* out, void* stream);
+
 /* ---- subsampled Fisher rows (npg_cg.py:58-62: obs[rand_idx], act[rand_idx]) ----
  * dst row i = src row idx[i] for i < n, rows of row_bytes bytes (a multiple of 4);
  * indices may repeat (np.random.choice draws with replacement).  Used to build

@@ -67,6 +67,9 @@ SIGNATURES = {
     "mjrl_cg_update": [I32, P, P, P, P, P, P, F32, P],
     "mjrl_scale_vec": [P, I32, F64, P, P],
     "mjrl_gather_rows": [P, I64, P, I64, P, P],
+    "mjrl_linear_baseline_gram_scratch": [I32, I64, C.POINTER(I64)],
+    "mjrl_linear_baseline_gram": [P, P, I64, I32, P, I64, P, P, P],
+    "mjrl_linear_baseline_residual": [P, P, I64, I32, P, I64, P, P, P, P],
     "mjrl_npg_step": [SP, P, P, P, I32, F32, F32, I32, F32, P, P, P, P],
 }
 

@@ -53,6 +53,7 @@ class BatchREINFORCE:
     def __getstate__(self):
         d = dict(self.__dict__)
         d["_engine"] = None
+        d["_last_batch"] = None   # device tensors
         return d
 
     def engine(self):
@@ -116,13 +117,24 @@ class BatchREINFORCE:
         eval_statistics.append(N)
         if self.save_logs:
             ts = timer.time()
-            error_before, error_after = self.baseline.fit(paths, return_errors=True)
+            error_before, error_after = self._fit_baseline(paths, return_errors=True)
             self.logger.log_kv("time_VF", timer.time() - ts)
             self.logger.log_kv("VF_error_before", error_before)
             self.logger.log_kv("VF_error_after", error_after)
         else:
-            self.baseline.fit(paths)
+            self._fit_baseline(paths)
         return eval_statistics
+
+    def _fit_baseline(self, paths, return_errors=False):
+        """baseline.fit(paths) (batch_reinforce.py:93-101).  A LinearBaseline is
+        fitted on the device from the batch still in HBM (its Gram products are
+        the T x k work); other baselines fit on the host."""
+        batch = getattr(self, "_last_batch", None)
+        if batch is not None and type(self.baseline).__name__ == "LinearBaseline" \
+                and hasattr(self.baseline, "_reg_coeff") and batch.T == sum(len(p["rewards"]) for p in paths):
+            self._last_batch = None
+            return self.engine().fit_linear_baseline(batch, self.baseline, return_errors=return_errors)
+        return self.baseline.fit(paths, return_errors=return_errors) if return_errors else self.baseline.fit(paths)
 
     def train_from_samples(self, paths, gamma, gae_lambda):
         """Returns + advantages + update from raw sampled paths with one staging:
@@ -139,7 +151,9 @@ class BatchREINFORCE:
             p["returns"] = ret[off[i]:off[i + 1]]
             p["baseline"] = base[off[i]:off[i + 1]]
             p["advantages"] = adv[off[i]:off[i + 1]]
-        return self._update(batch, paths, skip_gae=True, gamma=gamma)
+        out = self._update(batch, paths, skip_gae=True, gamma=gamma)
+        self._last_batch = batch   # obs + returns stay in HBM for the baseline fit
+        return out
 
     def train_from_paths(self, paths):
         eng = self.engine()

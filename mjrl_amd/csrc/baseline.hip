@@ -1,0 +1,261 @@
+// baseline.hip — LinearBaseline.fit on the device.
+//
+// Reference: mjrl/baselines/linear_baseline.py:10-44.  fit() builds the feature
+// matrix F = [clip(obs, +-10), a, a^2, a^3, 1] (a = index within the path / 1000)
+// and solves (F^T F + reg I) c = F^T y by lstsq, retrying with 10x reg on NaN.
+// The T x k products are the whole cost (Humanoid 1M: k = 380, 2 T k^2 = 289
+// GFLOP fp64); the k x k solve stays on the host, exactly as the reference runs it.
+//
+// k_gram computes the Gram matrix of the augmented rows [f_t, y_t] (k+1 = n+5
+// columns: F^T F, F^T y and y^T y in one pass) with v_mfma_f64_16x16x4_f64:
+//   - output 64 x 64 tiles of the upper triangle; workgroup = 4 waves, each wave
+//     a 32 x 32 quarter (2 x 2 MFMA tiles, 16 f64 accumulators per lane);
+//   - split-K over row slices (fixed slice count), slabs reduced in slice order
+//     by k_gram_reduce (deterministic, no atomics);
+//   - features are built on the fly from obs (HBM read once per XCD: the pair
+//     tiles of one row slice are mapped to the same XCD so they share its L2);
+//   - 32-row chunks double-buffered through LDS, the next chunk's loads in
+//     registers while the current one is multiplied.
+#include <math.h>
+
+#include "common.h"
+
+using namespace mjrl;
+
+namespace {
+
+typedef double doublex4 __attribute__((ext_vector_type(4)));
+
+constexpr int GT = 64;          // output tile
+constexpr int GRC = 32;         // rows per chunk
+constexpr int GLD = GT + 16;    // LDS row stride (doubles): rows 1 apart land 32 banks apart
+constexpr int GSLICES = 24;     // row slices (multiple of 8: one XCD per slice group)
+constexpr int GTHREADS = 256;
+
+// a_t = (t - path start) / 1000 for every row (np.arange(l) / 1000.0); one wave per path
+__global__ void __launch_bounds__(256) k_path_time(const int64_t* __restrict__ off, int64_t P,
+                                                   double* __restrict__ al) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t p = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; p < P; p += nw) {
+        const int64_t b = off[p], e = off[p + 1];
+        for (int64_t t = b + lane; t < e; t += 64) al[t] = (double)(t - b) / 1000.0;
+    }
+}
+
+// feature g of row `row` (linear_baseline.py:10-18), the return as feature n + 4, zero pad
+__device__ __forceinline__ double feat(const double* __restrict__ obs, const double* __restrict__ y,
+                                       const double* __restrict__ al, int64_t row, int g, int n) {
+    if (g < n) {
+        const double o = obs[row * n + g];
+        return o < -10.0 ? -10.0 : (o > 10.0 ? 10.0 : o);
+    }
+    const double a = al[row];
+    switch (g - n) {
+        case 0: return a;
+        case 1: return a * a;
+        case 2: return pow(a, 3.0);
+        case 3: return 1.0;
+        case 4: return y[row];
+        default: return 0.0;
+    }
+}
+
+struct GramArgs {
+    const double* obs;
+    const double* y;
+    const double* al;
+    int64_t T;
+    int n, ntile, npair;
+    double* slab;   // [GSLICES][npair][GT][GT]
+};
+
+__global__ void __launch_bounds__(GTHREADS, 2) k_gram(GramArgs a) {
+    __shared__ __attribute__((aligned(16))) double PI[2][GRC][GLD];
+    __shared__ __attribute__((aligned(16))) double PJ[2][GRC][GLD];
+    // block -> (slice, pair): the npair blocks of a slice sit on one XCD (b % 8)
+    const int b = blockIdx.x, xcd = b & 7, loc = b >> 3;
+    const int slice = (loc / a.npair) * 8 + xcd, pair = loc % a.npair;
+    if (slice >= GSLICES) return;
+    int ti = 0, rem = pair;
+    while (rem >= a.ntile - ti) {
+        rem -= a.ntile - ti;
+        ++ti;
+    }
+    const int tj = ti + rem;
+    const int64_t per = (a.T + GSLICES - 1) / GSLICES;
+    const int64_t r0 = (int64_t)slice * per, r1 = r0 + per < a.T ? r0 + per : a.T;
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wr = w >> 1, wc = w & 1;
+    // loader: thread -> (row tid / 8, columns 8 (tid % 8) .. +8) of both panels
+    const int lr = tid >> 3, lc = (tid & 7) * 8;
+    double vi[8], vj[8];
+    auto gload = [&](int64_t c0) {
+        const int64_t row = c0 + lr;
+        const bool in = row < r1;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            vi[u] = in ? feat(a.obs, a.y, a.al, row, ti * GT + lc + u, a.n) : 0.0;
+            vj[u] = in ? feat(a.obs, a.y, a.al, row, tj * GT + lc + u, a.n) : 0.0;
+        }
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            PI[buf][lr][lc + u] = vi[u];
+            PJ[buf][lr][lc + u] = vj[u];
+        }
+    };
+
+    doublex4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = doublex4{0.0, 0.0, 0.0, 0.0};
+
+    const int r16 = lane & 15, q = lane >> 4;
+    int buf = 0;
+    if (r0 < r1) {
+        gload(r0);
+        lstore(0);
+    }
+    __syncthreads();
+    for (int64_t c0 = r0; c0 < r1; c0 += GRC) {
+        const bool more = c0 + GRC < r1;
+        if (more) gload(c0 + GRC);
+#pragma unroll
+        for (int k = 0; k < GRC; k += 4) {
+            double av[2], bv[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) av[i] = PI[buf][k + q][wr * 32 + i * 16 + r16];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) bv[j] = PJ[buf][k + q][wc * 32 + j * 16 + r16];
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], bv[j], acc[i][j], 0, 0, 0);
+        }
+        if (more) lstore(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+    double* out = a.slab + ((int64_t)slice * a.npair + pair) * GT * GT;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = wr * 32 + i * 16 + q + 4 * r;   // f64 C/D map: row = (l>>4) + 4 reg
+                const int col = wc * 32 + j * 16 + r16;
+                out[row * GT + col] = acc[i][j][r];
+            }
+}
+
+// out[K][K] (K = n + 5) = sum over slices (in order) of the slab tiles, mirrored
+__global__ void __launch_bounds__(256) k_gram_reduce(const double* __restrict__ slab, int ntile, int npair, int K,
+                                                     double* __restrict__ out) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (int64_t)npair * GT * GT) return;
+    const int pair = (int)(e / (GT * GT)), rc = (int)(e % (GT * GT));
+    int ti = 0, rem = pair;
+    while (rem >= ntile - ti) {
+        rem -= ntile - ti;
+        ++ti;
+    }
+    const int tj = ti + rem;
+    const int gi = ti * GT + rc / GT, gj = tj * GT + rc % GT;
+    if (gi >= K || gj >= K || (ti == tj && gj < gi)) return;
+    double s = 0.0;
+    for (int sl = 0; sl < GSLICES; ++sl) s += slab[((int64_t)sl * npair + pair) * GT * GT + rc];
+    out[(int64_t)gi * K + gj] = s;
+    out[(int64_t)gj * K + gi] = s;
+}
+
+// r_t = y_t - [clip(o_t), a, a^2, a^3, 1] . c  (fit(return_errors=True)'s residuals)
+__global__ void __launch_bounds__(256) k_linear_residual(const double* __restrict__ obs, const double* __restrict__ y,
+                                                         const double* __restrict__ al, int64_t T, int n,
+                                                         const double* __restrict__ coef, double* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t row = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; row < T; row += nw) {
+        double acc = 0.0;
+        for (int j = lane; j < n; j += 64) {
+            double o = obs[row * n + j];
+            o = o < -10.0 ? -10.0 : (o > 10.0 ? 10.0 : o);
+            acc += o * coef[j];
+        }
+        acc = wave_sum(acc);
+        if (lane == 0) {
+            const double t = al[row];
+            acc += t * coef[n] + (t * t) * coef[n + 1] + pow(t, 3.0) * coef[n + 2] + coef[n + 3];
+            out[row] = y[row] - acc;
+        }
+    }
+}
+
+inline int err(hipError_t e) { return e == hipSuccess ? MJRL_OK : (int)e; }
+
+inline void gram_dims(int n, int& K, int& ntile, int& npair) {
+    K = n + 5;
+    ntile = (K + GT - 1) / GT;
+    npair = ntile * (ntile + 1) / 2;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mjrl_linear_baseline_gram_scratch(int32_t n, int64_t T, int64_t* doubles) {
+    if (n <= 0 || T < 0 || !doubles) return MJRL_EINVAL;
+    int K, ntile, npair;
+    gram_dims(n, K, ntile, npair);
+    *doubles = (int64_t)GSLICES * npair * GT * GT + T;
+    return MJRL_OK;
+}
+
+int mjrl_linear_baseline_gram(const double* obs, const double* returns, int64_t T, int32_t n,
+                              const int64_t* path_off, int64_t P, double* scratch, double* out, void* stream) {
+    if (n <= 0 || T < 0 || P < 0 || !out || !scratch || (T > 0 && (!obs || !returns || !path_off)))
+        return MJRL_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    int K, ntile, npair;
+    gram_dims(n, K, ntile, npair);
+    double* slab = scratch;
+    double* al = scratch + (int64_t)GSLICES * npair * GT * GT;
+    if (P > 0) {
+        const int64_t g = (P + 3) / 4;
+        hipLaunchKernelGGL(k_path_time, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, st, path_off, P, al);
+    }
+    GramArgs ga{obs, returns, al, T, n, ntile, npair, slab};
+    const int groups = (GSLICES + 7) / 8;   // slices per XCD
+    hipLaunchKernelGGL(k_gram, dim3(8 * groups * npair), dim3(GTHREADS), 0, st, ga);
+    const int64_t ne = (int64_t)npair * GT * GT;
+    hipLaunchKernelGGL(k_gram_reduce, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st, slab, ntile, npair, K,
+                       out);
+    return err(hipGetLastError());
+}
+
+int mjrl_linear_baseline_residual(const double* obs, const double* returns, int64_t T, int32_t n,
+                                  const int64_t* path_off, int64_t P, const double* coeffs, double* scratch,
+                                  double* out, void* stream) {
+    if (n <= 0 || T < 0 || P < 0 || (T > 0 && (!obs || !returns || !path_off || !coeffs || !scratch || !out)))
+        return MJRL_EINVAL;
+    if (T == 0) return MJRL_OK;
+    hipStream_t st = (hipStream_t)stream;
+    int K, ntile, npair;
+    gram_dims(n, K, ntile, npair);
+    double* al = scratch + (int64_t)GSLICES * npair * GT * GT;
+    if (P > 0) {
+        const int64_t g = (P + 3) / 4;
+        hipLaunchKernelGGL(k_path_time, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, st, path_off, P, al);
+    }
+    const int64_t g = (T + 3) / 4;
+    hipLaunchKernelGGL(k_linear_residual, dim3((unsigned)(g < 16384 ? g : 16384)), dim3(256), 0, st, obs, returns,
+                       al, T, n, coeffs, out);
+    return err(hipGetLastError());
+}
+
+}  // extern "C"

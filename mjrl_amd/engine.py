@@ -476,6 +476,54 @@ class UpdateEngine:
         return result
 
     # ------------------------------------------------------------------
+    def fit_linear_baseline(self, batch, baseline, returns=None, return_errors=False):
+        """LinearBaseline.fit (baselines/linear_baseline.py:20-44) on the batch's
+        RL rows already in HBM: the Gram products [F y]^T [F y] on the device
+        (mjrl_linear_baseline_gram, all-reduced when sharded), then the
+        reference's own lstsq retry loop on the k x k system.  `returns`: f64
+        device [T] (default: the returns of the last GAE scan).  Sets
+        baseline._coeffs; with return_errors, returns (error_before, error_after)
+        computed from device residuals as the reference does."""
+        L = self.lib
+        st = _lib.stream_ptr()
+        n, T, P = int(batch.obs.shape[1]), batch.T, batch.P
+        k = n + 4
+        y = returns if returns is not None else self.ws["ret"][:T]
+        nd = C.c_int64()
+        _lib.check(L.mjrl_linear_baseline_gram_scratch(n, T, C.byref(nd)), "mjrl_linear_baseline_gram_scratch")
+        f64 = dict(dtype=torch.float64, device=self.device)
+        scratch = torch.empty(max(nd.value, 1), **f64)
+        gram = torch.zeros((k + 1, k + 1), **f64)
+        _lib.check(L.mjrl_linear_baseline_gram(_lib.ptr(batch.obs), _lib.ptr(y), T, n, _lib.ptr(batch.path_off), P,
+                                               _lib.ptr(scratch), _lib.ptr(gram), st), "mjrl_linear_baseline_gram")
+        self.comm.allreduce_sum(gram)
+
+        def sse(coeffs):
+            r = torch.empty(max(T, 1), **f64)
+            c = torch.from_numpy(np.ascontiguousarray(coeffs, dtype=np.float64)).to(self.device)
+            _lib.check(L.mjrl_linear_baseline_residual(_lib.ptr(batch.obs), _lib.ptr(y), T, n,
+                                                       _lib.ptr(batch.path_off), P, _lib.ptr(c), _lib.ptr(scratch),
+                                                       _lib.ptr(r), st), "mjrl_linear_baseline_residual")
+            out = torch.zeros(8, **f64)
+            part = torch.empty(4 * 256, **f64)
+            _lib.check(L.mjrl_moments(_lib.ptr(r), T, None, _lib.ptr(part), _lib.ptr(out), st), "mjrl_moments")
+            self.comm.allreduce_sum(out)
+            return float(out[1].item())
+
+        G = gram.cpu().numpy()
+        FtF, Fty, yy = G[:k, :k], G[:k, k], G[k, k]
+        if return_errors:
+            err_before = (sse(baseline._coeffs) if baseline._coeffs is not None else yy) / yy
+        reg = baseline._reg_coeff
+        for _ in range(10):   # linear_baseline.py:31-38
+            c = np.linalg.lstsq(FtF + reg * np.identity(k), Fty, rcond=None)[0]
+            baseline._coeffs = c
+            if not np.any(np.isnan(c)):
+                break
+            reg *= 10
+        if return_errors:
+            return err_before, sse(baseline._coeffs) / yy
+
     def _hvp_draws(self, frac, N, T_local, K):
         """K row draws np.random.choice(N, int(frac N)) (npg_cg.py:58-62) made on
         rank 0, broadcast, and cut to this rank's rows (global index - row offset,

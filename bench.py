@@ -202,6 +202,8 @@ def main():
     ap.add_argument("--cpu-rows", type=int, default=200000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end-from-host-paths measurement")
+    ap.add_argument("--precision", default=None, choices=["auto", "split", "f32"],
+                    help="first-layer MFMA form (UpdateEngine precision; default: split where supported)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -223,7 +225,7 @@ def main():
     batch = stage_shard(p0, p1, device, base)
     T_total = args.paths * HORIZON
 
-    eng = UpdateEngine(N_OBS, N_ACT, HIDDEN, device=device, comm=comm)
+    eng = UpdateEngine(N_OBS, N_ACT, HIDDEN, device=device, comm=comm, precision=args.precision)
     rs = np.random.RandomState(0)
     theta = np.concatenate([(rs.randn(int(np.prod(s))) * 0.05).ravel()
                             for s in [(HIDDEN[0], N_OBS), (HIDDEN[0],), (HIDDEN[1], HIDDEN[0]), (HIDDEN[1],),

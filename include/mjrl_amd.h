@@ -61,6 +61,12 @@ typedef struct mjrl_rows {
     float* gu0;               /* [T][h0] per-row upstream gradient at layer 0 */
     float* gu1;               /* [T][h1] per-row upstream gradient at layer 1 */
     float* gp;                /* [T][mp] per-row upstream gradient at the output */
+    /* Split-f16 observation rows (alternative to xhat, MLP(64,64) with np % 128 == 0,
+     * see mjrl_split_supported): row t = [hi np][lo np] f16 of y = xhat[t] / xu[t],
+     * hi = f16(y), lo = f16(y - hi); xu[t] a power of two with |y| < 1.
+     * When xs is non-null the policy passes read xs / xu and ignore xhat. */
+    const void* xs;           /* [T][2][np] f16 */
+    const float* xu;          /* [T] */
 } mjrl_rows;
 
 /* Scratch the caller allocates once per (shape, T) — sizes from
@@ -87,6 +93,16 @@ int mjrl_pack_batch(const double* obs, const double* act, int64_t T, const mjrl_
                     const float* in_shift, const float* in_scale, float* xhat, float* act32,
                     void* stream);
 
+/* Same batch assembly into the split-f16 form of mjrl_rows.xs / xu (one wave per
+ * row: the row's max |xhat| picks xu[t] = 2^E, then hi / lo as described there).
+ * Only for shapes with mjrl_split_supported(s). */
+int mjrl_pack_batch_split(const double* obs, const double* act, int64_t T, const mjrl_shape* s,
+                          const float* in_shift, const float* in_scale, void* xs, float* xu,
+                          float* act32, void* stream);
+/* 1 if the policy passes for this shape accept split-f16 rows (mjrl_rows.xs): the
+ * K = np first layer then runs as three f16 MFMAs per product (hi*hi + hi*lo +
+ * lo*hi, f32 accumulate), the rest of the network in exact f32. */
+int mjrl_split_supported(const mjrl_shape* s);
 /* ---- returns / GAE (process_samples.py:3-44) ----
  * One lane per path, reverse recurrence in fp64, multiply-then-add (no FMA),
  * bit-identical to discount_sum.  use_gae = 0 selects returns - baseline

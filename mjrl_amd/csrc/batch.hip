@@ -43,6 +43,63 @@ __global__ void __launch_bounds__(256) k_pack_batch(const double* __restrict__ o
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < na; i += stride) act32[i] = (float)act[i];
 }
 
+// obs f64 [T][n] -> split-f16 rows (mjrl_rows.xs / xu): one wave per row, lane l
+// owns columns l, l + 64, ... (np <= 512), so every load (8 B per lane) and every
+// hi / lo store (2 B per lane) is one contiguous wave-wide segment.  The row's
+// max |xhat| (>= 1: the bias column) gives xu = 2^E with |xhat / xu| < 1; then
+// hi = f16(y), lo = f16(y - hi) (split8, common.h).  The xhat values are those of
+// k_pack_batch.
+constexpr int PS_MAXC = 8;   // columns per lane (np <= 512)
+__global__ void __launch_bounds__(256) k_pack_split(const double* __restrict__ obs, const double* __restrict__ act,
+                                                    int64_t T, int n, int m, int np,
+                                                    const float* __restrict__ in_shift,
+                                                    const float* __restrict__ in_scale, _Float16* __restrict__ xs,
+                                                    float* __restrict__ xu, float* __restrict__ act32) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const int nc = (np + 63) / 64;
+    for (int64_t row = wid; row < T; row += nw) {
+        const double* src = obs + row * n;
+        float v[PS_MAXC];
+        float mx = 0.f;
+#pragma unroll
+        for (int j = 0; j < PS_MAXC; ++j) {
+            const int c = lane + 64 * j;
+            float x = 0.f;
+            if (j < nc) {
+                if (c < n) {
+                    x = (float)src[c];                        // torch .float(): round to nearest
+                    if (in_shift) x = (x - in_shift[c]) / (in_scale[c] + 1e-8f);   // MuNet.forward:177
+                } else if (c == n) {
+                    x = 1.0f;                                 // bias column (zero padding after)
+                }
+            }
+            v[j] = x;
+            mx = fmaxf(mx, fabsf(x));
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+        float inv;
+        const float s = pow2_scale(mx, inv);
+        _Float16* dst = xs + row * (2 * (int64_t)np);
+#pragma unroll
+        for (int j = 0; j < PS_MAXC; ++j) {
+            const int c = lane + 64 * j;
+            if (j < nc && c < np) {
+                const float y = v[j] * s;
+                const _Float16 h = (_Float16)y;
+                dst[c] = h;
+                dst[np + c] = (_Float16)(y - (float)h);
+            }
+        }
+        if (lane == 0) xu[row] = inv;
+    }
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t na = (int64_t)T * m;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < na; i += stride) act32[i] = (float)act[i];
+}
+
 // One wave per path.  The path's rewards and baselines come into LDS with
 // coalesced loads, in windows of GW steps; lane 0 runs the serial fp64 chains out
 // of LDS (separate multiply and add, __dmul_rn / __dadd_rn cannot be contracted:
@@ -350,6 +407,19 @@ int mjrl_pack_batch(const double* obs, const double* act, int64_t T, const mjrl_
     const int g = grid_for(T * (s->np / 4), 256, 2048);
     hipLaunchKernelGGL(k_pack_batch, dim3(g), dim3(256), 0, (hipStream_t)stream, obs, act, T, s->n, s->m, s->np,
                        in_shift, in_scale, xhat, act32);
+    return err(hipGetLastError());
+}
+
+int mjrl_pack_batch_split(const double* obs, const double* act, int64_t T, const mjrl_shape* s,
+                          const float* in_shift, const float* in_scale, void* xs, float* xu, float* act32,
+                          void* stream) {
+    if (!s || T < 0 || (T > 0 && (!obs || !act || !xs || !xu || !act32))) return MJRL_EINVAL;
+    if ((in_shift == nullptr) != (in_scale == nullptr)) return MJRL_EINVAL;
+    if (s->np > 64 * PS_MAXC) return MJRL_ESHAPE;
+    if (T == 0) return MJRL_OK;
+    const int g = grid_for(T, 4, 8192);
+    hipLaunchKernelGGL(k_pack_split, dim3(g), dim3(256), 0, (hipStream_t)stream, obs, act, T, s->n, s->m, s->np,
+                       in_shift, in_scale, (_Float16*)xs, xu, act32);
     return err(hipGetLastError());
 }
 

@@ -35,6 +35,83 @@ __device__ __forceinline__ floatx4 mfma_k16(const float4& a, const float4& b, fl
 }
 
 // ---------------------------------------------------------------------------
+// Split-f16 operands ("fp16x3"): an f32 value y of a block scaled by a power of
+// two so max |y| < 1 is carried as hi = f16(y) and lo = f16(y - hi) (round to
+// nearest; y - hi is exact).  A product of two split operands is hi*hi + hi*lo +
+// lo*hi, three v_mfma_f32_16x16x32_f16 into ONE f32 accumulator (f16 products are
+// exact), dropping only lo*lo.  Error of one operand: <= 2^-24 |y| while lo is
+// normal (|y| >= 2^-2), and <= 2^-25 of the block max below that (lo is then an
+// f16 subnormal): 24-bit block floating point, the f32 mantissa width.  Three f16
+// MFMAs carry 8x the k of one v_mfma_f32_16x16x4_f32 in half its cycles: 5.3x
+// the f32 matrix rate.
+// ---------------------------------------------------------------------------
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef short short4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ floatx4 mfma_h(const half8& a, const half8& b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+// c += (ah + al)(bh + bl) - al bl
+__device__ __forceinline__ floatx4 mfma_x3(const half8& ah, const half8& al, const half8& bh, const half8& bl,
+                                           floatx4 c) {
+    c = mfma_h(ah, bh, c);
+    c = mfma_h(ah, bl, c);
+    return mfma_h(al, bh, c);
+}
+
+// Power-of-two scale for a block whose max |value| is M: returns s = 2^-E with
+// M * s in [0.5, 1) and sets inv = 2^E (s = inv = 1 for M == 0 / non-finite).
+__device__ __forceinline__ float pow2_scale(float M, float& inv) {
+    if (!(M > 0.f) || !(M < 3.0e38f)) {
+        inv = 1.f;
+        return 1.f;
+    }
+    int E;
+    frexpf(M, &E);
+    E = E < -120 ? -120 : E;
+    inv = ldexpf(1.f, E);
+    return ldexpf(1.f, -E);
+}
+
+typedef float float8v __attribute__((ext_vector_type(8)));
+typedef short short8v __attribute__((ext_vector_type(8)));
+
+// hi / lo of y = v * s (vector form: packed v_cvt_pk_f16_f32, round to nearest)
+__device__ __forceinline__ void split8(const float8v& v, float s, half8& hi, half8& lo) {
+    const float8v y = v * s;
+    hi = __builtin_convertvector(y, half8);
+    lo = __builtin_convertvector(y - __builtin_convertvector(hi, float8v), half8);
+}
+
+__device__ __forceinline__ float8v load8(const float* p) {
+    const float4 a = *reinterpret_cast<const float4*>(p);
+    const float4 b = *reinterpret_cast<const float4*>(p + 4);
+    return float8v{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+}
+
+__device__ __forceinline__ float absmax8(const float8v& v) {
+    float m = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(v[e]));
+    return m;
+}
+
+// max over the four 16-lane groups (lanes l, l^16, l^32, l^48)
+__device__ __forceinline__ float max_over_groups(float v) {
+    v = fmaxf(v, __shfl_xor(v, 16, 64));
+    return fmaxf(v, __shfl_xor(v, 32, 64));
+}
+
+// gfx950 ds_read_b64_tr_b16: per 16-lane group, lane 4r+p addresses row r,
+// columns 4p..4p+3 of a 4 x 16 block of 16-bit values; lane i receives column i
+// (row r in element r).  EXEC must be all ones.
+__device__ __forceinline__ short4v ds_read_tr16(const void* p) {
+    typedef __attribute__((address_space(3))) short4v lds_short4;
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(p));
+}
+
+// ---------------------------------------------------------------------------
 // Wave decomposition of an output tile [BT x N] (BT = 16*RB rows, N = 16*CB cols)
 // over the 4 waves of a workgroup: each wave owns NRW row blocks x NCW col blocks
 // and loads one B (weight) fragment per col block per k-step, reused across its

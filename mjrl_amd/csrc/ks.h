@@ -1,34 +1,49 @@
-// ks.h — persistent fused FWD / FVP kernel for the MLP(64,64) policy with a
+// ks.h — persistent fused FWD / FVP / EVAL kernel for the MLP(64,64) policy with a
 // wide observation (NP = 32*KG, up to 384: Humanoid), included by policy.hip.
 //
 // One 512-thread workgroup (8 waves) per CU walks 32-row tiles of timesteps with
-// NO global load inside the tile loop except the next tile's xhat prefetch (and,
-// for FVP, the cached activations):
+// NO global load inside the tile loop except the tile's xhat (and, for FVP, the
+// cached activations):
 //   - wave w owns hidden block cb = w&3 and observation half kh = w>>2: its slice of
-//     W0 (FWD) or of the tangent dW0 (FVP) — 16 x NP/2 floats — lives in
+//     W0 (FWD / EVAL) or of the tangent dW0 (FVP) — 16 x NP/2 — lives in
 //     REGISTERS as MFMA B fragments for the whole launch, and so does its slice of
 //     the gW0 accumulator;
 //   - W1 / dW1 / W2 / dW2 live in LDS for the whole launch;
 //   - the 32-row xhat tile sits in LDS for both the first-layer GEMM and the gW0
-//     update; the next tile is prefetched into registers meanwhile.
+//     update; the next tile's lines are pulled into L2 meanwhile.
 // Phase 1 computes per-half partial sums, folded through LDS; phases 2-5 are the
 // row chain of k_rows; gW1 / gW2 / biases accumulate in registers too.  Slabs
 // are written at the end in k_gather's layout.
+//
+// SX = true: the two K = NP products of the first layer (xhat W0^T and the gW0
+// update) run as split-f16 ("fp16x3", common.h) on v_mfma_f32_16x16x32_f16:
+//   - xhat arrives pre-split from mjrl_pack_batch_split: per row [hi NP][lo NP]
+//     f16 of y = xhat / u_r, u_r a power of two (row scale xu[r]);
+//   - the W0 / dW0 slice is scaled per hidden unit and split once per launch;
+//   - gW0's left operand (gu0 * u_r) is scaled per (tile, hidden unit) and split
+//     per tile; its right operand is read from the xhat image with the gfx950
+//     transposing LDS read (ds_read_b64_tr_b16).
+// The LDS images of xhat hi / lo use 16-byte chunks XOR-swizzled by row so both
+// the row reads (phase 1) and the transposed reads (gW0) are bank-conflict free.
+// The 64-wide layers stay on exact-f32 MFMA.
 #pragma once
 
 namespace {
 
 constexpr int KT = 512;
 
-template <int MP, int KG>
+template <int MP, int KG, bool SX>
 struct KLayout {
     static constexpr int H = 64, BT = 32, RB = 2;
     static constexpr int NP = 32 * KG, KH = NP / 2;
     static constexpr int LDX = NP + 16;   // rows 4 apart fall 16 banks apart for the b32 gW0 reads
     static constexpr int LD = H + 4, LDP = MP + 4;
+    static constexpr int LDG = BT + 4;    // SX: gu0 tile stored transposed, [H][LDG]
+    static constexpr int RBYTES = NP * 2; // SX: bytes of one f16 row of the hi / lo image
     static_assert(KT == BT * H / 4, "tanh_tile: one float4 per thread");
+    static constexpr int XFLOATS = SX ? 2 * BT * RBYTES / 4 : BT * LDX;
     static constexpr int oXT = 0;
-    static constexpr int oD0 = oXT + BT * LDX;
+    static constexpr int oD0 = oXT + XFLOATS;
     static constexpr int oA0 = oD0 + BT * LD;
     static constexpr int oD1 = oA0 + BT * LD;
     static constexpr int oA1 = oD1 + BT * LD;
@@ -37,12 +52,20 @@ struct KLayout {
     static constexpr int odW1 = oW1 + H * LD;      // [64][LD]  dW1 (FVP)
     static constexpr int oW2 = odW1 + H * LD;      // [MP][LD]  W2p
     static constexpr int odW2 = oW2 + MP * LD;     // [MP][LD]  dW2p (FVP)
-    static constexpr int total = odW2 + MP * LD;
+    static constexpr int oG0T = odW2 + MP * LD;    // SX: [H][LDG] gu0 * u_r, transposed
+    static constexpr int oU = oG0T + (SX ? H * LDG : 0);   // SX: [BT] row scales
+    static constexpr int total = oU + (SX ? BT : 0);
     static constexpr int bytes = total * 4;
     static_assert(bytes <= 160 * 1024, "LDS");
-    static constexpr int XPER = BT * NP / 4 / KT;  // float4 of the xhat tile per thread
+    static constexpr int XPER = BT * NP / 4 / KT;  // 16-byte pieces of the xhat tile per thread
     static_assert(XPER * KT * 4 == BT * NP, "NP must be a multiple of 64");
+    static_assert(!SX || NP % 128 == 0, "SX: the chunk swizzle needs NP % 128 == 0");
 };
+
+// XOR swizzle of the 16-byte chunks of row `row` in the SX xhat images:
+// ds_read_b128 of 16 consecutive rows and ds_read_b64_tr_b16 of rows
+// {r0..r0+3, r0+8..r0+11} both touch 64 distinct banks.
+__device__ __forceinline__ int chunk_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
 
 // acc += A[rows][k] (LDS, row-major) x B where B(k, n) = Bs[n][k] (LDS, row-major by n)
 template <int NR>
@@ -80,8 +103,8 @@ __device__ __forceinline__ void mm_lds_kn(floatx4 (&acc)[NR], const float* As, i
     }
 }
 
-// FWD activation of one [32][64] tile: A = tanh(U) in LDS and the a0 / a1 cache
-// rows in HBM, one float4 per thread (row-contiguous, coalesced stores).
+// Activation of one [32][64] tile: A = tanh(U) in LDS and (FWD) the a0 / a1
+// cache rows in HBM, one float4 per thread (row-contiguous, coalesced stores).
 __device__ __forceinline__ void tanh_tile(const float* U, float* A, float* cache, int64_t row_base, int64_t T,
                                           int tid) {
     constexpr int LD = 68;
@@ -90,16 +113,18 @@ __device__ __forceinline__ void tanh_tile(const float* U, float* A, float* cache
     const float4 v = make_float4(tanhf(u.x), tanhf(u.y), tanhf(u.z), tanhf(u.w));
     *reinterpret_cast<float4*>(A + row * LD + c) = v;
     const int64_t gr = row_base + row;
-    if (gr < T) *reinterpret_cast<float4*>(cache + gr * 64 + c) = v;
+    if (cache && gr < T) *reinterpret_cast<float4*>(cache + gr * 64 + c) = v;
 }
 
-template <int MP, int KG, int MODE>
+template <int MP, int KG, int MODE, bool SX>
 __global__ void __launch_bounds__(KT, 1) k_ks(RowArgs a, FOut o) {
-    static_assert(MODE == FWD || MODE == FVP, "k_ks runs the gradient modes");
-    using L = KLayout<MP, KG>;
+    using L = KLayout<MP, KG, SX>;
     constexpr int H = 64, BT = L::BT, NP = L::NP, KH = L::KH;
+    constexpr bool GRAD = MODE != EVAL;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float* XT = smem + L::oXT;
+    char* XHb = reinterpret_cast<char*>(smem + L::oXT);   // SX: hi image, then lo image
+    char* XLb = XHb + BT * L::RBYTES;
     float* D0 = smem + L::oD0;
     float* A0s = smem + L::oA0;
     float* D1 = smem + L::oD1;
@@ -109,6 +134,8 @@ __global__ void __launch_bounds__(KT, 1) k_ks(RowArgs a, FOut o) {
     float* sdW1 = smem + L::odW1;
     float* sW2 = smem + L::oW2;
     float* sdW2 = smem + L::odW2;
+    float* G0T = smem + L::oG0T;
+    float* Us = smem + L::oU;
 
     if (MODE == FVP && a.done && *a.done) return;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -132,10 +159,26 @@ __global__ void __launch_bounds__(KT, 1) k_ks(RowArgs a, FOut o) {
         sW2[row * L::LD + col] = P[pk.W2 + i];
         if (MODE == FVP) sdW2[row * L::LD + col] = a.V[pk.W2 + i];
     }
-    float4 wb[KG];   // B fragments: W0[cb*16 + r][kh*KH + 16g + 4q .. +3]
+    constexpr int KS = SX ? KH / 32 : 1;   // SX: k32 steps per observation half
+    float4 wb[SX ? 1 : KG];   // f32: B fragments W0[cb*16 + r][kh*KH + 16g + 4q .. +3]
+    half8 wh[KS], wl[KS];     // SX: split B fragments W0[cb*16 + r][kh*KH + 32s + 8q .. +7]
+    float wsc = 1.f;          // SX: 2^E of this lane's hidden unit (undoes the split scale)
+    if constexpr (SX) {
+        float8v v[KS];
+        float mx = 0.f;
 #pragma unroll
-    for (int g = 0; g < KG; ++g)
-        wb[g] = *reinterpret_cast<const float4*>(W0src + (cb * 16 + r16) * NP + kh * KH + 16 * g + 4 * q);
+        for (int s = 0; s < KS; ++s) {
+            v[s] = load8(W0src + (cb * 16 + r16) * NP + kh * KH + 32 * s + 8 * q);
+            mx = fmaxf(mx, absmax8(v[s]));
+        }
+        const float sc = pow2_scale(max_over_groups(mx), wsc);
+#pragma unroll
+        for (int s = 0; s < KS; ++s) split8(v[s], sc, wh[s], wl[s]);
+    } else {
+#pragma unroll
+        for (int g = 0; g < KG; ++g)
+            wb[g] = *reinterpret_cast<const float4*>(W0src + (cb * 16 + r16) * NP + kh * KH + 16 * g + 4 * q);
+    }
 
     // accumulators (FWD / FVP)
     floatx4 g0[KG];   // gW0[cb*16 ..][kh*KH + 16g ..]
@@ -146,8 +189,8 @@ __global__ void __launch_bounds__(KT, 1) k_ks(RowArgs a, FOut o) {
     g1[1] = zero4();
     floatx4 g2 = zero4();   // gW2 tile (nb = w>>2 < MP/16, kb = w&3)
     float b1acc = 0.f, b2acc = 0.f;
-    double racc0 = 0.0, racc1 = 0.0;   // row-pass partials (FWD), folded at the end
-    const float sls = MODE == FWD ? ls_sum(P + pk.ls, m) : 0.f;
+    double racc0 = 0.0, racc1 = 0.0;   // row-pass partials (FWD / EVAL), folded at the end
+    const float sls = MODE == FVP ? 0.f : ls_sum(P + pk.ls, m);
 
     // tile-invariant per-lane constants of the epilogues
     const float bias1 = (MODE == FVP ? a.V : P)[pk.b1 + cb * 16 + r16];
@@ -163,44 +206,72 @@ __global__ void __launch_bounds__(KT, 1) k_ks(RowArgs a, FOut o) {
     }
 
     float touch = 0.f;
-    float4 xr[L::XPER];
-    auto xload = [&](int64_t tile) {
-#pragma unroll
-        for (int u = 0; u < L::XPER; ++u) {
-            const int idx = tid + u * KT;
-            const int row = idx / (NP / 4), c4 = idx % (NP / 4);
-            const int64_t gr = tile * BT + row;
-            xr[u] = gr < T ? *reinterpret_cast<const float4*>(a.xhat + gr * NP + c4 * 4)
-                           : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-    };
     __syncthreads();   // weights in LDS
 
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        // Per-lane indices through a zero the compiler cannot see through: every
+        // lane-dependent address of the tile body is recomputed per tile (a few VALU)
+        // instead of being hoisted out of the loop into live registers (it spilled).
+        int opq = 0;
+        asm volatile("" : "+v"(opq));
+        const int ltid = tid + opq, llane = lane + opq, lr16 = r16 + opq, lq = q + opq;
         const int64_t row_base = tile * BT;
+        const int nrow = (int)(T - row_base < BT ? T - row_base : BT);   // valid rows of this tile
         // ---- publish this tile's xhat (L2-warm from the previous tile's touch) ----
         asm volatile("" ::"v"(touch));
-        xload(tile);
+        if constexpr (SX) {
+            // 16 threads per row (row = ltid / 16), piece c = ltid % 16 + 16 u of the row's
+            // NP/4 16-byte pieces: pieces u < NP/128 are hi chunks, the rest lo chunks;
+            // every address is a per-thread base plus an immediate
+            const char* src = reinterpret_cast<const char*>(a.xs);
+            const int row = ltid >> 4, c16 = ltid & 15;
+            const int64_t gr = row_base + row;
+            float4 xr[L::XPER];
 #pragma unroll
-        for (int u = 0; u < L::XPER; ++u) {
-            const int idx = tid + u * KT;
-            const int row = idx / (NP / 4), c4 = idx % (NP / 4);
-            *reinterpret_cast<float4*>(XT + row * L::LDX + c4 * 4) = xr[u];
+            for (int u = 0; u < L::XPER; ++u)
+                xr[u] = gr < T ? *reinterpret_cast<const float4*>(src + gr * (4 * NP) + 16 * (c16 + 16 * u))
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
+            char* dst = XHb + row * L::RBYTES + 16 * (c16 ^ chunk_swz(row));
+#pragma unroll
+            for (int u = 0; u < L::XPER; ++u) {
+                constexpr int UH = NP / 128;   // pieces per thread in each of hi / lo
+                *reinterpret_cast<float4*>(dst + (u / UH) * (BT * L::RBYTES) + 256 * (u % UH)) = xr[u];
+            }
+            if (ltid < BT) {
+                const int64_t gu = row_base + ltid;
+                Us[ltid] = gu < T ? a.xu[gu] : 1.f;
+            }
+        } else {
+            float4 xr[L::XPER];
+#pragma unroll
+            for (int u = 0; u < L::XPER; ++u) {
+                const int idx = ltid + u * KT;
+                const int row = idx / (NP / 4), c4 = idx % (NP / 4);
+                const int64_t gr = row_base + row;
+                xr[u] = gr < T ? *reinterpret_cast<const float4*>(a.xhat + gr * NP + c4 * 4)
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int u = 0; u < L::XPER; ++u) {
+                const int idx = ltid + u * KT;
+                const int row = idx / (NP / 4), c4 = idx % (NP / 4);
+                *reinterpret_cast<float4*>(XT + row * L::LDX + c4 * 4) = xr[u];
+            }
         }
-        // FVP: cached activations for this lane's epilogue-1 / -2 elements
+        // FVP: cached activations for this llane's epilogue-1 / -2 elements
         float pa0[2][4], pa1[4];
         if (MODE == FVP) {
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) {
-                    const int64_t gr = row_base + i * 16 + 4 * q + rr;
-                    pa0[i][rr] = (kh == 0 && gr < T) ? a.a0[gr * H + cb * 16 + r16] : 0.f;
+                    const int64_t gr = row_base + i * 16 + 4 * lq + rr;
+                    pa0[i][rr] = (kh == 0 && gr < T) ? a.a0[gr * H + cb * 16 + lr16] : 0.f;
                 }
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr) {
-                const int64_t gr = row_base + kh * 16 + 4 * q + rr;
-                pa1[rr] = gr < T ? a.a1[gr * H + cb * 16 + r16] : 0.f;
+                const int64_t gr = row_base + kh * 16 + 4 * lq + rr;
+                pa1[rr] = gr < T ? a.a1[gr * H + cb * 16 + lr16] : 0.f;
             }
         }
         __syncthreads();
@@ -208,31 +279,57 @@ __global__ void __launch_bounds__(KT, 1) k_ks(RowArgs a, FOut o) {
         // value is only kept alive until the next publish, 1 VGPR)
         {
             const int64_t nt = tile + gridDim.x;
-            constexpr int LPR = NP * 4 / 128;   // lines per row
-            if (nt < ntiles && tid < BT * LPR) {
-                const int64_t gr = nt * BT + tid / LPR;
-                if (gr < T) touch = a.xhat[gr * NP + (tid % LPR) * 32];
+            constexpr int LPR = (SX ? 4 * NP : 4 * NP) / 128;   // lines per row
+            if (nt < ntiles && ltid < BT * LPR) {
+                const int64_t gr = nt * BT + ltid / LPR;
+                if (gr < T) {
+                    if constexpr (SX)
+                        touch = reinterpret_cast<const float*>(a.xs)[gr * NP + (ltid % LPR) * 32];
+                    else
+                        touch = a.xhat[gr * NP + (ltid % LPR) * 32];
+                }
             }
         }
 
         // ---- phase 1: partial [32 x 16] over this wave's observation half ----
         floatx4 acc1[2] = {zero4(), zero4()};
+        if constexpr (SX) {
+            const int swz1 = chunk_swz(lr16);   // rows 16i + r16: same swizzle for both i
 #pragma unroll
-        for (int g = 0; g < KG; ++g) {
-            const int k = kh * KH + 16 * g + 4 * q;
+            for (int s = 0; s < KS; ++s) {
+                const int ch = kh * (KH / 8) + 4 * s + lq;
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const float4 x = *reinterpret_cast<const float4*>(XT + (i * 16 + r16) * L::LDX + k);
-                acc1[i] = mfma_k16(x, wb[g], acc1[i]);
+                for (int i = 0; i < 2; ++i) {
+                    const int row = i * 16 + lr16;
+                    const int off = row * L::RBYTES + 16 * (ch ^ swz1);
+                    const half8 xh = *reinterpret_cast<const half8*>(XHb + off);
+                    const half8 xl = *reinterpret_cast<const half8*>(XLb + off);
+                    acc1[i] = mfma_x3(xh, xl, wh[s], wl[s], acc1[i]);
+                }
+                if (s & 1) __builtin_amdgcn_sched_barrier(0);
             }
-            if ((g & 3) == 3) __builtin_amdgcn_sched_barrier(0);   // bound the hoisting of LDS reads
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) acc1[i][rr] *= Us[i * 16 + 4 * lq + rr] * wsc;
+        } else {
+#pragma unroll
+            for (int g = 0; g < KG; ++g) {
+                const int k = kh * KH + 16 * g + 4 * lq;
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const float4 x = *reinterpret_cast<const float4*>(XT + (i * 16 + lr16) * L::LDX + k);
+                    acc1[i] = mfma_k16(x, wb[g], acc1[i]);
+                }
+                if ((g & 3) == 3) __builtin_amdgcn_sched_barrier(0);   // bound the hoisting of LDS reads
+            }
         }
         // fold the two halves: kh = 1 publishes, kh = 0 finishes
         if (kh == 1) {
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
-                for (int rr = 0; rr < 4; ++rr) D0[(i * 16 + 4 * q + rr) * L::LD + cb * 16 + r16] = acc1[i][rr];
+                for (int rr = 0; rr < 4; ++rr) D0[(i * 16 + 4 * lq + rr) * L::LD + cb * 16 + lr16] = acc1[i][rr];
         }
         __syncthreads();
         if (kh == 0) {
@@ -240,8 +337,8 @@ __global__ void __launch_bounds__(KT, 1) k_ks(RowArgs a, FOut o) {
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) {
-                    const int row = i * 16 + 4 * q + rr;
-                    const int col = cb * 16 + r16;
+                    const int row = i * 16 + 4 * lq + rr;
+                    const int col = cb * 16 + lr16;
                     const float v = acc1[i][rr] + D0[row * L::LD + col];
                     if (MODE == FVP) {
                         const float av = pa0[i][rr];
@@ -253,8 +350,8 @@ __global__ void __launch_bounds__(KT, 1) k_ks(RowArgs a, FOut o) {
                 }
         }
         __syncthreads();
-        if (MODE == FWD) {
-            tanh_tile(D0, A0s, a.a0, row_base, T, tid);
+        if (MODE != FVP) {
+            tanh_tile(D0, A0s, MODE == FWD ? a.a0 : nullptr, row_base, T, ltid);
             __syncthreads();
         }
 
@@ -262,15 +359,15 @@ __global__ void __launch_bounds__(KT, 1) k_ks(RowArgs a, FOut o) {
         {
             floatx4 acc[1] = {zero4()};
             if (MODE == FVP) {
-                mm_lds_nk(acc, D0, L::LD, kh, 1, sW1, L::LD, cb, H, lane);
-                mm_lds_nk(acc, A0s, L::LD, kh, 1, sdW1, L::LD, cb, H, lane);
+                mm_lds_nk(acc, D0, L::LD, kh, 1, sW1, L::LD, cb, H, llane);
+                mm_lds_nk(acc, A0s, L::LD, kh, 1, sdW1, L::LD, cb, H, llane);
             } else {
-                mm_lds_nk(acc, A0s, L::LD, kh, 1, sW1, L::LD, cb, H, lane);
+                mm_lds_nk(acc, A0s, L::LD, kh, 1, sW1, L::LD, cb, H, llane);
             }
-            const int col = cb * 16 + r16;
+            const int col = cb * 16 + lr16;
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr) {
-                const int row = kh * 16 + 4 * q + rr;
+                const int row = kh * 16 + 4 * lq + rr;
                 const float v = acc[0][rr] + bias1;
                 if (MODE == FVP) {
                     const float av = pa1[rr];
@@ -282,8 +379,8 @@ __global__ void __launch_bounds__(KT, 1) k_ks(RowArgs a, FOut o) {
             }
         }
         __syncthreads();
-        if (MODE == FWD) {
-            tanh_tile(D1, A1s, a.a1, row_base, T, tid);
+        if (MODE != FVP) {
+            tanh_tile(D1, A1s, MODE == FWD ? a.a1 : nullptr, row_base, T, ltid);
             __syncthreads();
         }
 
@@ -291,15 +388,15 @@ __global__ void __launch_bounds__(KT, 1) k_ks(RowArgs a, FOut o) {
         if (w < 2 * (MP / 16)) {
             floatx4 acc[1] = {zero4()};
             if (MODE == FVP) {
-                mm_lds_nk(acc, D1, L::LD, rb3, 1, sW2, L::LD, cbo3, H, lane);
-                mm_lds_nk(acc, A1s, L::LD, rb3, 1, sdW2, L::LD, cbo3, H, lane);
+                mm_lds_nk(acc, D1, L::LD, rb3, 1, sW2, L::LD, cbo3, H, llane);
+                mm_lds_nk(acc, A1s, L::LD, rb3, 1, sdW2, L::LD, cbo3, H, llane);
             } else {
-                mm_lds_nk(acc, A1s, L::LD, rb3, 1, sW2, L::LD, cbo3, H, lane);
+                mm_lds_nk(acc, A1s, L::LD, rb3, 1, sW2, L::LD, cbo3, H, llane);
             }
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr) {
-                const int row = rb3 * 16 + 4 * q + rr;
-                const bool valid = row_base + row < T;
+                const int row = rb3 * 16 + 4 * lq + rr;
+                const bool valid = row < nrow;
                 const float v = acc[0][rr] + bias3;
                 if (MODE == FVP)
                     GPs[row * L::LDP + col3] = (col3 < m && valid) ? wq3 * v : 0.f;
@@ -309,63 +406,111 @@ __global__ void __launch_bounds__(KT, 1) k_ks(RowArgs a, FOut o) {
         }
         __syncthreads();
 
-        // ---- per-row pass (FWD: log-lik, caches, VPG upstream) ----
-        if (MODE == FWD) {
-            row_pass<MODE, BT, MP, KT, false>(a, P + pk.ls, sls, row_base, GPs, L::LDP, racc0, racc1, tid);
+        // ---- per-row pass (FWD: log-lik, caches, VPG upstream; EVAL: LR, KL) ----
+        if (MODE != FVP) {
+            row_pass<MODE, BT, MP, KT, false>(a, P + pk.ls, sls, row_base, GPs, L::LDP, racc0, racc1, ltid);
             __syncthreads();
         }
+        if (MODE == EVAL) continue;   // forward only
 
         {
             // ---- phase 4: gu1 = (1 - a1^2) (g W2); wave -> (rb = kh, cb) ----
             {
                 floatx4 acc[1] = {zero4()};
-                mm_lds_kn(acc, GPs, L::LDP, kh, 1, sW2, L::LD, cb, MP, lane);
-                const int col = cb * 16 + r16;
+                mm_lds_kn(acc, GPs, L::LDP, kh, 1, sW2, L::LD, cb, MP, llane);
+                const int col = cb * 16 + lr16;
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) {
-                    const int row = kh * 16 + 4 * q + rr;
+                    const int row = kh * 16 + 4 * lq + rr;
                     const float av = A1s[row * L::LD + col];
-                    D1[row * L::LD + col] = row_base + row < T ? (1.f - av * av) * acc[0][rr] : 0.f;
+                    D1[row * L::LD + col] = row < nrow ? (1.f - av * av) * acc[0][rr] : 0.f;
                 }
             }
             __syncthreads();
             // ---- phase 5: gu0 = (1 - a0^2) (gu1 W1) ----
             {
                 floatx4 acc[1] = {zero4()};
-                mm_lds_kn(acc, D1, L::LD, kh, 1, sW1, L::LD, cb, H, lane);
-                const int col = cb * 16 + r16;
+                mm_lds_kn(acc, D1, L::LD, kh, 1, sW1, L::LD, cb, H, llane);
+                const int col = cb * 16 + lr16;
+                float g[4];
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) {
-                    const int row = kh * 16 + 4 * q + rr;
+                    const int row = kh * 16 + 4 * lq + rr;
                     const float av = A0s[row * L::LD + col];
-                    D0[row * L::LD + col] = row_base + row < T ? (1.f - av * av) * acc[0][rr] : 0.f;
+                    g[rr] = row < nrow ? (1.f - av * av) * acc[0][rr] : 0.f;
+                }
+                if constexpr (SX) {
+                    // transposed, times the row scale: gW0 = sum_r (gu0_r u_r) (hi_r + lo_r 2^-12)
+                    const int r0 = kh * 16 + 4 * lq;
+                    *reinterpret_cast<float4*>(G0T + col * L::LDG + r0) =
+                        make_float4(g[0] * Us[r0], g[1] * Us[r0 + 1], g[2] * Us[r0 + 2], g[3] * Us[r0 + 3]);
+                } else {
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) D0[(kh * 16 + 4 * lq + rr) * L::LD + col] = g[rr];
                 }
             }
             __syncthreads();
             // ---- weight gradients (registers) ----
-#pragma unroll 1
-            for (int t = 0; t < BT; t += 4) {
-                const float gu = D0[(t + q) * L::LD + cb * 16 + r16];
+            if constexpr (SX) {
+                // left operand: gu0 rows 8q..8q+7 of hidden unit cb*16 + lr16, split per (tile, unit)
+                half8 gh, gl;
+                float sc4[4];
+                {
+                    const float8v v = load8(G0T + (cb * 16 + lr16) * L::LDG + 8 * lq);
+                    float inv;
+                    const float s = pow2_scale(max_over_groups(absmax8(v)), inv);
+                    split8(v, s, gh, gl);
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) sc4[rr] = __shfl(inv, 4 * lq + rr, 64);
+                }
+                // right operand: xhat rows 8q..8q+7 of columns kh*KH + 16g + lr16 (transposed reads)
+                const int tq = lr16 >> 2, tp = lr16 & 3;
+                const int cl = (kh * KH) / 8 + (tp >> 1);
 #pragma unroll
                 for (int g = 0; g < KG; ++g) {
-                    g0[g] = mfma4(gu, XT[(t + q) * L::LDX + kh * KH + 16 * g + r16], g0[g]);
-                    if ((g & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+                    const int c0 = cl + 2 * g;
+                    short4v th[2], tl[2];
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int row = 8 * lq + 4 * h + tq;
+                        const int off = row * L::RBYTES + 16 * (c0 ^ chunk_swz(row)) + 8 * (tp & 1);
+                        th[h] = ds_read_tr16(XHb + off);
+                        tl[h] = ds_read_tr16(XLb + off);
+                    }
+                    const half8 bh = __builtin_bit_cast(half8, __builtin_shufflevector(th[0], th[1], 0, 1, 2, 3, 4, 5, 6, 7));
+                    const half8 bl = __builtin_bit_cast(half8, __builtin_shufflevector(tl[0], tl[1], 0, 1, 2, 3, 4, 5, 6, 7));
+                    const floatx4 t = mfma_x3(gh, gl, bh, bl, zero4());
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) g0[g][rr] += t[rr] * sc4[rr];
+                    if (g & 1) __builtin_amdgcn_sched_barrier(0);   // bound the hoisting of the operand reads
                 }
-                const float gu1 = D1[(t + q) * L::LD + cb * 16 + r16];
+            }
+            constexpr int WUNR = SX ? BT / 4 : 1;   // SX: only the 64-wide sums remain, unroll fully
+#pragma unroll WUNR
+            for (int t = 0; t < BT; t += 4) {
+                if constexpr (!SX) {
+                    const float gu = D0[(t + lq) * L::LD + cb * 16 + lr16];
+#pragma unroll
+                    for (int g = 0; g < KG; ++g) {
+                        g0[g] = mfma4(gu, XT[(t + lq) * L::LDX + kh * KH + 16 * g + lr16], g0[g]);
+                        if ((g & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+                    }
+                }
+                const float gu1 = D1[(t + lq) * L::LD + cb * 16 + lr16];
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
-                    g1[j] = mfma4(gu1, A0s[(t + q) * L::LD + (kh + 2 * j) * 16 + r16], g1[j]);
+                    g1[j] = mfma4(gu1, A0s[(t + lq) * L::LD + (kh + 2 * j) * 16 + lr16], g1[j]);
                 if ((w >> 2) < MP / 16)
-                    g2 = mfma4(GPs[(t + q) * L::LDP + (w >> 2) * 16 + r16], A1s[(t + q) * L::LD + (w & 3) * 16 + r16],
+                    g2 = mfma4(GPs[(t + lq) * L::LDP + (w >> 2) * 16 + lr16], A1s[(t + lq) * L::LD + (w & 3) * 16 + lr16],
                                g2);
             }
-            if (tid < H) {
+            if (ltid < H) {
                 float s = 0.f;
-                for (int row = 0; row < BT; ++row) s += D1[row * L::LD + tid];
+                for (int row = 0; row < BT; ++row) s += D1[row * L::LD + ltid];
                 b1acc += s;
-            } else if (tid < H + MP) {
+            } else if (ltid < H + MP) {
                 float s = 0.f;
-                for (int row = 0; row < BT; ++row) s += GPs[row * L::LDP + tid - H];
+                for (int row = 0; row < BT; ++row) s += GPs[row * L::LDP + ltid - H];
                 b2acc += s;
             }
         }
@@ -373,35 +518,37 @@ __global__ void __launch_bounds__(KT, 1) k_ks(RowArgs a, FOut o) {
     }
 
     const int64_t blk = blockIdx.x;
+    if constexpr (GRAD) {
 #pragma unroll
-    for (int g = 0; g < KG; ++g)
+        for (int g = 0; g < KG; ++g)
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-            const int n = cb * 16 + 4 * q + rr;
-            const int k = kh * KH + 16 * g + r16;
-            o.wpart[o.off0 + (blk * H + n) * NP + k] = g0[g][rr];
+            for (int rr = 0; rr < 4; ++rr) {
+                const int n = cb * 16 + 4 * q + rr;
+                const int k = kh * KH + 16 * g + r16;
+                o.wpart[o.off0 + (blk * H + n) * NP + k] = g0[g][rr];
+            }
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int n = cb * 16 + 4 * q + rr;
+                const int k = (kh + 2 * j) * 16 + r16;
+                o.wpart[o.off1 + (blk * H + n) * H + k] = g1[j][rr];
+            }
+        if ((w >> 2) < MP / 16) {
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int n = (w >> 2) * 16 + 4 * q + rr;
+                const int k = (w & 3) * 16 + r16;
+                o.wpart[o.off2 + (blk * MP + n) * H + k] = g2[rr];
+            }
         }
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-            const int n = cb * 16 + 4 * q + rr;
-            const int k = (kh + 2 * j) * 16 + r16;
-            o.wpart[o.off1 + (blk * H + n) * H + k] = g1[j][rr];
-        }
-    if ((w >> 2) < MP / 16) {
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-            const int n = (w >> 2) * 16 + 4 * q + rr;
-            const int k = (w & 3) * 16 + r16;
-            o.wpart[o.off2 + (blk * MP + n) * H + k] = g2[rr];
-        }
+        if (tid < H)
+            o.wpart[o.boff1 + blk * H + tid] = b1acc;
+        else if (tid < H + MP)
+            o.wpart[o.boff2 + blk * MP + tid - H] = b2acc;
     }
-    if (tid < H)
-        o.wpart[o.boff1 + blk * H + tid] = b1acc;
-    else if (tid < H + MP)
-        o.wpart[o.boff2 + blk * MP + tid - H] = b2acc;
-    if (MODE == FWD) {
+    if (MODE != FVP) {
         static_assert(L::total >= 2 * KT, "row_pass_final scratch");
         __syncthreads();
         row_pass_final<MODE, MP, KT>(racc0, racc1, reinterpret_cast<double*>(smem), a.rpart, blk, tid);

@@ -44,6 +44,8 @@ struct RowArgs {
     double* rpart;        // per-workgroup partials
     const int32_t* done;
     float llc;            // -0.5 * m * log(2 pi) rounded to f32
+    const void* xs;       // split-f16 xhat rows [T][hi NP | lo NP] (k_ks<.., SX>), or null
+    const float* xu;      // [T] power-of-two row scales of xs
 };
 
 template <int H0, int H1, int MP>
@@ -775,6 +777,7 @@ RowArgs row_args(const mjrl_shape* s, const mjrl_rows* r, int64_t T) {
     ra.xhat = r->xhat; ra.act = r->act; ra.adv = r->adv; ra.adv_vpg = r->adv_vpg;
     ra.a0 = r->a0; ra.a1 = r->a1; ra.mu0 = r->mu0; ra.ll0 = r->ll0;
     ra.gu0 = r->gu0; ra.gu1 = r->gu1; ra.gp = r->gp;
+    ra.xs = r->xs; ra.xu = r->xu;
     ra.llc = (float)(-0.5 * (double)s->m * log(2.0 * M_PI));
     return ra;
 }
@@ -818,10 +821,13 @@ inline int grad_slices(const mjrl_shape* s, int64_t T) {
     return p == 2 ? ks_grid(T) : (p == 1 ? fused_grid(T) : wgrad_slices(T));
 }
 
-template <int MP, int KG, int MODE>
+// the split-f16 first layer additionally needs NP % 128 == 0 (chunk swizzle)
+bool ksx_supported(const mjrl_shape* s) { return ks_supported(s) && s->np % 128 == 0; }
+
+template <int MP, int KG, int MODE, bool SX>
 int launch_ks_t(const RowArgs& ra, const FOut& fo, int grid, hipStream_t st) {
-    using L = KLayout<MP, KG>;
-    auto fn = k_ks<MP, KG, MODE>;
+    using L = KLayout<MP, KG, SX>;
+    auto fn = k_ks<MP, KG, MODE, SX>;
     static bool attr = false;
     if (!attr) {
         hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, L::bytes);
@@ -832,11 +838,22 @@ int launch_ks_t(const RowArgs& ra, const FOut& fo, int grid, hipStream_t st) {
     return (int)hipGetLastError();
 }
 
+// rows given as split-f16 (ra.xs) run the SX kernel; f32 xhat the exact-f32 one
 template <int MODE>
 int launch_ks(const mjrl_shape* s, const RowArgs& ra, const FOut& fo, int grid, hipStream_t st) {
     const int kg = s->np / 32;
+    if (ra.xs) {
 #define MJRL_K(MP_, KG_) \
-    if (s->mp == MP_ && kg == KG_) return launch_ks_t<MP_, KG_, MODE>(ra, fo, grid, st);
+    if (s->mp == MP_ && kg == KG_) return launch_ks_t<MP_, KG_, MODE, true>(ra, fo, grid, st);
+#define MJRL_KN(MP_) MJRL_K(MP_, 4) MJRL_K(MP_, 8) MJRL_K(MP_, 12)
+        MJRL_KN(16)
+        MJRL_KN(32)
+#undef MJRL_KN
+#undef MJRL_K
+        return MJRL_ESHAPE;
+    }
+#define MJRL_K(MP_, KG_) \
+    if (s->mp == MP_ && kg == KG_) return launch_ks_t<MP_, KG_, MODE, false>(ra, fo, grid, st);
 #define MJRL_KN(MP_) MJRL_K(MP_, 2) MJRL_K(MP_, 4) MJRL_K(MP_, 6) MJRL_K(MP_, 8) MJRL_K(MP_, 12)
     MJRL_KN(16)
     MJRL_KN(32)
@@ -945,7 +962,9 @@ int run_wgrad_only(const mjrl_shape* s, const mjrl_rows* r, int64_t T, const mjr
 }
 
 bool rows_ok(const mjrl_shape* s, const mjrl_rows* r) {
-    if (!s || !r || r->T < 0 || !r->xhat) return false;
+    if (!s || !r || r->T < 0) return false;
+    // split-f16 rows (xs + xu) only feed the K-split kernel; every other path reads f32 xhat
+    if (r->xs ? (!r->xu || !ksx_supported(s)) : !r->xhat) return false;
     if (s->h0 && (!r->a0 || !r->a1 || !r->gu0 || !r->gu1)) return false;
     return r->gp != nullptr;
 }
@@ -1051,6 +1070,8 @@ int mjrl_policy_fvp(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_fvp, c
 
 int mjrl_fused_path(const mjrl_shape* s) { return s ? acc_path(s, 1) : 0; }
 
+int mjrl_split_supported(const mjrl_shape* s) { return s && ksx_supported(s) ? 1 : 0; }
+
 int mjrl_policy_eval(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_eval, const float* packed_theta_new,
                      const float* packed_theta_old, const float* out_shift, const float* out_scale,
                      const mjrl_scratch* sc, double* sums, void* stream) {
@@ -1065,10 +1086,11 @@ int mjrl_policy_eval(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_eval,
     ra.out_shift = out_shift;
     ra.out_scale = out_scale;
     ra.rpart = sc->rpart;
-    // forward-only: the row kernel (no weight-gradient state to keep resident)
-    const int G = row_grid(s, T_eval);
+    // forward-only: the K-split kernel in EVAL mode where it applies, else the row kernel
+    const bool ks = ks_supported(s);
+    const int G = ks ? ks_grid(T_eval) : row_grid(s, T_eval);
     if (T_eval > 0) {
-        int e = launch_rows<EVAL>(s, ra, G, st);
+        int e = ks ? launch_ks<EVAL>(s, ra, FOut{}, G, st) : launch_rows<EVAL>(s, ra, G, st);
         if (e) return e;
     } else {
         hipMemsetAsync(sc->rpart, 0, sizeof(double) * 2 * G, st);

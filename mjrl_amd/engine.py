@@ -13,6 +13,7 @@ mjrl/algos/batch_reinforce.py:106-164, mjrl/utils/process_samples.py:3-44.
 """
 import ctypes as C
 import math
+import os
 
 import numpy as np
 import torch
@@ -137,7 +138,11 @@ class DeviceBatch:
 class UpdateEngine:
     """Owns the HBM workspace for one policy shape and runs updates on it."""
 
-    def __init__(self, n, m, hidden, device=None, comm=None, min_log_std=-3.0):
+    def __init__(self, n, m, hidden, device=None, comm=None, min_log_std=-3.0, precision=None):
+        """precision: 'split' runs the K = obs first layer of the MLP(64,64) passes as
+        split-f16 MFMA (hi*hi + hi*lo + lo*hi, f32 accumulate), 'f32'
+        on exact-f32 MFMA; default (None / 'auto', or $MJRL_AMD_PRECISION): split
+        wherever the kernels support it (mjrl_split_supported), f32 elsewhere."""
         self.lib = _lib.lib()
         h0, h1 = (0, 0) if hidden is None else (int(hidden[0]), int(hidden[1]))
         self.shape = _lib.make_shape(int(n), int(m), h0, h1)
@@ -161,6 +166,13 @@ class UpdateEngine:
         self.transforms = (None, None, None, None)
         self.kernel_timing = None   # list -> (start, accumulate done, gather done) events per FVP
         self.fused = bool(self.lib.mjrl_fused_path(C.byref(self.shape)))
+        prec = precision or os.environ.get("MJRL_AMD_PRECISION", "auto")
+        if prec not in ("auto", "split", "f32"):
+            raise ValueError("precision must be 'auto', 'split' or 'f32', got %r" % (prec,))
+        can_split = bool(self.lib.mjrl_split_supported(C.byref(self.shape)))
+        if prec == "split" and not can_split:
+            raise ValueError("split precision is not available for this policy shape")
+        self.split = can_split and prec != "f32"
 
     # ------------------------------------------------------------------
     def set_transformations(self, in_shift=None, in_scale=None, out_shift=None, out_scale=None):
@@ -184,7 +196,12 @@ class UpdateEngine:
         f64 = dict(dtype=torch.float64, device=dev)
         self.ws = {}
         w = self.ws
-        w["xhat"] = torch.empty((T_all, s.np), **f32)
+        if self.split:
+            # split-f16 rows [hi np | lo np] + power-of-two row scales (mjrl_rows.xs / xu)
+            w["xs"] = torch.empty((T_all, 2 * s.np), dtype=torch.float16, device=dev)
+            w["xu"] = torch.empty(T_all, **f32)
+        else:
+            w["xhat"] = torch.empty((T_all, s.np), **f32)
         w["act32"] = torch.empty((T_all, s.m), **f32)
         w["ret"] = torch.empty(T_all, **f64)
         w["adv64"] = torch.empty(T_all, **f64)
@@ -222,9 +239,13 @@ class UpdateEngine:
         w = self.ws
         r = _lib.Rows()
         r.T = T
-        for k, key in (("xhat", "xhat"), ("act", "act32"), ("adv", "adv32"), ("a0", "a0"), ("a1", "a1"),
+        for k, key in (("act", "act32"), ("adv", "adv32"), ("a0", "a0"), ("a1", "a1"),
                        ("mu0", "mu0"), ("ll0", "ll0"), ("gu0", "gu0"), ("gu1", "gu1"), ("gp", "gp")):
             setattr(r, k, w[key].data_ptr())
+        if self.split:
+            r.xs, r.xu = w["xs"].data_ptr(), w["xu"].data_ptr()
+        else:
+            r.xhat = w["xhat"].data_ptr()
         r.adv_vpg = adv_vpg.data_ptr()
         return r
 
@@ -237,6 +258,19 @@ class UpdateEngine:
         _lib.check(fn(_lib.ptr(x), N, center, _lib.ptr(self.mom_part),
                       C.c_void_p(self.stats[out_slot:].data_ptr()), self.st), "mjrl_moments")
         self.comm.allreduce_sum(self._stat(out_slot))
+
+    def _pack(self, obs, act, T, st):
+        """a5 batch assembly: f64 obs / act -> the row format the policy passes read."""
+        w = self.ws
+        ins, isc, _, _ = self.transforms
+        sp = C.byref(self.shape)
+        if self.split:
+            _lib.check(self.lib.mjrl_pack_batch_split(_lib.ptr(obs), _lib.ptr(act), T, sp, _lib.ptr(ins),
+                                                      _lib.ptr(isc), _lib.ptr(w["xs"]), _lib.ptr(w["xu"]),
+                                                      _lib.ptr(w["act32"]), st), "mjrl_pack_batch_split")
+        else:
+            _lib.check(self.lib.mjrl_pack_batch(_lib.ptr(obs), _lib.ptr(act), T, sp, _lib.ptr(ins), _lib.ptr(isc),
+                                                _lib.ptr(w["xhat"]), _lib.ptr(w["act32"]), st), "mjrl_pack_batch")
 
     # ------------------------------------------------------------------
     def returns_advantages(self, batch, gamma, gae_lambda):
@@ -300,9 +334,7 @@ class UpdateEngine:
         timing = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
 
         # a5: batch assembly (f64 -> f32, input normalisation, bias column)
-        _lib.check(L.mjrl_pack_batch(_lib.ptr(batch.obs), _lib.ptr(batch.act), T_all, sp, _lib.ptr(ins),
-                                     _lib.ptr(isc), _lib.ptr(w["xhat"]), _lib.ptr(w["act32"]), st),
-                   "mjrl_pack_batch")
+        self._pack(batch.obs, batch.act, T_all, st)
         # a1-a3: returns / advantages
         if batch.advantages is not None:
             adv64 = batch.advantages
@@ -560,14 +592,19 @@ class UpdateEngine:
         cap = max(sub["max"], 1)
         f32 = dict(dtype=torch.float32, device=self.device)
         ws = self.__dict__.setdefault("ws_sub", {})
-        if "xs" not in ws or ws["xs"].shape[0] < cap:
-            ws["xs"] = torch.empty((cap, s.np), **f32)
-            if s.h0:
-                ws["a0s"] = torch.empty((cap, s.h0), **f32)
-                ws["a1s"] = torch.empty((cap, s.h1), **f32)
-        pairs = [("xhat", "xs", s.np)] + ([("a0", "a0s", s.h0), ("a1", "a1s", s.h1)] if s.h0 else [])
+        if "a0s" not in ws or ws["a0s"].shape[0] < cap:
+            if self.split:
+                ws["xss"] = torch.empty((cap, 2 * s.np), dtype=torch.float16, device=self.device)
+                ws["xus"] = torch.empty(cap, **f32)
+            else:
+                ws["xhs"] = torch.empty((cap, s.np), **f32)
+            ws["a0s"] = torch.empty((cap, max(s.h0, 1)), **f32)
+            ws["a1s"] = torch.empty((cap, max(s.h1, 1)), **f32)
+        pairs = [("xs", "xss", s.np), ("xu", "xus", 1)] if self.split else [("xhat", "xhs", s.np)]
+        if s.h0:
+            pairs += [("a0", "a0s", s.h0), ("a1", "a1s", s.h1)]
         rows = self._rows(n_k, adv_vpg)
-        for src, dst, width in pairs:
+        for src, dst, width in pairs:   # rows of 4 * width bytes (f32, or the f16 hi / lo pair of xs)
             _lib.check(self.lib.mjrl_gather_rows(_lib.ptr(w[src]), 4 * width, ip, n_k, _lib.ptr(ws[dst]), self.st),
                        "mjrl_gather_rows")
             setattr(rows, src, ws[dst].data_ptr())
@@ -628,9 +665,7 @@ class UpdateEngine:
         o = torch.from_numpy(np.ascontiguousarray(obs, dtype=np.float64)).to(dev)
         a = torch.from_numpy(np.ascontiguousarray(act, dtype=np.float64)).to(dev)
         ins, isc, _, _ = self.transforms
-        _lib.check(self.lib.mjrl_pack_batch(_lib.ptr(o), _lib.ptr(a), T, C.byref(self.shape), _lib.ptr(ins),
-                                            _lib.ptr(isc), _lib.ptr(self.ws["xhat"]), _lib.ptr(self.ws["act32"]), st),
-                   "mjrl_pack_batch")
+        self._pack(o, a, T, st)
         if adv is not None:
             self.ws["adv32"][:T].copy_(torch.from_numpy(np.asarray(adv, dtype=np.float64)).float().to(dev))
         else:

@@ -30,6 +30,10 @@ from conftest import golden_cases, GOLDEN
 pytestmark = pytest.mark.gpu
 
 CASES = golden_cases()
+# every case on the default precision (split-f16 first layer where the shape allows
+# it: the Humanoid-shaped c4), plus the exact-f32 kernels on those same cases
+SPLIT_CASES = [n for n in CASES if n.startswith("c4")]
+CASES_P = [(n, None) for n in CASES] + [(n, "f32") for n in SPLIT_CASES]
 
 
 def nrel(a, b):
@@ -64,13 +68,15 @@ def make_batch(c, dev):
                        t(c["terminated"].astype(np.uint8)), T_demo=T_demo)
 
 
-def run_case(name):
+def run_case(name, precision=None):
     from mjrl_amd.engine import UpdateEngine
     c, case_kwargs = load(name)
     kw = case_kwargs(c)
     dev = torch.device("cuda:0")
     hidden = c["hidden_t"]
-    eng = UpdateEngine(int(c["n"]), int(c["m"]), hidden, device=dev)
+    eng = UpdateEngine(int(c["n"]), int(c["m"]), hidden, device=dev, precision=precision)
+    if name in SPLIT_CASES:
+        assert eng.split == (precision != "f32")
     if c["transforms"] is not None:
         eng.set_transformations(*c["transforms"])
     batch = make_batch(c, dev)
@@ -94,9 +100,9 @@ def run_case(name):
     return c, kw, eng, res
 
 
-@pytest.mark.parametrize("name", CASES)
-def test_update_matches_reference(name):
-    c, kw, eng, res = run_case(name)
+@pytest.mark.parametrize("name,precision", CASES_P)
+def test_update_matches_reference(name, precision):
+    c, kw, eng, res = run_case(name, precision)
     w = eng.ws
     T = c["returns"].shape[0]
     assert np.array_equal(w["ret"][:T].cpu().numpy(), c["returns"])
@@ -133,9 +139,9 @@ def test_update_matches_reference(name):
         assert after == np.random.rand()
 
 
-@pytest.mark.parametrize("name", CASES)
-def test_fvp_and_teacher_forced_cg(name):
-    c, kw, eng, res = run_case(name)
+@pytest.mark.parametrize("name,precision", CASES_P)
+def test_fvp_and_teacher_forced_cg(name, precision):
+    c, kw, eng, res = run_case(name, precision)
     dev = torch.device("cuda:0")
     damping = kw.get("damping", 1e-4)
     from oracle import npg_cpu as O

@@ -34,6 +34,8 @@ N_OBS, N_ACT, HIDDEN = 376, 17, (64, 64)
 N_PATHS, HORIZON = 1000, 1000
 GAMMA, LAM, DELTA, CG_ITERS, DAMPING = 0.995, 0.97, 0.01, 10, 1e-4
 PEAK_F32_MFMA = 157.3   # TFLOP/s, MI355X dense fp32 matrix (MI355X_MICROARCH.md)
+PEAK_F16_MFMA = 2500.0  # TFLOP/s, dense f16 / bf16 matrix (no sparsity)
+PEAK_SPLIT = PEAK_F16_MFMA / 3   # f32-equivalent rate of the split-f16 products (3 f16 MFMAs each)
 PEAK_HBM = 8000.0       # GB/s
 
 
@@ -265,14 +267,20 @@ def main():
     fl = flops_per_row(N_OBS, N_ACT, *HIDDEN)
     rows_rank = batch.T
     path = eng.accumulate_path()
-    np_ = eng.shape.np
+    np_, mp = eng.shape.np, eng.shape.mp
+    # algorithmic HBM bytes per row of one FVP launch: the observation row (f32, or the
+    # split-f16 hi / lo pair + row scale) and the cached a0 / a1 activations
+    fvp_bytes = 4 * np_ + (4 if eng.split else 0) + 4 * (HIDDEN[0] + HIDDEN[1])
     if path == 0:   # rows kernel then split-K weight-gradient kernel: time each
         acc_name, acc_key, acc_fl = "k_rows<64,64,32,FVP>", "k_rows<64, 64, 32, 1>", fl["rows_fvp"]
         gat_name, gat_key, gat_fl = "k_wgrad", "k_wgrad", fl["weight_grads"]
     else:           # one persistent kernel does both; the gather is a pure slab reduction
-        mp = eng.shape.mp
-        acc_name = ("k_ks<%d,%d,FVP>" % (mp, np_ // 32)) if path == 2 else "k_fused<64,64,%d,FVP>" % mp
-        acc_key = ("k_ks<%d, %d, 1>" % (mp, np_ // 32)) if path == 2 else "k_fused<"
+        if path == 2 and eng.split:
+            acc_name, acc_key = "k_kx<%d,%d,FVP>" % (mp, np_ // 32), "k_kx<%d, %d, 1>" % (mp, np_ // 32)
+        elif path == 2:
+            acc_name, acc_key = "k_ks<%d,%d,FVP>" % (mp, np_ // 32), "k_ks<%d, %d, 1, false>" % (mp, np_ // 32)
+        else:
+            acc_name, acc_key = "k_fused<64,64,%d,FVP>" % mp, "k_fused<"
         acc_fl = fl["rows_fvp"] + fl["weight_grads"]
         gat_name, gat_key, gat_fl = "k_gather", "k_gather", 0
     kern = {acc_name: dict(avg_ms=t_acc * 1e3, tflops=acc_fl * rows_rank / t_acc / 1e12),
@@ -281,26 +289,44 @@ def main():
     traffic, tsrc = pmc_traffic(acc_key if dom == acc_name else gat_key)
     if traffic is not None and world > 1:
         traffic = traffic * rows_rank / T_total    # the committed PMC pass is the 1-GPU (1M-row) launch
-    roof = dict(bound="mfma", kernel=dom,
-                achieved=round(kern[dom]["tflops"], 3), peak=PEAK_F32_MFMA, unit="TFLOP/s",
-                frac=round(kern[dom]["tflops"] / PEAK_F32_MFMA, 4),
-                traffic=None if traffic is None else round(traffic),
+    # the roofline that binds the dominant kernel: the larger of its ideal MFMA time
+    # (algorithmic flops at the matrix peak of the form it computes in) and its ideal
+    # HBM time (algorithmic bytes at 8 TB/s)
+    t_dom = kern[dom]["avg_ms"] * 1e-3
+    peak_mm = PEAK_SPLIT if eng.split else PEAK_F32_MFMA
+    flops_dom = (acc_fl if dom == acc_name else gat_fl) * rows_rank
+    bytes_dom = fvp_bytes * rows_rank if dom == acc_name else None
+    t_mm = flops_dom / (peak_mm * 1e12)
+    t_hbm = bytes_dom / (PEAK_HBM * 1e9) if bytes_dom else 0.0
+    if t_hbm > t_mm:
+        roof = dict(bound="hbm", kernel=dom, achieved=round(bytes_dom / t_dom / 1e9, 1), peak=PEAK_HBM, unit="GB/s",
+                    frac=round(bytes_dom / t_dom / 1e9 / PEAK_HBM, 4), bytes_per_timestep=fvp_bytes)
+    else:
+        roof = dict(bound="mfma", kernel=dom, achieved=round(flops_dom / t_dom / 1e12, 3), peak=peak_mm,
+                    unit="TFLOP/s", frac=round(flops_dom / t_dom / 1e12 / peak_mm, 4))
+    roof.update(traffic=None if traffic is None else round(traffic),
                 traffic_unit="bytes/launch (HBM, PMC)", traffic_source=tsrc,
-                traffic_GBps=None if traffic is None else round(traffic / (kern[dom]["avg_ms"] * 1e-3) / 1e9, 1),
+                traffic_GBps=None if traffic is None else round(traffic / t_dom / 1e9, 1),
                 flops_per_timestep=acc_fl if dom == acc_name else gat_fl, rows_per_launch=rows_rank,
+                mfma_form="split-f16 (3 x v_mfma_f32_16x16x32_f16 per f32 product), peak %.1f TFLOP/s f32-equivalent"
+                          % PEAK_SPLIT if eng.split else "f32 (v_mfma_f32_16x16x4_f32)",
+                ideal_ms=dict(mfma=round(t_mm * 1e3, 4), hbm=round(t_hbm * 1e3, 4)),
+                achieved_tflops=round(flops_dom / t_dom / 1e12, 3),
                 launches=len(ev), kernels={k: {kk: round(vv, 4) for kk, vv in v.items()} for k, v in kern.items()})
     # whole-update algorithmic FLOP rate, all kernels and gaps included
     ufl = update_flops_per_row(N_OBS, N_ACT, HIDDEN[0], HIDDEN[1], CG_ITERS)
     ut = ufl * T_total / (elapsed / args.steps) / 1e12
     roof["update"] = dict(flops_per_timestep=ufl, achieved=round(ut, 3), unit="TFLOP/s",
-                          frac=round(ut / (PEAK_F32_MFMA * world), 4),
-                          note="algorithmic FLOPs of a whole update / wall time per update, vs n_gpus x peak")
+                          frac_f32_peak=round(ut / (PEAK_F32_MFMA * world), 4),
+                          note="algorithmic FLOPs of a whole update / wall time per update, vs n_gpus x the "
+                               "f32 matrix peak")
 
     if rank == 0:
         ms = elapsed / args.steps * 1e3
         out = dict(metric=METRIC, value=round(T_total * args.steps / elapsed, 1), unit="timesteps/s",
                    n_gpus=world, steps=args.steps, warmup=args.warmup, ms_per_step=round(ms, 3),
-                   higher_is_better=True, scaling="strong", vs_baseline=None, dtype="f32",
+                   higher_is_better=True, scaling="strong", vs_baseline=None,
+                   dtype="f32" if not eng.split else "f32 (split-f16 MFMA, f32 accumulate)",
                    data="synthetic (seeded N(0,1) obs/act/rewards, LinearBaseline fitted on 20 paths)",
                    config=dict(workload="humanoid_npg_1M", obs_dim=N_OBS, act_dim=N_ACT, hidden=list(HIDDEN),
                                timesteps=T_total, paths=args.paths, horizon=HORIZON, cg_iters=CG_ITERS,

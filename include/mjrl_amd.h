@@ -220,10 +220,14 @@ int mjrl_gather_grads(const mjrl_shape* s, const mjrl_rows* rows, int64_t T,
 int mjrl_fused_path(const mjrl_shape* s);
 
 /* ---- conjugate gradient on device (cg_solve.py:3-22) ----
- * State cg[8] (f32 scalars, device): [rdotr, v, mu, pz, done_flag(as int bits), iters, ...].
+ * State cg[MJRL_CG_STATE] (f32, device): cg[0] rdotr, cg[1] iterations run,
+ * cg[2] v, cg[3] mu, cg[4] p.z; cg[8..] scratch of the multi-workgroup step
+ * (ticket and per-workgroup partials).
  * init: x = 0, r = b, p = b, rdotr = b.b; packs p into packed_p.
  * step: z = gsum * inv_T + c(sigma) * p_logstd + damping * p, then the
- *       reference's update of x, r, p, rdotr and the residual_tol break. */
+ *       reference's update of x, r, p, rdotr and the residual_tol break
+ *       (three multi-workgroup launches; fixed-order fp64 dot products). */
+#define MJRL_CG_STATE 1024
 int mjrl_cg_init(const mjrl_shape* s, const float* b, float* x, float* r, float* p,
                  float* packed_p, float* cg, int32_t* done, void* stream);
 int mjrl_cg_step(const mjrl_shape* s, const float* gsum, double inv_T, float damping,

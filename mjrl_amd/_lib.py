@@ -19,6 +19,7 @@ LIB_PATH = os.path.join(HERE, "lib", "libmjrl_amd.so")
 MJRL_OK = 0
 MJRL_EINVAL = -1
 MJRL_ESHAPE = -2
+CG_STATE = 1024   # MJRL_CG_STATE: floats of the device CG state
 
 
 class Shape(C.Structure):
@@ -82,11 +83,13 @@ class MjrlError(RuntimeError):
     pass
 
 
-def load(path=LIB_PATH):
-    """Loads the shared library and declares every entry point (no GPU needed)."""
+def load(path=None):
+    """Loads the shared library and declares every entry point (no GPU needed).
+    $MJRL_AMD_LIB selects another build of it (e.g. the profiling variant)."""
     global _LIB
     if _LIB is not None:
         return _LIB
+    path = path or os.environ.get("MJRL_AMD_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise MjrlError("mjrl_amd HIP library not built: %s (run `python -m mjrl_amd.build`)" % path)
     lib = C.CDLL(path)

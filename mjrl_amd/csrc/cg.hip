@@ -94,6 +94,7 @@ __global__ void __launch_bounds__(CG_THREADS) k_cg_init(mjrl_shape s, const floa
     if (threadIdx.x == 0) {
         cg[0] = (float)rr;   // rdotr
         cg[1] = 0.f;         // iterations run
+        *reinterpret_cast<unsigned*>(cg + 8) = 0u;   // k_cgm_* ticket
         *done = 0;
     }
 }
@@ -193,6 +194,121 @@ __global__ void __launch_bounds__(CG_THREADS) k_cg_step(mjrl_shape s, const floa
         cg[3] = mu;
         cg[4] = pz;
         if (rr < tol) *done = 1;   // cg_solve.py:19-20
+    }
+}
+
+// ---------------------------------------------------------------------------
+// The same iteration as k_cg_step over many workgroups (MJRL_CG_WG elements
+// each), in three launches; each dot product is a fixed-order fp64 sum of
+// per-workgroup partials folded by the LAST workgroup to arrive (atomic ticket,
+// no spinning), so results do not depend on scheduling:
+//   k_cgm_z : z = F p + damping p, pz            -> cg[4] = pz, cg[2] = v = rdotr / pz
+//   k_cgm_xr: x += v p, r -= v z, rr             -> cg[0] = rr, cg[3] = mu, iters, done
+//   k_cgm_p : p = r + mu p, packed p
+// State beyond cg[0..7]: cg[8] = ticket (u32), cg[16..] = double partials.
+// ---------------------------------------------------------------------------
+constexpr int CGM_T = 256;                 // threads per workgroup
+constexpr int CGM_U = 4;                   // elements per thread
+constexpr int CGM_WG = CGM_T * CGM_U;      // elements per workgroup
+constexpr int CGM_MAXWG = (MJRL_CG_STATE - 16) / 2;
+
+// fixed-order fold of nwg per-workgroup partials by the last workgroup to finish
+__device__ __forceinline__ bool cgm_last(double part, float* cg, int nwg, double* red, double& total) {
+    double* parts = reinterpret_cast<double*>(cg + 16);
+    const double b = block_sum<CGM_T>(part, red);
+    __shared__ unsigned ticket;
+    if (threadIdx.x == 0) {
+        parts[blockIdx.x] = b;
+        __threadfence();
+        ticket = atomicAdd(reinterpret_cast<unsigned*>(cg + 8), 1u);
+    }
+    __syncthreads();
+    if (ticket != (unsigned)(nwg - 1)) return false;
+    __threadfence();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int i = 0; i < nwg; ++i) t += parts[i];   // visible after the acquire fence above
+        total = t;
+        *reinterpret_cast<unsigned*>(cg + 8) = 0u;   // reset the ticket for the next launch
+    }
+    return true;
+}
+
+__global__ void __launch_bounds__(CGM_T) k_cgm_z(mjrl_shape s, const float* __restrict__ gsum, double inv_T,
+                                                 float damping, const float* __restrict__ packed_theta,
+                                                 const float* __restrict__ p, float* __restrict__ z, float* cg,
+                                                 const int32_t* __restrict__ done) {
+    __shared__ double red[CGM_T / 64];
+    if (*done) return;
+    const Packed pk(s.h0, s.h1, s.np, s.mp);
+    const int ls0 = s.d - s.m, d = s.d;
+    double acc = 0.0;
+#pragma unroll
+    for (int u = 0; u < CGM_U; ++u) {
+        const int f = blockIdx.x * CGM_WG + u * CGM_T + threadIdx.x;
+        if (f >= d) continue;
+        const float pf = p[f];
+        float hv;
+        if (f >= ls0) {
+            const float sg = expf(packed_theta[pk.ls + (f - ls0)]);
+            const double uu = (double)sg * (double)sg;
+            const double c = 4.0 * uu * (2.0 * uu - 1e-8) / ((2.0 * uu + 1e-8) * (2.0 * uu + 1e-8));
+            hv = (float)(c * (double)pf);
+        } else {
+            hv = (float)((double)gsum[f] * inv_T);
+        }
+        const float zf = __fadd_rn(hv, __fmul_rn(damping, pf));   // hvp_flat + regu_coef*vector
+        z[f] = zf;
+        acc += (double)pf * (double)zf;
+    }
+    double t;
+    if (cgm_last(acc, cg, gridDim.x, red, t) && threadIdx.x == 0) {
+        const float pz = (float)t;
+        cg[4] = pz;
+        cg[2] = cg[0] / pz;   // v = rdotr / p.z
+    }
+}
+
+__global__ void __launch_bounds__(CGM_T) k_cgm_xr(int d, const float* __restrict__ p, const float* __restrict__ z,
+                                                  float* __restrict__ x, float* __restrict__ r, float* cg,
+                                                  int32_t* __restrict__ done, float tol) {
+    __shared__ double red[CGM_T / 64];
+    if (*done) return;
+    const float v = cg[2];
+    double acc = 0.0;
+#pragma unroll
+    for (int u = 0; u < CGM_U; ++u) {
+        const int f = blockIdx.x * CGM_WG + u * CGM_T + threadIdx.x;
+        if (f >= d) continue;
+        x[f] = __fadd_rn(x[f], __fmul_rn(v, p[f]));
+        const float rf = __fsub_rn(r[f], __fmul_rn(v, z[f]));
+        r[f] = rf;
+        acc += (double)rf * (double)rf;
+    }
+    double t;
+    if (cgm_last(acc, cg, gridDim.x, red, t) && threadIdx.x == 0) {
+        const float rr = (float)t;
+        const float rdotr = cg[0];
+        cg[3] = rr / rdotr;   // mu
+        cg[0] = rr;
+        cg[1] += 1.f;
+        if (rr < tol) *done = 1;   // cg_solve.py:19-20
+    }
+}
+
+__global__ void __launch_bounds__(CGM_T) k_cgm_p(mjrl_shape s, const float* __restrict__ r, float* __restrict__ p,
+                                                 float* __restrict__ packed_p, const float* cg,
+                                                 const int32_t* __restrict__ done) {
+    if (*done) return;   // converged: p is not used again
+    const PackMap pm(s);
+    const float mu = cg[3];
+#pragma unroll
+    for (int u = 0; u < CGM_U; ++u) {
+        const int f = blockIdx.x * CGM_WG + u * CGM_T + threadIdx.x;
+        if (f >= s.d) continue;
+        const float pf = __fadd_rn(r[f], __fmul_rn(mu, p[f]));
+        p[f] = pf;
+        pack_one(pm, f, pf, packed_p, false, 0.f);
     }
 }
 
@@ -310,8 +426,16 @@ int mjrl_cg_step(const mjrl_shape* s, const float* gsum, double inv_T, float dam
                  float* x, float* r, float* p, float* z, float* packed_p, float* cg, int32_t* done,
                  float residual_tol, void* stream) {
     if (!s || !gsum || !packed_theta || !x || !r || !p || !z || !packed_p || !cg || !done) return MJRL_EINVAL;
-    hipLaunchKernelGGL(k_cg_step, dim3(1), dim3(CG_THREADS), 0, (hipStream_t)stream, *s, gsum, inv_T, damping,
-                       packed_theta, x, r, p, z, packed_p, cg, done, residual_tol);
+    hipStream_t st = (hipStream_t)stream;
+    const int nwg = (s->d + CGM_WG - 1) / CGM_WG;
+    if (nwg > CGM_MAXWG) {   // beyond the partials the state holds: the single-workgroup form
+        hipLaunchKernelGGL(k_cg_step, dim3(1), dim3(CG_THREADS), 0, st, *s, gsum, inv_T, damping, packed_theta, x, r,
+                           p, z, packed_p, cg, done, residual_tol);
+        return err(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_cgm_z, dim3(nwg), dim3(CGM_T), 0, st, *s, gsum, inv_T, damping, packed_theta, p, z, cg, done);
+    hipLaunchKernelGGL(k_cgm_xr, dim3(nwg), dim3(CGM_T), 0, st, s->d, p, z, x, r, cg, done, residual_tol);
+    hipLaunchKernelGGL(k_cgm_p, dim3(nwg), dim3(CGM_T), 0, st, *s, r, p, packed_p, cg, done);
     return err(hipGetLastError());
 }
 

@@ -62,10 +62,14 @@ struct KLayout {
     static_assert(!SX || NP % 128 == 0, "SX: the chunk swizzle needs NP % 128 == 0");
 };
 
-// XOR swizzle of the 16-byte chunks of row `row` in the SX xhat images:
-// ds_read_b128 of 16 consecutive rows and ds_read_b64_tr_b16 of rows
-// {r0..r0+3, r0+8..r0+11} both touch 64 distinct banks.
-__device__ __forceinline__ int chunk_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+// XOR swizzle of the 16-byte chunks of row `row` in the SX xhat images (rows of
+// NP halves, a multiple of 256 B): ds_read_b128 of 16 rows (lane groups
+// {0-3,12-15,20-27}, ... of MI355X_MICROARCH.md §LDS) and ds_read_b64_tr_b16 of
+// rows {8q + 4h + 0..3} (32-lane halves) both touch 64 distinct banks (found by
+// exhaustive search over XOR-linear maps, tools/swizzle_search.py).
+__device__ __forceinline__ int chunk_swz(int row) {
+    return ((row & 1) << 1) | (((row >> 1) & 1) << 2) | (((row >> 3) & 1) << 3);
+}
 
 // acc += A[rows][k] (LDS, row-major) x B where B(k, n) = Bs[n][k] (LDS, row-major by n)
 template <int NR>

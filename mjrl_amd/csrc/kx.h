@@ -1,0 +1,725 @@
+// kx.h — the K-split persistent FWD / FVP / EVAL kernel for the MLP(64,64) policy
+// with EVERY product on split-f16 MFMA (common.h "fp16x3": hi*hi + hi*lo + lo*hi
+// on v_mfma_f32_16x16x32_f16, f32 accumulate), included by policy.hip.
+//
+// Same tile walk as k_ks<.., SX = true> (ks.h): one 512-thread workgroup per CU,
+// 32-row tiles, the first layer K-split over the 8 waves with the W0 / dW0 slice
+// and the gW0 accumulator in registers, the xhat tile as swizzled hi / lo images.
+// The 64-wide layers, which k_ks keeps on exact-f32 MFMA, run here as split
+// products too:
+//   weights  — split once per launch into LDS images (hi, lo), each scaled by a
+//              power of two per row or per column; one image serves a layer's
+//              forward product (row reads) and its backward product (transposed
+//              reads, ds_read_b64_tr_b16) when it is column-scaled, the column
+//              scale being folded into the dynamic left operand;
+//   cached activations a0 / a1 (|a| < 1) — split without scaling into
+//              [feature][row] images read both ways;
+//   dynamic operands (tangents, upstream gradients) — scaled by a power of two
+//              per row (over the K of the product, max over the 4 lane groups)
+//              or, for the weight-gradient sums, per (tile, unit) column, split
+//              in registers, and unscaled on the f32 accumulator.
+// Phases per tile (barriers between them): publish, first layer + fold,
+// P2 (layer 1), P3 (output layer), P4 (gu1), P5 (gu0), weight-gradient sums.
+#pragma once
+
+#ifdef MJRL_KX_PROF
+// phase profile (debug builds): wave 0 of block 0 accumulates s_memtime cycles
+// between stamps in (wave-uniform, scalar) registers, written once at the end;
+// read with mjrl_debug_kx_prof
+__device__ unsigned long long g_kx_prof[16];
+#define KX_STAMP(i)                                                     \
+    do {                                                                \
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime();   \
+        kx_acc_[i] += now_ - kx_last_;                                  \
+        kx_last_ = now_;                                                \
+    } while (0)
+#else
+#define KX_STAMP(i) \
+    do {            \
+    } while (0)
+#endif
+
+namespace {
+
+constexpr int AIMG_BYTES = 64 * 64;   // one [64 feature][32 row] f16 activation image
+
+template <int MP, int KG>
+struct XLayout {
+    static constexpr int H = 64, BT = 32;
+    static constexpr int NP = 32 * KG, KH = NP / 2;
+    static constexpr int RBYTES = NP * 2;          // one f16 row of the xhat hi / lo image
+    static constexpr int LD = H + 4;               // f32 [row][LD] buffers
+    static constexpr int LDT = BT + 4;             // f32 transposed [unit][LDT] buffers
+    static constexpr int LDG = 32 + 4;             // GPf [row][LDG] (MP padded to 32)
+    static constexpr int WIMG = 64 * 128;          // one 64-row weight image (hi or lo), bytes
+    static constexpr int WIMG2 = 32 * 128;         // one 32-row (output layer) weight image
+    static constexpr int AIMG = AIMG_BYTES;
+    // byte offsets
+    static constexpr int oXH = 0;
+    static constexpr int oXL = oXH + BT * RBYTES;
+    static constexpr int oS1 = oXL + BT * RBYTES;  // W1c (FVP / FWD) | W1r (EVAL): hi, lo
+    static constexpr int oS2 = oS1 + 2 * WIMG;     // dW1r (FVP) | W1r (FWD)
+    static constexpr int oS3 = oS2 + 2 * WIMG;     // W2c (FVP / FWD) | W2r (EVAL)
+    static constexpr int oS4 = oS3 + 2 * WIMG2;    // dW2r (FVP) | W2r (FWD)
+    static constexpr int oSC = oS4 + 2 * WIMG2;    // f32 inverse scales: s1[64] s2[64] s3[64] s4[32]
+    static constexpr int oU = oSC + (64 + 64 + 64 + 32) * 4;
+    static constexpr int oD0 = oU + BT * 4;        // f32 [BT][LD]: D0 (P1 -> P2), then G1 (P4 -> P5)
+    static constexpr int oD1 = oD0 + BT * LD * 4;  // f32 [BT][LD]: D1 (P2 -> P3), then G0T [H][LDT] (P5 -> P6)
+    static constexpr int D1SZ = (BT * LD > H * LDT ? BT * LD : H * LDT) * 4;
+    static constexpr int oGP = oD1 + D1SZ;         // f32 [BT][LDG]
+    static constexpr int oGPT = oGP + BT * LDG * 4;  // f32 [32][LDT] (units x rows)
+    static constexpr int oG1T = oGPT + 32 * LDT * 4; // f32 [H][LDT]
+    static constexpr int oA0 = oG1T + H * LDT * 4;   // a0 image hi, lo
+    static constexpr int oA1 = oA0 + 2 * AIMG;       // a1 image hi, lo
+    static constexpr int bytes = oA1 + 2 * AIMG;
+    static_assert(bytes <= 160 * 1024, "LDS");
+    static_assert(bytes >= 2 * KT * 8, "row_pass_final scratch");
+    static constexpr int XPER = BT * NP / 4 / KT;
+    static_assert(NP % 128 == 0, "chunk swizzle of the xhat images");
+    static_assert(MP == 16 || MP == 32, "output layer: one k32 step");
+};
+
+// 128-byte-row f16 images (weights [row][64]) and 64-byte-row images
+// (activations [feature][32 rows]): XOR swizzles of the 16-byte chunks under which
+// the b128 row reads and the transposed reads of each image are bank-conflict
+// free (tools/swizzle_search.py).
+__device__ __forceinline__ int swz128(int r) { return (((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2); }
+__device__ __forceinline__ int woff(int row, int col) { return row * 128 + 16 * ((col >> 3) ^ swz128(row)) + 2 * (col & 7); }
+__device__ __forceinline__ int aoff(int f, int row) { return f * 64 + 16 * ((row >> 3) ^ (((f >> 3) & 1) << 1)) + 2 * (row & 7); }
+
+__device__ __forceinline__ half8 cat_tr(const short4v& a, const short4v& b) {
+    return __builtin_bit_cast(half8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+// B operand of out = A W^T from a weight image: lane (j = jb*16 + r, k = 32 s + 8 q ..)
+__device__ __forceinline__ void wrow(const char* img, int imgbytes, int j, int s, int q, half8& h, half8& l) {
+    const int off = woff(j, 32 * s + 8 * q);
+    h = *reinterpret_cast<const half8*>(img + off);
+    l = *reinterpret_cast<const half8*>(img + imgbytes + off);
+}
+// B operand of out = A W from a weight image (B[k = j][n = h] = W[j][h]): transposed reads
+__device__ __forceinline__ void wcol(const char* img, int imgbytes, int hb, int s, int q, int r, half8& h, half8& l) {
+    const int tq = r >> 2, tp = r & 3;
+    const int o0 = woff(32 * s + 8 * q + tq, hb * 16 + 4 * tp);
+    const int o1 = woff(32 * s + 8 * q + 4 + tq, hb * 16 + 4 * tp);
+    h = cat_tr(ds_read_tr16(img + o0), ds_read_tr16(img + o1));
+    l = cat_tr(ds_read_tr16(img + imgbytes + o0), ds_read_tr16(img + imgbytes + o1));
+}
+// A operand of out = A W^T from an activation image [feature][row] (rows rb*16 + r)
+__device__ __forceinline__ void arow(const char* img, int rb, int s, int q, int r, half8& h, half8& l) {
+    const int tq = r >> 2, tp = r & 3;
+    const int o0 = aoff(32 * s + 8 * q + tq, rb * 16 + 4 * tp);
+    const int o1 = aoff(32 * s + 8 * q + 4 + tq, rb * 16 + 4 * tp);
+    h = cat_tr(ds_read_tr16(img + o0), ds_read_tr16(img + o1));
+    l = cat_tr(ds_read_tr16(img + AIMG_BYTES + o0), ds_read_tr16(img + AIMG_BYTES + o1));
+}
+// B operand of a weight-gradient sum (B[k = row][n = feature]) from an activation image
+__device__ __forceinline__ void acol(const char* img, int f, int q, half8& h, half8& l) {
+    const int off = aoff(f, 8 * q);
+    h = *reinterpret_cast<const half8*>(img + off);
+    l = *reinterpret_cast<const half8*>(img + AIMG_BYTES + off);
+}
+// a at (feature f, row) from an activation image (hi + lo)
+__device__ __forceinline__ float aval(const char* img, int f, int row) {
+    const int off = aoff(f, row);
+    return (float)*reinterpret_cast<const _Float16*>(img + off) +
+           (float)*reinterpret_cast<const _Float16*>(img + AIMG_BYTES + off);
+}
+// store 4 consecutive rows (row0..row0+3, row0 % 4 == 0) of feature f into an activation image
+__device__ __forceinline__ void astore4(char* img, int f, int row0, const float (&v)[4]) {
+    typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+    const float4 x = make_float4(v[0], v[1], v[2], v[3]);
+    half4 h, l;
+    h[0] = (_Float16)x.x; h[1] = (_Float16)x.y; h[2] = (_Float16)x.z; h[3] = (_Float16)x.w;
+    l[0] = (_Float16)(x.x - (float)h[0]); l[1] = (_Float16)(x.y - (float)h[1]);
+    l[2] = (_Float16)(x.z - (float)h[2]); l[3] = (_Float16)(x.w - (float)h[3]);
+    const int off = aoff(f, row0);
+    *reinterpret_cast<half4*>(img + off) = h;
+    *reinterpret_cast<half4*>(img + AIMG_BYTES + off) = l;
+}
+
+// Dynamic left operand from an f32 [row][ld] buffer: rows rb*16 + r, K = 32*KS
+// columns, optionally times fold[k] (a column scale of the right operand);
+// scaled per row (power of two over the row's K), split.  Returns the row's
+// inverse scale (same in all four lane groups).
+template <int KS>
+__device__ __forceinline__ float adyn(const float* buf, int ld, int rb, int q, int r, const float* fold,
+                                      half8 (&h)[KS], half8 (&l)[KS]) {
+    float8v v[KS];
+    float mx = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+        v[s] = load8(buf + (rb * 16 + r) * ld + 32 * s + 8 * q);
+        if (fold) v[s] *= load8(fold + 32 * s + 8 * q);
+        mx = fmaxf(mx, absmax8(v[s]));
+    }
+    float inv;
+    const float sc = pow2_scale(max_over_groups(mx), inv);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) split8(v[s], sc, h[s], l[s]);
+    return inv;
+}
+
+// Dynamic left operand of a weight-gradient sum from a transposed f32 [unit][LDT]
+// buffer: unit u = ub*16 + r, rows 8q..8q+7; scaled per (tile, unit); returns in
+// sc4[rr] the inverse scale of output row (unit) 4q + rr of the block.
+__device__ __forceinline__ void gdyn(const float* bufT, int ldt, int ub, int q, int r, half8& h, half8& l,
+                                     float (&sc4)[4]) {
+    const float8v v = load8(bufT + (ub * 16 + r) * ldt + 8 * q);
+    float inv;
+    const float s = pow2_scale(max_over_groups(absmax8(v)), inv);
+    split8(v, s, h, l);
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) sc4[rr] = __shfl(inv, 4 * q + rr, 64);
+}
+
+// Split a [rows][64] f32 weight matrix (global, row-major, row stride 64) into an
+// LDS image pair scaled per row (COLS = false) or per column (COLS = true);
+// inverse scales to inv[].  rows <= 64; rows >= nrows of the image are zero.
+template <bool COLS>
+__device__ void wsplit(const float* __restrict__ W, int nrows, int img_rows, char* img, int imgbytes, float* inv,
+                       int tid) {
+    const int lane = tid & 63, w = tid >> 6;
+    if (COLS) {
+        // wave 0: lane = column; scales from the column max
+        if (w == 0) {
+            float mx = 0.f;
+            for (int j = 0; j < nrows; ++j) mx = fmaxf(mx, fabsf(W[j * 64 + lane]));
+            float iv;
+            pow2_scale(mx, iv);
+            inv[lane] = iv;
+        }
+    } else {
+        for (int j = w; j < img_rows; j += KT / 64) {
+            float mx = j < nrows ? fabsf(W[j * 64 + lane]) : 0.f;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+            float iv;
+            pow2_scale(mx, iv);
+            if (lane == 0) inv[j] = iv;
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < img_rows * 64; i += KT) {
+        const int j = i >> 6, c = i & 63;
+        const float x = j < nrows ? W[j * 64 + c] : 0.f;
+        const float y = x / inv[COLS ? c : j];   // exact: inv is a power of two
+        const _Float16 h = (_Float16)y;
+        const int off = woff(j, c);
+        *reinterpret_cast<_Float16*>(img + off) = h;
+        *reinterpret_cast<_Float16*>(img + imgbytes + off) = (_Float16)(y - (float)h);
+    }
+}
+
+template <int MP, int KG, int MODE>
+__global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
+    using L = XLayout<MP, KG>;
+    constexpr int H = 64, BT = L::BT, NP = L::NP, KH = L::KH;
+    constexpr bool GRAD = MODE != EVAL;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    char* sb = reinterpret_cast<char*>(smem);
+    char* XHb = sb + L::oXH;
+    char* XLb = sb + L::oXL;
+    char* S1 = sb + L::oS1;
+    char* S2 = sb + L::oS2;
+    char* S3 = sb + L::oS3;
+    char* S4 = sb + L::oS4;
+    float* sc1 = reinterpret_cast<float*>(sb + L::oSC);
+    float* sc2 = sc1 + 64;
+    float* sc3 = sc2 + 64;
+    float* sc4v = sc3 + 64;
+    float* Us = reinterpret_cast<float*>(sb + L::oU);
+    float* D0 = reinterpret_cast<float*>(sb + L::oD0);    // D0, then G1
+    float* D1 = reinterpret_cast<float*>(sb + L::oD1);    // D1, then G0T
+    float* GPf = reinterpret_cast<float*>(sb + L::oGP);
+    float* GPT = reinterpret_cast<float*>(sb + L::oGPT);
+    float* G1T = reinterpret_cast<float*>(sb + L::oG1T);
+    char* A0i = sb + L::oA0;
+    char* A1i = sb + L::oA1;
+
+    if (MODE == FVP && a.done && *a.done) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int r16 = lane & 15, q = lane >> 4;
+    const int cb = w & 3, kh = w >> 2;
+    const int m = a.m;
+    const int64_t T = a.T;
+    const int64_t ntiles = (T + BT - 1) / BT;
+    const float* P = a.P;
+    const Packed pk(H, H, NP, MP);
+    const float* W0src = (MODE == FVP ? a.V : P) + pk.W0;
+
+    // ---- launch preamble: weight images, this wave's W0 / dW0 slice to registers ----
+    if (MODE == EVAL) {
+        wsplit<false>(P + pk.W1, H, H, S1, L::WIMG, sc1, tid);
+        wsplit<false>(P + pk.W2, MP, 32, S3, L::WIMG2, sc3, tid);
+    } else {
+        wsplit<true>(P + pk.W1, H, H, S1, L::WIMG, sc1, tid);
+        wsplit<true>(P + pk.W2, MP, 32, S3, L::WIMG2, sc3, tid);
+        const float* src = MODE == FVP ? a.V : P;   // FVP: dW1r / dW2r;  FWD: W1r / W2r
+        wsplit<false>(src + pk.W1, H, H, S2, L::WIMG, sc2, tid);
+        wsplit<false>(src + pk.W2, MP, 32, S4, L::WIMG2, sc4v, tid);
+    }
+    constexpr int KS = KH / 32;   // k32 steps per observation half
+    half8 wh[KS], wl[KS];
+    float wsc;
+    {
+        float8v v[KS];
+        float mx = 0.f;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            v[s] = load8(W0src + (cb * 16 + r16) * NP + kh * KH + 32 * s + 8 * q);
+            mx = fmaxf(mx, absmax8(v[s]));
+        }
+        const float sc = pow2_scale(max_over_groups(mx), wsc);
+#pragma unroll
+        for (int s = 0; s < KS; ++s) split8(v[s], sc, wh[s], wl[s]);
+    }
+
+    floatx4 g0[KG];
+#pragma unroll
+    for (int g = 0; g < KG; ++g) g0[g] = zero4();
+    floatx4 g1[2] = {zero4(), zero4()};   // gW1 blocks (jb = cb, kb = kh + 2j)
+    floatx4 g2 = zero4();                 // gW2 block (jb = w >> 2 < MP/16, kb = w & 3)
+    float b1acc = 0.f, b2acc = 0.f;
+    double racc0 = 0.0, racc1 = 0.0;
+    const float sls = MODE == FVP ? 0.f : ls_sum(P + pk.ls, m);
+
+    const float* BV = MODE == FVP ? a.V : P;
+    const float bias1 = BV[pk.b1 + cb * 16 + r16];
+    const int cbo3 = w & (MP / 16 - 1), rb3 = w / (MP / 16);   // P3: waves < 2 * MP/16
+    const int col3 = cbo3 * 16 + r16;
+    const float bias3 = BV[pk.b2 + col3];
+    const float os3 = a.out_scale ? (col3 < m ? a.out_scale[col3] : 1.f) : 1.f;
+    const float osh3 = a.out_shift ? (col3 < m ? a.out_shift[col3] : 0.f) : 0.f;
+    float wq3 = 0.f;
+    if (MODE == FVP) {
+        const float sg = expf(P[pk.ls + col3]);
+        wq3 = os3 * os3 * (2.f / (2.f * sg * sg + 1e-8f));
+    }
+
+    float touch[2] = {0.f, 0.f};
+    // the xhat tile is software-pipelined through registers: tile t+1's pieces are
+    // loaded at the start of tile t's weight-gradient phase and stored to the
+    // images at the top of the next iteration (16 threads per row, piece c = tid %
+    // 16 + 16 u: u < NP/128 hi chunks, the rest lo chunks)
+    float4 xn[L::XPER];
+    float un = 1.f;
+    auto xload = [&](int64_t t_, int tid_) {
+        const int64_t rb_ = t_ * BT;
+        const int row = tid_ >> 4, c16 = tid_ & 15;
+        const bool ok = t_ < ntiles && rb_ + row < T;
+        const char* src = reinterpret_cast<const char*>(a.xs) + (ok ? (rb_ + row) * (4 * NP) : 0);
+#pragma unroll
+        for (int u = 0; u < L::XPER; ++u)
+            xn[u] = ok ? *reinterpret_cast<const float4*>(src + 16 * (c16 + 16 * u)) : make_float4(0.f, 0.f, 0.f, 0.f);
+        un = (tid_ < BT && t_ < ntiles && rb_ + tid_ < T) ? a.xu[rb_ + tid_] : 1.f;
+    };
+    xload(blockIdx.x, tid);
+    __syncthreads();   // images and scales ready
+#ifdef MJRL_KX_PROF
+    unsigned long long kx_acc_[16] = {0};
+    unsigned long long kx_last_ = __builtin_amdgcn_s_memtime();
+#endif
+
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        KX_STAMP(9);   // loop top (the wait on the previous tile's last barrier)
+        // per-lane indices through an opaque zero: recomputed per tile rather than
+        // hoisted into live registers (see ks.h)
+        int opq = 0;
+        asm volatile("" : "+v"(opq));
+        const int ltid = tid + opq, lr16 = r16 + opq, lq = q + opq;
+        const int64_t row_base = tile * BT;
+        const int nrow = (int)(T - row_base < BT ? T - row_base : BT);
+
+        // ---- publish: xhat tile -> images, row scales; FVP: cached activations ----
+        asm volatile("" ::"v"(touch[0]), "v"(touch[1]));
+        {
+            const int row = ltid >> 4, c16 = ltid & 15;
+            char* dst = XHb + row * L::RBYTES + 16 * (c16 ^ chunk_swz(row));
+#pragma unroll
+            for (int u = 0; u < L::XPER; ++u) {
+                constexpr int UH = NP / 128;
+                *reinterpret_cast<float4*>(dst + (u / UH) * (BT * L::RBYTES) + 256 * (u % UH)) = xn[u];
+            }
+            if (ltid < BT) Us[ltid] = un;
+        }
+        float pa0[4], pa1[4];   // FVP: cached a0 / a1 at (rows kh*16 + 4q + rr, unit cb*16 + r)
+        if (MODE == FVP) {
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int row = kh * 16 + 4 * lq + rr;
+                pa0[rr] = row < nrow ? a.a0[(row_base + row) * H + cb * 16 + lr16] : 0.f;
+                pa1[rr] = row < nrow ? a.a1[(row_base + row) * H + cb * 16 + lr16] : 0.f;
+            }
+        }
+        __syncthreads();
+        KX_STAMP(0);
+        // pull the next tile's other per-row inputs into L2: one dword per 128-byte
+        // line (FVP the a0 / a1 caches; FWD / EVAL actions, advantages and the old
+        // means / log-likelihoods), kept alive in 2 VGPRs until the next publish
+        {
+            const int64_t nt = tile + gridDim.x;
+            if (nt < ntiles) {
+                const int64_t nb = nt * BT;
+                const int nr = (int)(T - nb < BT ? T - nb : BT);
+                const int mline = (BT * m * 4 + 127) / 128;   // lines of a [BT][m] f32 slab
+                const int idx = ltid;
+                const float* p = nullptr;
+                if (MODE == FVP) {
+                    if (idx < 4 * BT && (idx & 63) / 2 < nr)
+                        p = (idx < 2 * BT ? a.a0 : a.a1) + (nb + (idx & 63) / 2) * H + (idx & 1) * 32;
+                } else {
+                    const int ne = nr * m;
+                    if (idx < mline) {
+                        if (32 * idx < ne) p = a.act + nb * m + 32 * idx;
+                    } else if (MODE == EVAL && idx < 2 * mline) {
+                        if (32 * (idx - mline) < ne) p = a.mu0 + nb * m + 32 * (idx - mline);
+                    } else if (idx == 2 * mline) {
+                        p = (MODE == FWD ? a.adv_vpg : a.adv) + nb;
+                    } else if (MODE == EVAL && idx == 2 * mline + 1) {
+                        p = a.ll0 + nb;
+                    }
+                }
+                if (p) touch[0] = *p;
+            }
+        }
+        if (MODE == EVAL) xload(tile + gridDim.x, ltid);   // EVAL has no weight-gradient phase
+
+        // ---- P1: first layer, partial over this wave's observation half ----
+        floatx4 acc1[2] = {zero4(), zero4()};
+        {
+            const int swz1 = chunk_swz(lr16);
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                const int ch = kh * (KH / 8) + 4 * s + lq;
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const int off = (i * 16 + lr16) * L::RBYTES + 16 * (ch ^ swz1);
+                    const half8 xh = *reinterpret_cast<const half8*>(XHb + off);
+                    const half8 xl = *reinterpret_cast<const half8*>(XLb + off);
+                    acc1[i] = mfma_x3(xh, xl, wh[s], wl[s], acc1[i]);
+                }
+                if (s & 1) __builtin_amdgcn_sched_barrier(0);
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) acc1[i][rr] *= Us[i * 16 + 4 * lq + rr] * wsc;
+        }
+        // fold the observation halves: wave (cb, kh) hands its partial of row block
+        // 1 - kh to its partner and finishes row block kh
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+            D0[((1 - kh) * 16 + 4 * lq + rr) * L::LD + cb * 16 + lr16] = kh ? acc1[0][rr] : acc1[1][rr];
+        __syncthreads();
+        KX_STAMP(1);
+        {
+            const int col = cb * 16 + lr16;
+            float av[4], dv[4];
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int row = kh * 16 + 4 * lq + rr;
+                const float v = (kh ? acc1[1][rr] : acc1[0][rr]) + D0[row * L::LD + col];
+                if (MODE == FVP) {
+                    av[rr] = pa0[rr];
+                    dv[rr] = (1.f - av[rr] * av[rr]) * v;
+                } else {
+                    av[rr] = tanhf(v);
+                    if (MODE == FWD && row < nrow) a.a0[(row_base + row) * H + col] = av[rr];
+                }
+            }
+            if (MODE == FVP) {
+                // the partner reads our block-(1 - kh) slots only; ours are free to overwrite
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) D0[(kh * 16 + 4 * lq + rr) * L::LD + col] = dv[rr];
+            }
+            astore4(A0i, col, kh * 16 + 4 * lq, av);
+        }
+        __syncthreads();
+        KX_STAMP(2);
+
+        // ---- P2: layer 1, wave -> (rb = kh, cb) ----
+        {
+            const int j = cb * 16 + lr16;
+            floatx4 acc = zero4();
+            float rinv = 1.f;
+            if (MODE == FVP) {
+                // D0 W1^T (W1c, column scale folded into D0) + a0 dW1^T (dW1r)
+                half8 ah[2], al[2];
+                rinv = adyn<2>(D0, L::LD, kh, lq, lr16, sc1, ah, al);
+                floatx4 accb = zero4();
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    half8 bh, bl, xh, xl;
+                    wrow(S1, L::WIMG, j, s, lq, bh, bl);
+                    acc = mfma_x3(ah[s], al[s], bh, bl, acc);
+                    arow(A0i, kh, s, lq, lr16, xh, xl);
+                    wrow(S2, L::WIMG, j, s, lq, bh, bl);
+                    accb = mfma_x3(xh, xl, bh, bl, accb);
+                }
+                const float dsc = sc2[j];
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) acc[rr] = acc[rr] * __shfl(rinv, 4 * lq + rr, 64) + accb[rr] * dsc;
+            } else {
+                // a0 W1^T (W1r: FWD slot 2, EVAL slot 1)
+                const char* img = MODE == FWD ? S2 : S1;
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    half8 bh, bl, xh, xl;
+                    arow(A0i, kh, s, lq, lr16, xh, xl);
+                    wrow(img, L::WIMG, j, s, lq, bh, bl);
+                    acc = mfma_x3(xh, xl, bh, bl, acc);
+                }
+                const float rsc = (MODE == FWD ? sc2 : sc1)[j];
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) acc[rr] *= rsc;
+            }
+            float av[4];
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int row = kh * 16 + 4 * lq + rr;
+                const float v = acc[rr] + bias1;
+                if (MODE == FVP) {
+                    av[rr] = pa1[rr];
+                    D1[row * L::LD + j] = (1.f - av[rr] * av[rr]) * v;
+                } else {
+                    av[rr] = tanhf(v);
+                    if (MODE == FWD && row < nrow) a.a1[(row_base + row) * H + j] = av[rr];
+                }
+            }
+            astore4(A1i, j, kh * 16 + 4 * lq, av);
+        }
+        __syncthreads();
+        KX_STAMP(3);
+
+        // ---- P3: output layer [32 x MP], waves < 2 * MP/16 -> (rb3, cbo3) ----
+        if (w < 2 * (MP / 16)) {
+            floatx4 acc = zero4();
+            if (MODE == FVP) {
+                // D1 W2^T (W2c, folded) + a1 dW2^T (dW2r)
+                half8 ah[2], al[2];
+                const float rinv = adyn<2>(D1, L::LD, rb3, lq, lr16, sc3, ah, al);
+                floatx4 accb = zero4();
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    half8 bh, bl, xh, xl;
+                    wrow(S3, L::WIMG2, col3, s, lq, bh, bl);
+                    acc = mfma_x3(ah[s], al[s], bh, bl, acc);
+                    arow(A1i, rb3, s, lq, lr16, xh, xl);
+                    wrow(S4, L::WIMG2, col3, s, lq, bh, bl);
+                    accb = mfma_x3(xh, xl, bh, bl, accb);
+                }
+                const float dsc = sc4v[col3];
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) acc[rr] = acc[rr] * __shfl(rinv, 4 * lq + rr, 64) + accb[rr] * dsc;
+            } else {
+                const char* img = MODE == FWD ? S4 : S3;
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    half8 bh, bl, xh, xl;
+                    arow(A1i, rb3, s, lq, lr16, xh, xl);
+                    wrow(img, L::WIMG2, col3, s, lq, bh, bl);
+                    acc = mfma_x3(xh, xl, bh, bl, acc);
+                }
+                const float rsc = (MODE == FWD ? sc4v : sc3)[col3];
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) acc[rr] *= rsc;
+            }
+            float gv[4];
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int row = rb3 * 16 + 4 * lq + rr;
+                const float v = acc[rr] + bias3;
+                if (MODE == FVP)
+                    gv[rr] = (col3 < m && row < nrow) ? wq3 * v : 0.f;
+                else
+                    gv[rr] = col3 < m ? v * os3 + osh3 : 0.f;
+                GPf[row * L::LDG + col3] = gv[rr];
+            }
+            if (MODE == FVP)
+                *reinterpret_cast<float4*>(GPT + col3 * L::LDT + rb3 * 16 + 4 * lq) =
+                    make_float4(gv[0], gv[1], gv[2], gv[3]);
+        }
+        if (MP == 16) {   // the padded k16..31 of the P4 operand
+            for (int i = ltid; i < BT * 16; i += KT) GPf[(i >> 4) * L::LDG + 16 + (i & 15)] = 0.f;
+        }
+        __syncthreads();
+        KX_STAMP(4);
+
+        if (MODE != FVP) {
+            // per-row pass: FWD log-lik / caches / VPG upstream; EVAL LR and KL
+            row_pass<MODE, BT, MP, KT, false>(a, P + pk.ls, sls, row_base, GPf, L::LDG, racc0, racc1, ltid);
+            __syncthreads();
+        KX_STAMP(5);
+            if (MODE == EVAL) continue;
+            for (int i = ltid; i < BT * MP; i += KT) {   // GPT for the gW2 sums
+                const int row = i / MP, jj = i % MP;
+                GPT[jj * L::LDT + row] = GPf[row * L::LDG + jj];
+            }
+        }
+        if (MODE == EVAL) continue;
+
+        // ---- P4: gu1 = (1 - a1^2) (gp W2), wave -> (rb = kh, cb) ----
+        {
+            const int hcol = cb * 16 + lr16;
+            half8 ah[1], al[1];
+            const float rinv = adyn<1>(GPf, L::LDG, kh, lq, lr16, nullptr, ah, al);
+            half8 bh, bl;
+            wcol(S3, L::WIMG2, cb, 0, lq, lr16, bh, bl);
+            const floatx4 acc = mfma_x3(ah[0], al[0], bh, bl, zero4());
+            const float csc = sc3[hcol];
+            float gv[4];
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int row = kh * 16 + 4 * lq + rr;
+                const float av = MODE == FVP ? pa1[rr] : aval(A1i, hcol, row);
+                gv[rr] = (1.f - av * av) * (acc[rr] * __shfl(rinv, 4 * lq + rr, 64) * csc);
+                D0[row * L::LD + hcol] = gv[rr];   // G1
+            }
+            *reinterpret_cast<float4*>(G1T + hcol * L::LDT + kh * 16 + 4 * lq) = make_float4(gv[0], gv[1], gv[2], gv[3]);
+        }
+        __syncthreads();
+        KX_STAMP(6);
+        // ---- P5: gu0 = (1 - a0^2) (gu1 W1), times the xhat row scale ----
+        {
+            const int hcol = cb * 16 + lr16;
+            half8 ah[2], al[2];
+            const float rinv = adyn<2>(D0, L::LD, kh, lq, lr16, nullptr, ah, al);
+            floatx4 acc = zero4();
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                half8 bh, bl;
+                wcol(S1, L::WIMG, cb, s, lq, lr16, bh, bl);
+                acc = mfma_x3(ah[s], al[s], bh, bl, acc);
+            }
+            const float csc = sc1[hcol];
+            float gv[4];
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int row = kh * 16 + 4 * lq + rr;
+                const float av = aval(A0i, hcol, row);
+                gv[rr] = (1.f - av * av) * (acc[rr] * __shfl(rinv, 4 * lq + rr, 64) * csc) * Us[row];
+            }
+            *reinterpret_cast<float4*>(D1 + hcol * L::LDT + kh * 16 + 4 * lq) = make_float4(gv[0], gv[1], gv[2], gv[3]);
+        }
+        __syncthreads();
+        KX_STAMP(7);
+
+        // ---- P6: weight-gradient sums ----
+        xload(tile + gridDim.x, ltid);   // next tile's xhat, consumed at the next publish
+        KX_STAMP(10);
+        {
+            // gW0 (xhat transposed reads), gW1 (a0 image), gW2 (a1 image)
+            half8 gh, gl;
+            float s4[4];
+            gdyn(D1, L::LDT, cb, lq, lr16, gh, gl, s4);   // G0T
+            KX_STAMP(11);
+            const int tq = lr16 >> 2, tp = lr16 & 3;
+            const int cl = (kh * KH) / 8 + (tp >> 1);
+#pragma unroll
+            for (int g = 0; g < KG; ++g) {
+                const int c0 = cl + 2 * g;
+                short4v th[2], tl[2];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int row = 8 * lq + 4 * h + tq;
+                    const int off = row * L::RBYTES + 16 * (c0 ^ chunk_swz(row)) + 8 * (tp & 1);
+                    th[h] = ds_read_tr16(XHb + off);
+                    tl[h] = ds_read_tr16(XLb + off);
+                }
+                const floatx4 t = mfma_x3(gh, gl, cat_tr(th[0], th[1]), cat_tr(tl[0], tl[1]), zero4());
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) g0[g][rr] += t[rr] * s4[rr];
+                if (g & 1) __builtin_amdgcn_sched_barrier(0);
+            }
+            KX_STAMP(12);
+            // gW1[jb = cb][kb = kh + 2jj] += gu1^T a0;  gb1 = row sums of gu1 (waves kh = 0)
+            {
+                const float8v v = load8(G1T + (cb * 16 + lr16) * L::LDT + 8 * lq);
+                float inv;
+                const float sc = pow2_scale(max_over_groups(absmax8(v)), inv);
+                split8(v, sc, gh, gl);
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) s4[rr] = __shfl(inv, 4 * lq + rr, 64);
+                if (kh == 0) {
+                    float t = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+                    t += __shfl_xor(t, 16, 64);
+                    t += __shfl_xor(t, 32, 64);
+                    b1acc += t;
+                }
+            }
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj) {
+                half8 bh, bl;
+                acol(A0i, (kh + 2 * jj) * 16 + lr16, lq, bh, bl);
+                const floatx4 t = mfma_x3(gh, gl, bh, bl, zero4());
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) g1[jj][rr] += t[rr] * s4[rr];
+            }
+            KX_STAMP(13);
+            // gW2[jb = w >> 2][kb = w & 3] += gp^T a1;  gb2 = row sums of gp (waves kb = 0)
+            if ((w >> 2) < MP / 16) {
+                const float8v v = load8(GPT + ((w >> 2) * 16 + lr16) * L::LDT + 8 * lq);
+                float inv;
+                const float sc = pow2_scale(max_over_groups(absmax8(v)), inv);
+                split8(v, sc, gh, gl);
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) s4[rr] = __shfl(inv, 4 * lq + rr, 64);
+                if ((w & 3) == 0) {
+                    float t = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+                    t += __shfl_xor(t, 16, 64);
+                    t += __shfl_xor(t, 32, 64);
+                    b2acc += t;
+                }
+                half8 bh, bl;
+                acol(A1i, (w & 3) * 16 + lr16, lq, bh, bl);
+                const floatx4 t = mfma_x3(gh, gl, bh, bl, zero4());
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) g2[rr] += t[rr] * s4[rr];
+            }
+        }
+        KX_STAMP(14);
+        __syncthreads();
+        KX_STAMP(8);
+    }
+
+    const int64_t blk = blockIdx.x;
+    if constexpr (GRAD) {
+#pragma unroll
+        for (int g = 0; g < KG; ++g)
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int n = cb * 16 + 4 * q + rr;
+                const int k = kh * KH + 16 * g + r16;
+                o.wpart[o.off0 + (blk * H + n) * NP + k] = g0[g][rr];
+            }
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int n = cb * 16 + 4 * q + rr;
+                const int k = (kh + 2 * j) * 16 + r16;
+                o.wpart[o.off1 + (blk * H + n) * H + k] = g1[j][rr];
+            }
+        if ((w >> 2) < MP / 16) {
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int n = (w >> 2) * 16 + 4 * q + rr;
+                const int k = (w & 3) * 16 + r16;
+                o.wpart[o.off2 + (blk * MP + n) * H + k] = g2[rr];
+            }
+        }
+        if (kh == 0 && q == 0) o.wpart[o.boff1 + blk * H + cb * 16 + r16] = b1acc;
+        if ((w >> 2) < MP / 16 && (w & 3) == 0 && q == 0) o.wpart[o.boff2 + blk * MP + (w >> 2) * 16 + r16] = b2acc;
+    }
+    if (MODE != FVP) {
+        __syncthreads();
+        row_pass_final<MODE, MP, KT>(racc0, racc1, reinterpret_cast<double*>(smem), a.rpart, blk, tid);
+    }
+#ifdef MJRL_KX_PROF
+    if (blockIdx.x == 0 && tid == 0)
+        for (int i = 0; i < 16; ++i) g_kx_prof[i] += kx_acc_[i];
+#endif
+}
+
+}  // namespace

@@ -14,6 +14,7 @@
 // Reference math: mjrl/policies/gaussian_mlp.py:100-182, gaussian_linear.py:98-175,
 // mjrl/algos/batch_reinforce.py:37-55, mjrl/algos/npg_cg.py:55-74.
 #include <math.h>
+#include <stdlib.h>
 
 #include "common.h"
 
@@ -587,10 +588,12 @@ struct GArgs {
     const int32_t* done;
 };
 
-// Block = 8 waves over 64 consecutive flat parameters: lane -> parameter, wave w
-// sums its contiguous share of the slices in order, and wave 0 adds the eight
-// wave partials in order (deterministic, fp64).
-constexpr int GATHER_WAVES = 8;
+// Block = 16 waves over 64 consecutive flat parameters: lane -> parameter, wave w
+// loads its contiguous share of the slices (all loads in flight at once) and sums
+// them in slice order; wave 0 adds the sixteen wave partials in order
+// (deterministic, fp64).
+constexpr int GATHER_WAVES = 16;
+constexpr int GATHER_PER = 16;   // slices per wave per batch (S <= 256: one batch)
 
 __global__ void __launch_bounds__(64 * GATHER_WAVES) k_gather(GArgs a) {
     if (a.done && *a.done) return;
@@ -640,15 +643,13 @@ __global__ void __launch_bounds__(64 * GATHER_WAVES) k_gather(GArgs a) {
         const int per = (a.S + GATHER_WAVES - 1) / GATHER_WAVES;
         const int s0 = w * per, s1 = min(a.S, s0 + per);
         const float* p = a.wpart + src;
-        int s = s0;
-        for (; s + 8 <= s1; s += 8) {
-            float v[8];
+        for (int sb = s0; sb < s1; sb += GATHER_PER) {
+            float v[GATHER_PER];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = p[(int64_t)(s + j) * stride];
+            for (int j = 0; j < GATHER_PER; ++j) v[j] = sb + j < s1 ? p[(int64_t)(sb + j) * stride] : 0.f;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) acc += (double)v[j];
+            for (int j = 0; j < GATHER_PER; ++j) acc += (double)v[j];
         }
-        for (; s < s1; ++s) acc += (double)p[(int64_t)s * stride];
     } else if (lsj >= 0 && a.lspart) {
         const int per = (a.G + GATHER_WAVES - 1) / GATHER_WAVES;
         const int b0 = w * per, b1 = min(a.G, b0 + per);
@@ -683,6 +684,7 @@ __global__ void __launch_bounds__(64) k_eval_final(const double* __restrict__ rp
 
 #include "fused.h"
 #include "ks.h"
+#include "kx.h"
 
 namespace {
 
@@ -838,10 +840,46 @@ int launch_ks_t(const RowArgs& ra, const FOut& fo, int grid, hipStream_t st) {
     return (int)hipGetLastError();
 }
 
-// rows given as split-f16 (ra.xs) run the SX kernel; f32 xhat the exact-f32 one
+template <int MP, int KG, int MODE>
+int launch_kx_t(const RowArgs& ra, const FOut& fo, int grid, hipStream_t st) {
+    using L = XLayout<MP, KG>;
+    auto fn = k_kx<MP, KG, MODE>;
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, L::bytes);
+        if (e != hipSuccess) return (int)e;
+        attr = true;
+    }
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(KT), L::bytes, st, ra, fo);
+    return (int)hipGetLastError();
+}
+
+// MJRL_AMD_SPLIT_LAYERS=1 keeps the 64-wide layers of the split path on exact f32
+// (k_ks<.., SX>: only the first layer split), for A/B measurement
+static bool first_layer_only() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("MJRL_AMD_SPLIT_LAYERS");
+        v = (e && e[0] == '1') ? 1 : 0;
+    }
+    return v == 1;
+}
+
+// rows given as split-f16 (ra.xs) run the all-split kernel k_kx (or k_ks<.., SX>);
+// f32 xhat the exact-f32 k_ks
 template <int MODE>
 int launch_ks(const mjrl_shape* s, const RowArgs& ra, const FOut& fo, int grid, hipStream_t st) {
     const int kg = s->np / 32;
+    if (ra.xs && !first_layer_only()) {
+#define MJRL_K(MP_, KG_) \
+    if (s->mp == MP_ && kg == KG_) return launch_kx_t<MP_, KG_, MODE>(ra, fo, grid, st);
+#define MJRL_KN(MP_) MJRL_K(MP_, 4) MJRL_K(MP_, 8) MJRL_K(MP_, 12)
+        MJRL_KN(16)
+        MJRL_KN(32)
+#undef MJRL_KN
+#undef MJRL_K
+        return MJRL_ESHAPE;
+    }
     if (ra.xs) {
 #define MJRL_K(MP_, KG_) \
     if (s->mp == MP_ && kg == KG_) return launch_ks_t<MP_, KG_, MODE, true>(ra, fo, grid, st);
@@ -972,6 +1010,16 @@ bool rows_ok(const mjrl_shape* s, const mjrl_rows* r) {
 }  // namespace
 
 extern "C" {
+
+#ifdef MJRL_KX_PROF
+// debug builds only: copy out and clear the k_kx phase profile (16 counters)
+int mjrl_debug_kx_prof(unsigned long long* out) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_kx_prof), sizeof(unsigned long long) * 16);
+    if (e != hipSuccess) return (int)e;
+    unsigned long long z[16] = {0};
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_kx_prof), z, sizeof(z));
+}
+#endif
 
 int mjrl_shape_init(mjrl_shape* s, int32_t n, int32_t m, int32_t h0, int32_t h1) {
     if (!s || n <= 0 || m <= 0 || h0 < 0 || h1 < 0) return MJRL_EINVAL;

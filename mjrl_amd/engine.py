@@ -158,7 +158,7 @@ class UpdateEngine:
         self.packed_new = torch.zeros(s.packed, **f32)
         self.packed_p = torch.zeros(s.packed, **f32)
         self.vec = {k: torch.zeros(s.d, **f32) for k in ("g", "gsum", "x", "r", "p", "z", "theta_new")}
-        self.cg = torch.zeros(8, **f32)
+        self.cg = torch.zeros(_lib.CG_STATE, **f32)   # MJRL_CG_STATE
         self.done = torch.zeros(1, dtype=torch.int32, device=dev)
         self.out = torch.zeros(4, **f32)
         self.stats = torch.zeros(N_STATS, dtype=torch.float64, device=dev)

@@ -19,7 +19,7 @@ def cg_solve(f_Ax, b, x_0=None, cg_iters=10, residual_tol=1e-10):
     b32 = torch.from_numpy(np.ascontiguousarray(b, dtype=np.float32)).to(dev)
     d = int(b32.numel())
     x, r, p, z = (torch.empty(d, dtype=torch.float32, device=dev) for _ in range(4))
-    cg = torch.zeros(8, dtype=torch.float32, device=dev)
+    cg = torch.zeros(_lib.CG_STATE, dtype=torch.float32, device=dev)   # MJRL_CG_STATE
     done = torch.zeros(1, dtype=torch.int32, device=dev)
     _lib.check(L.mjrl_cg_init_vec(d, _lib.ptr(b32), _lib.ptr(x), _lib.ptr(r), _lib.ptr(p), _lib.ptr(cg),
                                   _lib.ptr(done), st), "mjrl_cg_init_vec")

@@ -204,6 +204,9 @@ def main():
     ap.add_argument("--cpu-rows", type=int, default=200000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end-from-host-paths measurement")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only to rehearse the N > 1 "
+                         "path with several ranks on one GPU)")
     ap.add_argument("--precision", default=None, choices=["auto", "split", "f32"],
                     help="first-layer MFMA form (UpdateEngine precision; default: split where supported)")
     args = ap.parse_args()
@@ -211,12 +214,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    ndev = max(torch.cuda.device_count(), 1)
+    dev_idx = local % ndev if args.backend == "gloo" else local
+    torch.cuda.set_device(dev_idx)
+    device = torch.device("cuda", dev_idx)
     comm = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=device)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group("gloo")
         from mjrl_amd.comm import DistComm
         comm = DistComm()
     from mjrl_amd.comm import partition_paths

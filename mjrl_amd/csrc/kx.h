@@ -683,34 +683,40 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
         KX_STAMP(8);
     }
 
+    // slabs in the flat, parameter-chunk-major layout wpart[f / 64][S][64] (f = the
+    // reference's flat parameter index, S = gridDim.x): k_gather_flat then reads
+    // every chunk as one contiguous run
     const int64_t blk = blockIdx.x;
     if constexpr (GRAD) {
+        const int n = o.n, mm = o.m;
+        const int64_t S = gridDim.x;
+        auto put = [&](int f, float v) { o.wpart[(((int64_t)(f >> 6)) * S + blk) * 64 + (f & 63)] = v; };
+        const int fb0 = H * n, fW1 = fb0 + H, fb1 = fW1 + H * H, fW2 = fb1 + H, fb2 = fW2 + mm * H;
 #pragma unroll
         for (int g = 0; g < KG; ++g)
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr) {
-                const int n = cb * 16 + 4 * q + rr;
+                const int hid = cb * 16 + 4 * q + rr;
                 const int k = kh * KH + 16 * g + r16;
-                o.wpart[o.off0 + (blk * H + n) * NP + k] = g0[g][rr];
+                if (k < n)
+                    put(hid * n + k, g0[g][rr]);
+                else if (k == n)
+                    put(fb0 + hid, g0[g][rr]);   // b0 rides in the bias column
             }
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int rr = 0; rr < 4; ++rr) {
-                const int n = cb * 16 + 4 * q + rr;
-                const int k = (kh + 2 * j) * 16 + r16;
-                o.wpart[o.off1 + (blk * H + n) * H + k] = g1[j][rr];
-            }
+            for (int rr = 0; rr < 4; ++rr) put(fW1 + (cb * 16 + 4 * q + rr) * H + (kh + 2 * j) * 16 + r16, g1[j][rr]);
         if ((w >> 2) < MP / 16) {
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr) {
-                const int n = (w >> 2) * 16 + 4 * q + rr;
-                const int k = (w & 3) * 16 + r16;
-                o.wpart[o.off2 + (blk * MP + n) * H + k] = g2[rr];
+                const int j = (w >> 2) * 16 + 4 * q + rr;
+                if (j < mm) put(fW2 + j * H + (w & 3) * 16 + r16, g2[rr]);
             }
         }
-        if (kh == 0 && q == 0) o.wpart[o.boff1 + blk * H + cb * 16 + r16] = b1acc;
-        if ((w >> 2) < MP / 16 && (w & 3) == 0 && q == 0) o.wpart[o.boff2 + blk * MP + (w >> 2) * 16 + r16] = b2acc;
+        if (kh == 0 && q == 0) put(fb1 + cb * 16 + r16, b1acc);
+        if ((w >> 2) < MP / 16 && (w & 3) == 0 && q == 0 && (w >> 2) * 16 + r16 < mm)
+            put(fb2 + (w >> 2) * 16 + r16, b2acc);
     }
     if (MODE != FVP) {
         __syncthreads();

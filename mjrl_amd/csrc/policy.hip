@@ -665,6 +665,45 @@ __global__ void __launch_bounds__(64 * GATHER_WAVES) k_gather(GArgs a) {
     }
 }
 
+// Gather of the flat slab layout of k_kx: block c folds wpart[c][0..S)[64] — one
+// contiguous run — for flat parameters 64c..64c+63 (waves take 16 slices each,
+// loads all in flight, fixed-order fp64 sums); log-std entries (FWD) from lspart.
+__global__ void __launch_bounds__(64 * GATHER_WAVES) k_gather_flat(const float* __restrict__ wpart, int S, int d_mu,
+                                                                   int d, const double* __restrict__ lspart, int G,
+                                                                   int mp, float* __restrict__ gsum,
+                                                                   const int32_t* __restrict__ done) {
+    if (done && *done) return;
+    __shared__ double part[GATHER_WAVES][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int f = blockIdx.x * 64 + lane;
+    double acc = 0.0;
+    if (f < d_mu) {
+        const int per = (S + GATHER_WAVES - 1) / GATHER_WAVES;
+        const int s0 = w * per, s1 = min(S, s0 + per);
+        const float* p = wpart + (int64_t)blockIdx.x * S * 64 + lane;
+        for (int sb = s0; sb < s1; sb += GATHER_PER) {
+            float v[GATHER_PER];
+#pragma unroll
+            for (int j = 0; j < GATHER_PER; ++j) v[j] = sb + j < s1 ? p[(int64_t)(sb + j) * 64] : 0.f;
+#pragma unroll
+            for (int j = 0; j < GATHER_PER; ++j) acc += (double)v[j];
+        }
+    } else if (f < d && lspart) {
+        const int lsj = f - d_mu;
+        const int per = (G + GATHER_WAVES - 1) / GATHER_WAVES;
+        const int b0 = w * per, b1 = min(G, b0 + per);
+        for (int b = b0; b < b1; ++b) acc += lspart[(int64_t)b * mp + lsj];
+    }
+    part[w][lane] = acc;
+    __syncthreads();
+    if (w == 0 && f < d) {
+        double t = part[0][lane];
+#pragma unroll
+        for (int j = 1; j < GATHER_WAVES; ++j) t += part[j][lane];
+        gsum[f] = (float)t;
+    }
+}
+
 __global__ void __launch_bounds__(64) k_eval_final(const double* __restrict__ rpart, int G, double* __restrict__ sums) {
     // one wave: lane l folds partials l, l+64, ... in order, then a fixed shuffle tree
     double s = 0.0, k = 0.0;
@@ -942,6 +981,8 @@ int run_fused(int mode, const mjrl_shape* s, const mjrl_rows* r, int64_t T, cons
     fo.boff1 = js.job[1].boff;
     fo.off2 = js.job[2].off;
     fo.boff2 = js.job[2].boff;
+    fo.n = s->n;
+    fo.m = s->m;
     if (ks) {
         if (mode == FWD) return launch_ks<FWD>(s, ra, fo, G, st);
         return launch_ks<FVP>(s, ra, fo, G, st);
@@ -952,6 +993,12 @@ int run_fused(int mode, const mjrl_shape* s, const mjrl_rows* r, int64_t T, cons
 int run_gather(const mjrl_shape* s, const mjrl_rows* r, int64_t T, const mjrl_scratch* sc, const double* lspart,
                const int32_t* done, float* gsum, hipStream_t st) {
     const int S = grad_slices(s, T);
+    if (acc_path(s, T) == 2 && r->xs && !first_layer_only()) {   // k_kx: flat slab layout
+        const int d_mu = s->d - s->m;
+        hipLaunchKernelGGL(k_gather_flat, dim3((s->d + 63) / 64), dim3(64 * GATHER_WAVES), 0, st, sc->wpart, S, d_mu,
+                           s->d, lspart, ks_grid(T), s->mp, gsum, done);
+        return (int)hipGetLastError();
+    }
     JobSet js = make_jobs(s, r, S);
     GArgs ga{};
     ga.n = s->n; ga.m = s->m; ga.h0 = s->h0; ga.h1 = s->h1; ga.np = s->np; ga.mp = s->mp; ga.d = s->d; ga.S = S;

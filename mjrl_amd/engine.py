@@ -252,12 +252,25 @@ class UpdateEngine:
     def _stat(self, slot, n=3):
         return self.stats[slot:slot + n]
 
-    def _moments(self, x, N, out_slot, center_slot=None, f32=False):
+    def _moments(self, x, N, out_slot, center_slot=None, f32=False, reduce=True):
         fn = self.lib.mjrl_moments_f32 if f32 else self.lib.mjrl_moments
         center = None if center_slot is None else C.c_void_p(self.stats[center_slot:].data_ptr())
         _lib.check(fn(_lib.ptr(x), N, center, _lib.ptr(self.mom_part),
                       C.c_void_p(self.stats[out_slot:].data_ptr()), self.st), "mjrl_moments")
-        self.comm.allreduce_sum(self._stat(out_slot))
+        if reduce:
+            self.comm.allreduce_sum(self._stat(out_slot))
+
+    def _allreduce_slots(self, slots):
+        """One SUM all-reduce over several (start, length) slices of the stats buffer
+        (gathered into one small tensor): fewer latency-bound collectives per update."""
+        if self.comm.world_size <= 1:
+            return
+        buf = torch.cat([self.stats[a:a + n] for a, n in slots])
+        self.comm.allreduce_sum(buf)
+        o = 0
+        for a, n in slots:
+            self.stats[a:a + n].copy_(buf[o:o + n])
+            o += n
 
     def _pack(self, obs, act, T, st):
         """a5 batch assembly: f64 obs / act -> the row format the policy passes read."""
@@ -345,19 +358,24 @@ class UpdateEngine:
         else:
             self.returns_advantages(batch, gamma, gae_lambda)
             adv64 = w["adv64"]
-        # whitening (npg_cg.py:91), two-pass fp64 moments, all-reduced when sharded
-        self._moments(adv64, T, S_M1)
-        self._moments(adv64, T, S_M2, center_slot=S_M1)
+        # whitening (npg_cg.py:91) and path-return statistics (npg_cg.py:97-102):
+        # two-pass fp64 moments; when sharded, each pass's sums of both quantities
+        # share one all-reduce (plus one MAX for the path-return extrema)
+        self._moments(adv64, T, S_M1, reduce=False)
+        self._moments(w["path_ret"], P, S_PM1, reduce=False)
+        self._allreduce_slots([(S_M1, 3), (S_PM1, 3)])
+        self.comm.allreduce_max(self.stats[S_PM1 + 4:S_PM1 + 6])
+        self._moments(adv64, T, S_M2, center_slot=S_M1, reduce=False)
+        self._moments(w["path_ret"], P, S_PM2, center_slot=S_PM1, reduce=False)
+        self._allreduce_slots([(S_M2, 3), (S_PM2, 3)])
         dapg = algo == "dapg" and demo_coef is not None
         _lib.check(L.mjrl_whiten(_lib.ptr(adv64), T, C.c_void_p(self.stats[S_M1:].data_ptr()),
                                  C.c_void_p(self.stats[S_M2:].data_ptr()), 1e-6, _lib.ptr(w["adv32"]),
                                  _lib.ptr(w["w64"]) if dapg else None, st), "mjrl_whiten")
-        # surr_before = mean(LR * adv) with LR == 1 (npg_cg.py:113)
-        self._moments(w["adv32"], T, S_MS, f32=True)
-        # path-return statistics (npg_cg.py:97-102)
-        self._moments(w["path_ret"], P, S_PM1)
-        self.comm.allreduce_max(self.stats[S_PM1 + 4:S_PM1 + 6])
-        self._moments(w["path_ret"], P, S_PM2, center_slot=S_PM1)
+        # surr_before = mean(LR * adv) with LR == 1 (npg_cg.py:113); its all-reduce rides
+        # with the first post-step evaluation's
+        self._moments(w["adv32"], T, S_MS, f32=True, reduce=False)
+        ms_pending = [True]
         if dapg:
             self._moments(w["w64"], T, S_MW1)
             self._moments(w["w64"], T, S_MW2, center_slot=S_MW1)
@@ -434,7 +452,11 @@ class UpdateEngine:
                                           _lib.ptr(self.packed_theta), _lib.ptr(osh), _lib.ptr(osc),
                                           C.byref(sc_fvp), C.c_void_p(self.stats[S_EVAL:].data_ptr()), st),
                        "mjrl_policy_eval")
-            self.comm.allreduce_sum(self.stats[S_EVAL:S_EVAL + 2])
+            if ms_pending[0]:
+                self._allreduce_slots([(S_MS, 3), (S_EVAL, 2)])
+                ms_pending[0] = False
+            else:
+                self._allreduce_slots([(S_EVAL, 2)])
 
         trials = []
         if algo == "vpg":

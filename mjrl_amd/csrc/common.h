@@ -97,10 +97,23 @@ __device__ __forceinline__ float absmax8(const float8v& v) {
     return m;
 }
 
-// max over the four 16-lane groups (lanes l, l^16, l^32, l^48)
+// Exchange across 16-lane groups with the gfx950 lane-swap VALU ops (no LDS
+// round trip): permlane16_swap(x, x) gives every lane {x[l], x[l ^ 16]} in
+// (lower group, upper group) order, permlane32_swap(x, x) {x[l], x[l ^ 32]}
+// likewise (checked by tools/permlane_check.hip).
 __device__ __forceinline__ float max_over_groups(float v) {
-    v = fmaxf(v, __shfl_xor(v, 16, 64));
-    return fmaxf(v, __shfl_xor(v, 32, 64));
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+
+// sum over the four 16-lane groups, the same fixed order in every lane
+__device__ __forceinline__ float sum_over_groups(float v) {
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
 // gfx950 ds_read_b64_tr_b16: per 16-lane group, lane 4r+p addresses row r,

@@ -71,7 +71,8 @@ struct XLayout {
     static constexpr int oG1T = oGPT + 32 * LDT * 4; // f32 [H][LDT]
     static constexpr int oA0 = oG1T + H * LDT * 4;   // a0 image hi, lo
     static constexpr int oA1 = oA0 + 2 * AIMG;       // a1 image hi, lo
-    static constexpr int bytes = oA1 + 2 * AIMG;
+    static constexpr int oD0B = oA1 + 2 * AIMG;      // FVP: f32 [BT][LD] partial of observation half 1
+    static constexpr int bytes = oD0B + BT * LD * 4;
     static_assert(bytes <= 160 * 1024, "LDS");
     static_assert(bytes >= 2 * KT * 8, "row_pass_final scratch");
     static constexpr int XPER = BT * NP / 4 / KT;
@@ -229,7 +230,8 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
     float* sc3 = sc2 + 64;
     float* sc4v = sc3 + 64;
     float* Us = reinterpret_cast<float*>(sb + L::oU);
-    float* D0 = reinterpret_cast<float*>(sb + L::oD0);    // D0, then G1
+    float* D0 = reinterpret_cast<float*>(sb + L::oD0);    // D0 (FVP: half-0 partial), then G1
+    float* D0B = reinterpret_cast<float*>(sb + L::oD0B);  // FVP: half-1 partial
     float* D1 = reinterpret_cast<float*>(sb + L::oD1);    // D1, then G0T
     float* GPf = reinterpret_cast<float*>(sb + L::oGP);
     float* GPT = reinterpret_cast<float*>(sb + L::oGPT);
@@ -406,37 +408,42 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) acc1[i][rr] *= Us[i * 16 + 4 * lq + rr] * wsc;
         }
-        // fold the observation halves: wave (cb, kh) hands its partial of row block
-        // 1 - kh to its partner and finishes row block kh
+        if (MODE == FVP) {
+            // FVP: both observation-half partials go to LDS whole (kh = 0 -> D0, kh = 1 ->
+            // D0B) and P2 folds them while it loads its operand: no fold phase.  The
+            // cached activations of this wave's rows go into the a0 / a1 images.
+            float* dst = kh ? D0B : D0;
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr)
-            D0[((1 - kh) * 16 + 4 * lq + rr) * L::LD + cb * 16 + lr16] = kh ? acc1[0][rr] : acc1[1][rr];
-        __syncthreads();
-        KX_STAMP(1);
-        {
-            const int col = cb * 16 + lr16;
-            float av[4], dv[4];
+            for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int rr = 0; rr < 4; ++rr) {
-                const int row = kh * 16 + 4 * lq + rr;
-                const float v = (kh ? acc1[1][rr] : acc1[0][rr]) + D0[row * L::LD + col];
-                if (MODE == FVP) {
-                    av[rr] = pa0[rr];
-                    dv[rr] = (1.f - av[rr] * av[rr]) * v;
-                } else {
-                    av[rr] = tanhf(v);
+                for (int rr = 0; rr < 4; ++rr) dst[(i * 16 + 4 * lq + rr) * L::LD + cb * 16 + lr16] = acc1[i][rr];
+            astore4(A0i, cb * 16 + lr16, kh * 16 + 4 * lq, pa0);
+            astore4(A1i, cb * 16 + lr16, kh * 16 + 4 * lq, pa1);
+            __syncthreads();
+            KX_STAMP(1);
+            KX_STAMP(2);
+        } else {
+            // fold the observation halves: wave (cb, kh) hands its partial of row block
+            // 1 - kh to its partner and finishes row block kh
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr)
+                D0[((1 - kh) * 16 + 4 * lq + rr) * L::LD + cb * 16 + lr16] = kh ? acc1[0][rr] : acc1[1][rr];
+            __syncthreads();
+            KX_STAMP(1);
+            {
+                const int col = cb * 16 + lr16;
+                float av[4];
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    const int row = kh * 16 + 4 * lq + rr;
+                    av[rr] = tanhf((kh ? acc1[1][rr] : acc1[0][rr]) + D0[row * L::LD + col]);
                     if (MODE == FWD && row < nrow) a.a0[(row_base + row) * H + col] = av[rr];
                 }
+                astore4(A0i, col, kh * 16 + 4 * lq, av);
             }
-            if (MODE == FVP) {
-                // the partner reads our block-(1 - kh) slots only; ours are free to overwrite
-#pragma unroll
-                for (int rr = 0; rr < 4; ++rr) D0[(kh * 16 + 4 * lq + rr) * L::LD + col] = dv[rr];
-            }
-            astore4(A0i, col, kh * 16 + 4 * lq, av);
+            __syncthreads();
+            KX_STAMP(2);
         }
-        __syncthreads();
-        KX_STAMP(2);
 
         // ---- P2: layer 1, wave -> (rb = kh, cb) ----
         {
@@ -444,22 +451,37 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
             floatx4 acc = zero4();
             float rinv = 1.f;
             if (MODE == FVP) {
-                // D0 W1^T (W1c, column scale folded into D0) + a0 dW1^T (dW1r)
-                half8 ah[2], al[2];
-                rinv = adyn<2>(D0, L::LD, kh, lq, lr16, sc1, ah, al);
+                // d0 = (partial_kh0 + partial_kh1) (1 - a0^2), times the W1c column scale,
+                // scaled per row and split: d0 W1^T;  + a0 dW1^T (dW1r), a0 from the image
+                half8 xh[2], xl[2], ah[2], al[2];
+                float8v dv[2];
+                float mx = 0.f;
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    arow(A0i, kh, s, lq, lr16, xh[s], xl[s]);
+                    const int o = (kh * 16 + lr16) * L::LD + 32 * s + 8 * lq;
+                    const float8v av =
+                        __builtin_convertvector(xh[s], float8v) + __builtin_convertvector(xl[s], float8v);
+                    dv[s] = ((load8(D0 + o) + load8(D0B + o)) * (1.f - av * av)) * load8(sc1 + 32 * s + 8 * lq);
+                    mx = fmaxf(mx, absmax8(dv[s]));
+                }
+                const float sc = pow2_scale(max_over_groups(mx), rinv);
+                float ri[4];
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) ri[rr] = __shfl(rinv, 4 * lq + rr, 64);
                 floatx4 accb = zero4();
 #pragma unroll
                 for (int s = 0; s < 2; ++s) {
-                    half8 bh, bl, xh, xl;
+                    split8(dv[s], sc, ah[s], al[s]);
+                    half8 bh, bl;
                     wrow(S1, L::WIMG, j, s, lq, bh, bl);
                     acc = mfma_x3(ah[s], al[s], bh, bl, acc);
-                    arow(A0i, kh, s, lq, lr16, xh, xl);
                     wrow(S2, L::WIMG, j, s, lq, bh, bl);
-                    accb = mfma_x3(xh, xl, bh, bl, accb);
+                    accb = mfma_x3(xh[s], xl[s], bh, bl, accb);
                 }
                 const float dsc = sc2[j];
 #pragma unroll
-                for (int rr = 0; rr < 4; ++rr) acc[rr] = acc[rr] * __shfl(rinv, 4 * lq + rr, 64) + accb[rr] * dsc;
+                for (int rr = 0; rr < 4; ++rr) acc[rr] = acc[rr] * ri[rr] + accb[rr] * dsc;
             } else {
                 // a0 W1^T (W1r: FWD slot 2, EVAL slot 1)
                 const char* img = MODE == FWD ? S2 : S1;
@@ -480,14 +502,13 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
                 const int row = kh * 16 + 4 * lq + rr;
                 const float v = acc[rr] + bias1;
                 if (MODE == FVP) {
-                    av[rr] = pa1[rr];
-                    D1[row * L::LD + j] = (1.f - av[rr] * av[rr]) * v;
+                    D1[row * L::LD + j] = (1.f - pa1[rr] * pa1[rr]) * v;
                 } else {
                     av[rr] = tanhf(v);
                     if (MODE == FWD && row < nrow) a.a1[(row_base + row) * H + j] = av[rr];
                 }
             }
-            astore4(A1i, j, kh * 16 + 4 * lq, av);
+            if (MODE != FVP) astore4(A1i, j, kh * 16 + 4 * lq, av);
         }
         __syncthreads();
         KX_STAMP(3);
@@ -499,6 +520,9 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
                 // D1 W2^T (W2c, folded) + a1 dW2^T (dW2r)
                 half8 ah[2], al[2];
                 const float rinv = adyn<2>(D1, L::LD, rb3, lq, lr16, sc3, ah, al);
+                float ri[4];
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) ri[rr] = __shfl(rinv, 4 * lq + rr, 64);
                 floatx4 accb = zero4();
 #pragma unroll
                 for (int s = 0; s < 2; ++s) {
@@ -511,7 +535,7 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
                 }
                 const float dsc = sc4v[col3];
 #pragma unroll
-                for (int rr = 0; rr < 4; ++rr) acc[rr] = acc[rr] * __shfl(rinv, 4 * lq + rr, 64) + accb[rr] * dsc;
+                for (int rr = 0; rr < 4; ++rr) acc[rr] = acc[rr] * ri[rr] + accb[rr] * dsc;
             } else {
                 const char* img = MODE == FWD ? S4 : S3;
 #pragma unroll
@@ -564,6 +588,9 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
             const int hcol = cb * 16 + lr16;
             half8 ah[1], al[1];
             const float rinv = adyn<1>(GPf, L::LDG, kh, lq, lr16, nullptr, ah, al);
+            float ri[4];
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) ri[rr] = __shfl(rinv, 4 * lq + rr, 64);
             half8 bh, bl;
             wcol(S3, L::WIMG2, cb, 0, lq, lr16, bh, bl);
             const floatx4 acc = mfma_x3(ah[0], al[0], bh, bl, zero4());
@@ -573,7 +600,7 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
             for (int rr = 0; rr < 4; ++rr) {
                 const int row = kh * 16 + 4 * lq + rr;
                 const float av = MODE == FVP ? pa1[rr] : aval(A1i, hcol, row);
-                gv[rr] = (1.f - av * av) * (acc[rr] * __shfl(rinv, 4 * lq + rr, 64) * csc);
+                gv[rr] = (1.f - av * av) * (acc[rr] * ri[rr] * csc);
                 D0[row * L::LD + hcol] = gv[rr];   // G1
             }
             *reinterpret_cast<float4*>(G1T + hcol * L::LDT + kh * 16 + 4 * lq) = make_float4(gv[0], gv[1], gv[2], gv[3]);
@@ -585,6 +612,9 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
             const int hcol = cb * 16 + lr16;
             half8 ah[2], al[2];
             const float rinv = adyn<2>(D0, L::LD, kh, lq, lr16, nullptr, ah, al);
+            float ri[4];
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) ri[rr] = __shfl(rinv, 4 * lq + rr, 64);
             floatx4 acc = zero4();
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
@@ -598,7 +628,7 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
             for (int rr = 0; rr < 4; ++rr) {
                 const int row = kh * 16 + 4 * lq + rr;
                 const float av = aval(A0i, hcol, row);
-                gv[rr] = (1.f - av * av) * (acc[rr] * __shfl(rinv, 4 * lq + rr, 64) * csc) * Us[row];
+                gv[rr] = (1.f - av * av) * (acc[rr] * ri[rr] * csc) * Us[row];
             }
             *reinterpret_cast<float4*>(D1 + hcol * L::LDT + kh * 16 + 4 * lq) = make_float4(gv[0], gv[1], gv[2], gv[3]);
         }
@@ -642,10 +672,7 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) s4[rr] = __shfl(inv, 4 * lq + rr, 64);
                 if (kh == 0) {
-                    float t = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
-                    t += __shfl_xor(t, 16, 64);
-                    t += __shfl_xor(t, 32, 64);
-                    b1acc += t;
+                    b1acc += sum_over_groups(((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7])));
                 }
             }
 #pragma unroll
@@ -666,10 +693,7 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) s4[rr] = __shfl(inv, 4 * lq + rr, 64);
                 if ((w & 3) == 0) {
-                    float t = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
-                    t += __shfl_xor(t, 16, 64);
-                    t += __shfl_xor(t, 32, 64);
-                    b2acc += t;
+                    b2acc += sum_over_groups(((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7])));
                 }
                 half8 bh, bl;
                 acol(A1i, (w & 3) * 16 + lr16, lq, bh, bl);

@@ -26,7 +26,8 @@
 // phase profile (debug builds): wave 0 of block 0 accumulates s_memtime cycles
 // between stamps in (wave-uniform, scalar) registers, written once at the end;
 // read with mjrl_debug_kx_prof
-__device__ unsigned long long g_kx_prof[16];
+constexpr int KX_NPROF = 18;   // 0-14 phases, 15 launch preamble, 16 tail (slab writes), 17 launches
+__device__ unsigned long long g_kx_prof[KX_NPROF];
 #define KX_STAMP(i)                                                     \
     do {                                                                \
         const unsigned long long now_ = __builtin_amdgcn_s_memtime();   \
@@ -176,37 +177,62 @@ __device__ __forceinline__ void gdyn(const float* bufT, int ldt, int ub, int q, 
 
 // Split a [rows][64] f32 weight matrix (global, row-major, row stride 64) into an
 // LDS image pair scaled per row (COLS = false) or per column (COLS = true);
-// inverse scales to inv[].  rows <= 64; rows >= nrows of the image are zero.
-template <bool COLS>
-__device__ void wsplit(const float* __restrict__ W, int nrows, int img_rows, char* img, int imgbytes, float* inv,
-                       int tid) {
+// inverse scales to inv[].  Three steps, so that a launch issues the loads of all
+// its images before it waits on any: wload (thread = column lane, rows w + 8k;
+// rows >= nrows read as zero), wscale (row maxima by wave shuffles, column maxima
+// through red[8][64] in LDS) and wstore.  IR = image rows / 8.
+template <int IR>
+__device__ __forceinline__ void wload(const float* __restrict__ W, int nrows, float (&v)[IR], int tid) {
+    const int lane = tid & 63, w = tid >> 6;
+#pragma unroll
+    for (int k = 0; k < IR; ++k) {
+        const int j = w + 8 * k;
+        v[k] = j < nrows ? W[j * 64 + lane] : 0.f;
+    }
+}
+
+template <bool COLS, int IR>
+__device__ __forceinline__ void wscale(const float (&v)[IR], float* inv, float* red, int tid) {
     const int lane = tid & 63, w = tid >> 6;
     if (COLS) {
-        // wave 0: lane = column; scales from the column max
-        if (w == 0) {
-            float mx = 0.f;
-            for (int j = 0; j < nrows; ++j) mx = fmaxf(mx, fabsf(W[j * 64 + lane]));
-            float iv;
-            pow2_scale(mx, iv);
-            inv[lane] = iv;
-        }
+        float mx = 0.f;
+#pragma unroll
+        for (int k = 0; k < IR; ++k) mx = fmaxf(mx, fabsf(v[k]));
+        red[w * 64 + lane] = mx;
     } else {
-        for (int j = w; j < img_rows; j += KT / 64) {
-            float mx = j < nrows ? fabsf(W[j * 64 + lane]) : 0.f;
+#pragma unroll
+        for (int k = 0; k < IR; ++k) {
+            float mx = fabsf(v[k]);
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
             float iv;
             pow2_scale(mx, iv);
-            if (lane == 0) inv[j] = iv;
+            if (lane == 0) inv[w + 8 * k] = iv;
         }
     }
-    __syncthreads();
-    for (int i = tid; i < img_rows * 64; i += KT) {
-        const int j = i >> 6, c = i & 63;
-        const float x = j < nrows ? W[j * 64 + c] : 0.f;
-        const float y = x / inv[COLS ? c : j];   // exact: inv is a power of two
+}
+
+// COLS images: the column maxima in red[] -> inv[] (wave 0, after a barrier)
+__device__ __forceinline__ void wscale_cols(float* inv, const float* red, int tid) {
+    if (tid < 64) {
+        float mx = 0.f;
+#pragma unroll
+        for (int i = 0; i < KT / 64; ++i) mx = fmaxf(mx, red[i * 64 + tid]);
+        float iv;
+        pow2_scale(mx, iv);
+        inv[tid] = iv;
+    }
+}
+
+template <bool COLS, int IR>
+__device__ __forceinline__ void wstore(const float (&v)[IR], char* img, int imgbytes, const float* inv, int tid) {
+    const int lane = tid & 63, w = tid >> 6;
+#pragma unroll
+    for (int k = 0; k < IR; ++k) {
+        const int j = w + 8 * k;
+        const float y = v[k] / inv[COLS ? lane : j];   // exact: inv is a power of two
         const _Float16 h = (_Float16)y;
-        const int off = woff(j, c);
+        const int off = woff(j, lane);
         *reinterpret_cast<_Float16*>(img + off) = h;
         *reinterpret_cast<_Float16*>(img + imgbytes + off) = (_Float16)(y - (float)h);
     }
@@ -240,6 +266,9 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
     char* A1i = sb + L::oA1;
 
     if (MODE == FVP && a.done && *a.done) return;
+#ifdef MJRL_KX_PROF
+    const unsigned long long kx_t0_ = __builtin_amdgcn_s_memtime();
+#endif
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int r16 = lane & 15, q = lane >> 4;
     const int cb = w & 3, kh = w >> 2;
@@ -250,42 +279,19 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
     const Packed pk(H, H, NP, MP);
     const float* W0src = (MODE == FVP ? a.V : P) + pk.W0;
 
+
     // ---- launch preamble: weight images, this wave's W0 / dW0 slice to registers ----
-    if (MODE == EVAL) {
-        wsplit<false>(P + pk.W1, H, H, S1, L::WIMG, sc1, tid);
-        wsplit<false>(P + pk.W2, MP, 32, S3, L::WIMG2, sc3, tid);
-    } else {
-        wsplit<true>(P + pk.W1, H, H, S1, L::WIMG, sc1, tid);
-        wsplit<true>(P + pk.W2, MP, 32, S3, L::WIMG2, sc3, tid);
-        const float* src = MODE == FVP ? a.V : P;   // FVP: dW1r / dW2r;  FWD: W1r / W2r
-        wsplit<false>(src + pk.W1, H, H, S2, L::WIMG, sc2, tid);
-        wsplit<false>(src + pk.W2, MP, 32, S4, L::WIMG2, sc4v, tid);
-    }
+    // every global load of the preamble is issued before the first wait
     constexpr int KS = KH / 32;   // k32 steps per observation half
-    half8 wh[KS], wl[KS];
-    float wsc;
-    {
-        float8v v[KS];
-        float mx = 0.f;
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-            v[s] = load8(W0src + (cb * 16 + r16) * NP + kh * KH + 32 * s + 8 * q);
-            mx = fmaxf(mx, absmax8(v[s]));
-        }
-        const float sc = pow2_scale(max_over_groups(mx), wsc);
-#pragma unroll
-        for (int s = 0; s < KS; ++s) split8(v[s], sc, wh[s], wl[s]);
+    static_assert(KT == 512 && MP <= 32, "preamble layout: 8 waves, output-layer images of 32 rows");
+    float w1v[8], w3v[4], w2v[8], w4v[4];
+    wload(P + pk.W1, H, w1v, tid);
+    wload(P + pk.W2, MP, w3v, tid);
+    if (MODE != EVAL) {
+        const float* src = MODE == FVP ? a.V : P;   // FVP: dW1r / dW2r;  FWD: W1r / W2r
+        wload(src + pk.W1, H, w2v, tid);
+        wload(src + pk.W2, MP, w4v, tid);
     }
-
-    floatx4 g0[KG];
-#pragma unroll
-    for (int g = 0; g < KG; ++g) g0[g] = zero4();
-    floatx4 g1[2] = {zero4(), zero4()};   // gW1 blocks (jb = cb, kb = kh + 2j)
-    floatx4 g2 = zero4();                 // gW2 block (jb = w >> 2 < MP/16, kb = w & 3)
-    float b1acc = 0.f, b2acc = 0.f;
-    double racc0 = 0.0, racc1 = 0.0;
-    const float sls = MODE == FVP ? 0.f : ls_sum(P + pk.ls, m);
-
     const float* BV = MODE == FVP ? a.V : P;
     const float bias1 = BV[pk.b1 + cb * 16 + r16];
     const int cbo3 = w & (MP / 16 - 1), rb3 = w / (MP / 16);   // P3: waves < 2 * MP/16
@@ -298,6 +304,57 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
         const float sg = expf(P[pk.ls + col3]);
         wq3 = os3 * os3 * (2.f / (2.f * sg * sg + 1e-8f));
     }
+    const float sls = MODE == FVP ? 0.f : ls_sum(P + pk.ls, m);
+    half8 wh[KS], wl[KS];
+    float wsc;
+    {
+        float8v v[KS];
+#pragma unroll
+        for (int s = 0; s < KS; ++s) v[s] = load8(W0src + (cb * 16 + r16) * NP + kh * KH + 32 * s + 8 * q);
+        float mx = 0.f;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) mx = fmaxf(mx, absmax8(v[s]));
+        const float sc = pow2_scale(max_over_groups(mx), wsc);
+#pragma unroll
+        for (int s = 0; s < KS; ++s) split8(v[s], sc, wh[s], wl[s]);
+    }
+    {
+        float* red1 = D0;          // [8][64] column-max partials (D0 / D0B are free until P1)
+        float* red3 = D0 + 512;
+        if (MODE == EVAL) {
+            wscale<false>(w1v, sc1, nullptr, tid);
+            wscale<false>(w3v, sc3, nullptr, tid);
+        } else {
+            wscale<true>(w1v, sc1, red1, tid);
+            wscale<true>(w3v, sc3, red3, tid);
+            wscale<false>(w2v, sc2, nullptr, tid);
+            wscale<false>(w4v, sc4v, nullptr, tid);
+        }
+        __syncthreads();
+        if (MODE != EVAL) {
+            wscale_cols(sc1, red1, tid);
+            wscale_cols(sc3, red3, tid);
+            __syncthreads();
+        }
+        if (MODE == EVAL) {
+            wstore<false>(w1v, S1, L::WIMG, sc1, tid);
+            wstore<false>(w3v, S3, L::WIMG2, sc3, tid);
+        } else {
+            wstore<true>(w1v, S1, L::WIMG, sc1, tid);
+            wstore<true>(w3v, S3, L::WIMG2, sc3, tid);
+            wstore<false>(w2v, S2, L::WIMG, sc2, tid);
+            wstore<false>(w4v, S4, L::WIMG2, sc4v, tid);
+        }
+    }
+
+    floatx4 g0[KG];
+#pragma unroll
+    for (int g = 0; g < KG; ++g) g0[g] = zero4();
+    floatx4 g1[2] = {zero4(), zero4()};   // gW1 blocks (jb = cb, kb = kh + 2j)
+    floatx4 g2 = zero4();                 // gW2 block (jb = w >> 2 < MP/16, kb = w & 3)
+    float b1acc = 0.f, b2acc = 0.f;
+    double racc0 = 0.0, racc1 = 0.0;
+
 
     float touch[2] = {0.f, 0.f};
     // the xhat tile is software-pipelined through registers: tile t+1's pieces are
@@ -319,8 +376,10 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
     xload(blockIdx.x, tid);
     __syncthreads();   // images and scales ready
 #ifdef MJRL_KX_PROF
-    unsigned long long kx_acc_[16] = {0};
+    unsigned long long kx_acc_[KX_NPROF] = {0};
     unsigned long long kx_last_ = __builtin_amdgcn_s_memtime();
+    kx_acc_[15] = kx_last_ - kx_t0_;
+    kx_acc_[17] = 1;
 #endif
 
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
@@ -747,8 +806,9 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
         row_pass_final<MODE, MP, KT>(racc0, racc1, reinterpret_cast<double*>(smem), a.rpart, blk, tid);
     }
 #ifdef MJRL_KX_PROF
+    kx_acc_[16] = __builtin_amdgcn_s_memtime() - kx_last_;
     if (blockIdx.x == 0 && tid == 0)
-        for (int i = 0; i < 16; ++i) g_kx_prof[i] += kx_acc_[i];
+        for (int i = 0; i < KX_NPROF; ++i) g_kx_prof[i] += kx_acc_[i];
 #endif
 }
 

@@ -77,8 +77,16 @@ __device__ __forceinline__ float tanh_f(float x) { return tanhf(x); }
 
 // sum_j log_std_j in action order (the -sum(log_std) term of log_likelihood)
 __device__ __forceinline__ float ls_sum(const float* __restrict__ P_ls, int m) {
+    // sum(log_std) front to back; the loads of a 16-chunk are issued together
+    // (adding the zero padding is exact)
     float s = 0.f;
-    for (int j = 0; j < m; ++j) s += P_ls[j];
+    for (int j0 = 0; j0 < m; j0 += 16) {
+        float v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = j0 + u < m ? P_ls[j0 + u] : 0.f;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) s += v[u];
+    }
     return s;
 }
 
@@ -1061,9 +1069,9 @@ extern "C" {
 #ifdef MJRL_KX_PROF
 // debug builds only: copy out and clear the k_kx phase profile (16 counters)
 int mjrl_debug_kx_prof(unsigned long long* out) {
-    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_kx_prof), sizeof(unsigned long long) * 16);
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_kx_prof), sizeof(unsigned long long) * KX_NPROF);
     if (e != hipSuccess) return (int)e;
-    unsigned long long z[16] = {0};
+    unsigned long long z[KX_NPROF] = {0};
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_kx_prof), z, sizeof(z));
 }
 #endif

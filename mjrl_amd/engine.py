@@ -286,10 +286,18 @@ class UpdateEngine:
                                                 _lib.ptr(w["xhat"]), _lib.ptr(w["act32"]), st), "mjrl_pack_batch")
 
     # ------------------------------------------------------------------
-    def returns_advantages(self, batch, gamma, gae_lambda):
+    def _side_stream(self):
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        return self._side
+
+    def returns_advantages(self, batch, gamma, gae_lambda, stream=None):
         """process_samples.compute_returns + compute_advantages on device (a1-a3).
-        Leaves f64 returns / advantages in ws['ret'] / ws['adv64']."""
-        self.st = _lib.stream_ptr()
+        Leaves f64 returns / advantages in ws['ret'] / ws['adv64'].  `stream`: run on
+        that HIP stream (update() overlaps the scan with the batch assembly)."""
+        st = stream if stream is not None else _lib.stream_ptr()
+        if stream is None:
+            self.st = st
         self._ensure(batch.T + batch.T_demo, batch.P)
         w = self.ws
         use_gae = not (gae_lambda is None or gae_lambda < 0.0 or gae_lambda > 1.0)
@@ -297,7 +305,7 @@ class UpdateEngine:
         _lib.check(self.lib.mjrl_gae(
             _lib.ptr(batch.rewards), _lib.ptr(base), _lib.ptr(batch.path_off), _lib.ptr(batch.terminated),
             batch.P, float(gamma), float(gae_lambda) if use_gae else 0.0, int(use_gae),
-            _lib.ptr(w["ret"]), _lib.ptr(w["adv64"]), _lib.ptr(w["path_ret"]), self.st), "mjrl_gae")
+            _lib.ptr(w["ret"]), _lib.ptr(w["adv64"]), _lib.ptr(w["path_ret"]), st), "mjrl_gae")
         return w["ret"][:batch.T], w["adv64"][:batch.T]
 
     def normalize_advantages(self, T):
@@ -346,18 +354,22 @@ class UpdateEngine:
         ins, isc, osh, osc = self.transforms
         timing = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
 
-        # a5: batch assembly (f64 -> f32, input normalisation, bias column)
-        self._pack(batch.obs, batch.act, T_all, st)
-        # a1-a3: returns / advantages
+        # a1-a3: returns / advantages.  The scan is a serial fp64 chain per path
+        # (latency-bound, few waves): it runs on a side stream beside the HBM-bound
+        # batch assembly and joins before the moments.
+        main = torch.cuda.current_stream(self.device)
+        side = self._side_stream()
+        side.wait_stream(main)
+        adv64 = w["adv64"]
         if batch.advantages is not None:
             adv64 = batch.advantages
             # path returns still come from the rewards (npg_cg.py:97)
-            self.returns_advantages(batch, gamma, None)
-        elif skip_gae:
-            adv64 = w["adv64"]
-        else:
-            self.returns_advantages(batch, gamma, gae_lambda)
-            adv64 = w["adv64"]
+            self.returns_advantages(batch, gamma, None, stream=C.c_void_p(side.cuda_stream))
+        elif not skip_gae:
+            self.returns_advantages(batch, gamma, gae_lambda, stream=C.c_void_p(side.cuda_stream))
+        # a5: batch assembly (f64 -> f32, input normalisation, bias column)
+        self._pack(batch.obs, batch.act, T_all, st)
+        main.wait_stream(side)
         # whitening (npg_cg.py:91) and path-return statistics (npg_cg.py:97-102):
         # two-pass fp64 moments; when sharded, each pass's sums of both quantities
         # share one all-reduce (plus one MAX for the path-return extrema)

@@ -20,10 +20,13 @@ NAMES = ["publish", "P1 first layer", "P1 fold", "P2", "P3", "row pass", "P4", "
          "P6 xload", "P6 G0 split", "P6 gW0", "P6 gW1", "P6 gW2+bias"]
 
 
+NPROF = 18
+
+
 def read(lib):
-    out = (C.c_ulonglong * 16)()
+    out = (C.c_ulonglong * NPROF)()
     _lib.check(lib.mjrl_debug_kx_prof(out), "mjrl_debug_kx_prof")
-    return np.array(out[:15], dtype=np.float64)
+    return np.array(out[:NPROF], dtype=np.float64)
 
 
 def main(T=1000000):
@@ -43,10 +46,14 @@ def main(T=1000000):
     torch.cuda.synchronize()
     res = {"FWD": read(lib)}
     v = torch.from_numpy(rs.randn(29410).astype(np.float32)).cuda()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
     for _ in range(3):
         eng.fvp(v, T=T)
+    e1.record()
     torch.cuda.synchronize()
     res["FVP"] = read(lib) / 3
+    print("FVP + gather: %.1f us per call (events)" % (e0.elapsed_time(e1) / 3 * 1e3))
     eng.eval_pass(th, T)
     torch.cuda.synchronize()
     res["EVAL"] = read(lib)
@@ -54,8 +61,12 @@ def main(T=1000000):
     print("%-16s" % "phase" + "".join("%10s" % k for k in res))
     for i, n in enumerate(NAMES):
         print("%-16s" % n + "".join("%10.0f" % (r[i] / tiles) for r in res.values()))
-    print("%-16s" % "total" + "".join("%10.0f" % (r.sum() / tiles) for r in res.values()))
+    print("%-16s" % "total" + "".join("%10.0f" % (r[:15].sum() / tiles) for r in res.values()))
+    print("per launch (cycles, workgroup 0):")
+    for i, n in ((15, "preamble"), (16, "tail")):
+        print("%-16s" % n + "".join("%10.0f" % (r[i] / max(r[17], 1)) for r in res.values()))
+    print("%-16s" % "tile loop" + "".join("%10.0f" % (r[:15].sum() / max(r[17], 1)) for r in res.values()))
 
 
 if __name__ == "__main__":
-    main()
+    main(int(sys.argv[1]) if len(sys.argv) > 1 else 1000000)

@@ -77,11 +77,51 @@ __device__ __forceinline__ float pow2_scale(float M, float& inv) {
 typedef float float8v __attribute__((ext_vector_type(8)));
 typedef short short8v __attribute__((ext_vector_type(8)));
 
-// hi / lo of y = v * s (vector form: packed v_cvt_pk_f16_f32, round to nearest)
+typedef unsigned uint4v __attribute__((ext_vector_type(4)));
+
+// lo = f16(y - hi) for a packed pair (hi2: two f16; y0, y1: f32): v_fma_mixlo_f16 /
+// v_fma_mixhi_f16 compute hi * -1 + y exactly in f32 and round once to f16 (y - hi is
+// exact, so this equals f16((float)(y - hi))), one instruction per value instead of
+// an f16 -> f32 conversion, a subtraction and a conversion back
+__device__ __forceinline__ unsigned mix_lo2(unsigned hi2, float y0, float y1) {
+    unsigned t;
+    asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(t) : "v"(hi2), "v"(y0));
+    asm("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(t) : "v"(hi2), "v"(y1));
+    return t;
+}
+
+// hi / lo of y = v * s (packed v_cvt_pk_f16_f32, round to nearest; lo via mix_lo2)
 __device__ __forceinline__ void split8(const float8v& v, float s, half8& hi, half8& lo) {
     const float8v y = v * s;
     hi = __builtin_convertvector(y, half8);
-    lo = __builtin_convertvector(y - __builtin_convertvector(hi, float8v), half8);
+    const uint4v h = __builtin_bit_cast(uint4v, hi);
+    uint4v l;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) l[p] = mix_lo2(h[p], y[2 * p], y[2 * p + 1]);
+    lo = __builtin_bit_cast(half8, l);
+}
+
+// (float)hi + (float)lo for the two halves of packed f16 pairs (v_fma_mix_f32: hi * 1 + lo,
+// exact in f32)
+__device__ __forceinline__ float mix_add_lo(unsigned h2, unsigned l2) {
+    float r;
+    asm("v_fma_mix_f32 %0, %1, 1.0, %2 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(h2), "v"(l2));
+    return r;
+}
+__device__ __forceinline__ float mix_add_hi(unsigned h2, unsigned l2) {
+    float r;
+    asm("v_fma_mix_f32 %0, %1, 1.0, %2 op_sel:[1,0,1] op_sel_hi:[1,0,1]" : "=v"(r) : "v"(h2), "v"(l2));
+    return r;
+}
+__device__ __forceinline__ float8v hilo8(const half8& hh, const half8& ll) {
+    const uint4v h = __builtin_bit_cast(uint4v, hh), l = __builtin_bit_cast(uint4v, ll);
+    float8v r;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        r[2 * p] = mix_add_lo(h[p], l[p]);
+        r[2 * p + 1] = mix_add_hi(h[p], l[p]);
+    }
+    return r;
 }
 
 __device__ __forceinline__ float8v load8(const float* p) {

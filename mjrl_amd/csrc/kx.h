@@ -124,20 +124,21 @@ __device__ __forceinline__ void acol(const char* img, int f, int q, half8& h, ha
 // a at (feature f, row) from an activation image (hi + lo)
 __device__ __forceinline__ float aval(const char* img, int f, int row) {
     const int off = aoff(f, row);
-    return (float)*reinterpret_cast<const _Float16*>(img + off) +
-           (float)*reinterpret_cast<const _Float16*>(img + AIMG_BYTES + off);
+    return mix_add_lo(*reinterpret_cast<const unsigned short*>(img + off),
+                      *reinterpret_cast<const unsigned short*>(img + AIMG_BYTES + off));
 }
 // store 4 consecutive rows (row0..row0+3, row0 % 4 == 0) of feature f into an activation image
 __device__ __forceinline__ void astore4(char* img, int f, int row0, const float (&v)[4]) {
     typedef _Float16 half4 __attribute__((ext_vector_type(4)));
-    const float4 x = make_float4(v[0], v[1], v[2], v[3]);
-    half4 h, l;
-    h[0] = (_Float16)x.x; h[1] = (_Float16)x.y; h[2] = (_Float16)x.z; h[3] = (_Float16)x.w;
-    l[0] = (_Float16)(x.x - (float)h[0]); l[1] = (_Float16)(x.y - (float)h[1]);
-    l[2] = (_Float16)(x.z - (float)h[2]); l[3] = (_Float16)(x.w - (float)h[3]);
+    typedef unsigned uint2v __attribute__((ext_vector_type(2)));
+    typedef float float4v __attribute__((ext_vector_type(4)));
+    const float4v x = {v[0], v[1], v[2], v[3]};
+    const half4 h = __builtin_convertvector(x, half4);
+    const uint2v hb = __builtin_bit_cast(uint2v, h);
+    const uint2v lb = {mix_lo2(hb[0], v[0], v[1]), mix_lo2(hb[1], v[2], v[3])};
     const int off = aoff(f, row0);
-    *reinterpret_cast<half4*>(img + off) = h;
-    *reinterpret_cast<half4*>(img + AIMG_BYTES + off) = l;
+    *reinterpret_cast<uint2v*>(img + off) = hb;
+    *reinterpret_cast<uint2v*>(img + AIMG_BYTES + off) = lb;
 }
 
 // Dynamic left operand from an f32 [row][ld] buffer: rows rb*16 + r, K = 32*KS
@@ -230,7 +231,7 @@ __device__ __forceinline__ void wstore(const float (&v)[IR], char* img, int imgb
 #pragma unroll
     for (int k = 0; k < IR; ++k) {
         const int j = w + 8 * k;
-        const float y = v[k] / inv[COLS ? lane : j];   // exact: inv is a power of two
+        const float y = v[k] * __builtin_amdgcn_rcpf(inv[COLS ? lane : j]);   // exact: inv is a power of two
         const _Float16 h = (_Float16)y;
         const int off = woff(j, lane);
         *reinterpret_cast<_Float16*>(img + off) = h;
@@ -240,6 +241,9 @@ __device__ __forceinline__ void wstore(const float (&v)[IR], char* img, int imgb
 
 template <int MP, int KG, int MODE>
 __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
+    // multiply-add chains in this kernel contract to FMA (the reference-order
+    // elementwise code lives in other kernels; -ffp-contract=off is the file default)
+#pragma clang fp contract(fast)
     using L = XLayout<MP, KG>;
     constexpr int H = 64, BT = L::BT, NP = L::NP, KH = L::KH;
     constexpr bool GRAD = MODE != EVAL;
@@ -519,8 +523,7 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
                 for (int s = 0; s < 2; ++s) {
                     arow(A0i, kh, s, lq, lr16, xh[s], xl[s]);
                     const int o = (kh * 16 + lr16) * L::LD + 32 * s + 8 * lq;
-                    const float8v av =
-                        __builtin_convertvector(xh[s], float8v) + __builtin_convertvector(xl[s], float8v);
+                    const float8v av = hilo8(xh[s], xl[s]);
                     dv[s] = ((load8(D0 + o) + load8(D0B + o)) * (1.f - av * av)) * load8(sc1 + 32 * s + 8 * lq);
                     mx = fmaxf(mx, absmax8(dv[s]));
                 }
@@ -666,7 +669,10 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
         }
         __syncthreads();
         KX_STAMP(6);
-        // ---- P5: gu0 = (1 - a0^2) (gu1 W1), times the xhat row scale ----
+        // ---- P5: gu0 = (1 - a0^2) (gu1 W1), times the xhat row scale; beside it the
+        // gW1 / gW2 sums (their operands are complete since P4) and the next tile's
+        // xhat loads (consumed at the next publish) ----
+        xload(tile + gridDim.x, ltid);
         {
             const int hcol = cb * 16 + lr16;
             half8 ah[2], al[2];
@@ -691,14 +697,54 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
             }
             *reinterpret_cast<float4*>(D1 + hcol * L::LDT + kh * 16 + 4 * lq) = make_float4(gv[0], gv[1], gv[2], gv[3]);
         }
+        {
+            half8 gh, gl;
+            float s4[4];
+            // gW1[jb = cb][kb = kh + 2jj] += gu1^T a0;  gb1 = row sums of gu1 (waves kh = 0)
+            {
+                const float8v v = load8(G1T + (cb * 16 + lr16) * L::LDT + 8 * lq);
+                float inv;
+                const float sc = pow2_scale(max_over_groups(absmax8(v)), inv);
+                split8(v, sc, gh, gl);
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) s4[rr] = __shfl(inv, 4 * lq + rr, 64);
+                if (kh == 0) {
+                    b1acc += sum_over_groups(((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7])));
+                }
+            }
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj) {
+                half8 bh, bl;
+                acol(A0i, (kh + 2 * jj) * 16 + lr16, lq, bh, bl);
+                const floatx4 t = mfma_x3(gh, gl, bh, bl, zero4());
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) g1[jj][rr] += t[rr] * s4[rr];
+            }
+            // gW2[jb = w >> 2][kb = w & 3] += gp^T a1;  gb2 = row sums of gp (waves kb = 0)
+            if ((w >> 2) < MP / 16) {
+                const float8v v = load8(GPT + ((w >> 2) * 16 + lr16) * L::LDT + 8 * lq);
+                float inv;
+                const float sc = pow2_scale(max_over_groups(absmax8(v)), inv);
+                split8(v, sc, gh, gl);
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) s4[rr] = __shfl(inv, 4 * lq + rr, 64);
+                if ((w & 3) == 0) {
+                    b2acc += sum_over_groups(((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7])));
+                }
+                half8 bh, bl;
+                acol(A1i, (w & 3) * 16 + lr16, lq, bh, bl);
+                const floatx4 t = mfma_x3(gh, gl, bh, bl, zero4());
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) g2[rr] += t[rr] * s4[rr];
+            }
+        }
         __syncthreads();
         KX_STAMP(7);
 
-        // ---- P6: weight-gradient sums ----
-        xload(tile + gridDim.x, ltid);   // next tile's xhat, consumed at the next publish
+        // ---- P6: the gW0 sums ----
         KX_STAMP(10);
         {
-            // gW0 (xhat transposed reads), gW1 (a0 image), gW2 (a1 image)
+            // gW0 (xhat transposed reads)
             half8 gh, gl;
             float s4[4];
             gdyn(D1, L::LDT, cb, lq, lr16, gh, gl, s4);   // G0T
@@ -722,44 +768,6 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
                 if (g & 1) __builtin_amdgcn_sched_barrier(0);
             }
             KX_STAMP(12);
-            // gW1[jb = cb][kb = kh + 2jj] += gu1^T a0;  gb1 = row sums of gu1 (waves kh = 0)
-            {
-                const float8v v = load8(G1T + (cb * 16 + lr16) * L::LDT + 8 * lq);
-                float inv;
-                const float sc = pow2_scale(max_over_groups(absmax8(v)), inv);
-                split8(v, sc, gh, gl);
-#pragma unroll
-                for (int rr = 0; rr < 4; ++rr) s4[rr] = __shfl(inv, 4 * lq + rr, 64);
-                if (kh == 0) {
-                    b1acc += sum_over_groups(((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7])));
-                }
-            }
-#pragma unroll
-            for (int jj = 0; jj < 2; ++jj) {
-                half8 bh, bl;
-                acol(A0i, (kh + 2 * jj) * 16 + lr16, lq, bh, bl);
-                const floatx4 t = mfma_x3(gh, gl, bh, bl, zero4());
-#pragma unroll
-                for (int rr = 0; rr < 4; ++rr) g1[jj][rr] += t[rr] * s4[rr];
-            }
-            KX_STAMP(13);
-            // gW2[jb = w >> 2][kb = w & 3] += gp^T a1;  gb2 = row sums of gp (waves kb = 0)
-            if ((w >> 2) < MP / 16) {
-                const float8v v = load8(GPT + ((w >> 2) * 16 + lr16) * L::LDT + 8 * lq);
-                float inv;
-                const float sc = pow2_scale(max_over_groups(absmax8(v)), inv);
-                split8(v, sc, gh, gl);
-#pragma unroll
-                for (int rr = 0; rr < 4; ++rr) s4[rr] = __shfl(inv, 4 * lq + rr, 64);
-                if ((w & 3) == 0) {
-                    b2acc += sum_over_groups(((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7])));
-                }
-                half8 bh, bl;
-                acol(A1i, (w & 3) * 16 + lr16, lq, bh, bl);
-                const floatx4 t = mfma_x3(gh, gl, bh, bl, zero4());
-#pragma unroll
-                for (int rr = 0; rr < 4; ++rr) g2[rr] += t[rr] * s4[rr];
-            }
         }
         KX_STAMP(14);
         __syncthreads();

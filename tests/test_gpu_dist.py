@@ -61,7 +61,7 @@ def _worker(rank, world, port, name, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name", ["c2_ragged", "c3_halfcheetah_trpo", "c2_hvp_sub"])
+@pytest.mark.parametrize("name", ["c2_ragged", "c3_halfcheetah_trpo", "c2_hvp_sub", "c4_humanoid"])
 def test_two_rank_update(name):
     from oracle import npg_cpu as O
     world = 2

@@ -82,6 +82,7 @@ __global__ void __launch_bounds__(CG_THREADS) k_cg_init(mjrl_shape s, const floa
     __shared__ double red[CG_THREADS / 64];
     const PackMap pm(s);
     double acc = 0.0;
+#pragma unroll 8
     for (int f = threadIdx.x; f < s.d; f += CG_THREADS) {
         const float v = b[f];
         x[f] = 0.f;
@@ -225,11 +226,16 @@ __device__ __forceinline__ bool cgm_last(double part, float* cg, int nwg, double
     __syncthreads();
     if (ticket != (unsigned)(nwg - 1)) return false;
     __threadfence();
-    if (threadIdx.x == 0) {
+    if (threadIdx.x < 64) {
+        // wave 0: lane l folds partials l, l + 64, ... in order (all loads in flight
+        // together), then a fixed shuffle tree; the same order on every run
         double t = 0.0;
-        for (int i = 0; i < nwg; ++i) t += parts[i];   // visible after the acquire fence above
-        total = t;
-        *reinterpret_cast<unsigned*>(cg + 8) = 0u;   // reset the ticket for the next launch
+        for (int i = threadIdx.x; i < nwg; i += 64) t += parts[i];   // visible after the acquire fence above
+        t = wave_sum(t);
+        if (threadIdx.x == 0) {
+            total = t;
+            *reinterpret_cast<unsigned*>(cg + 8) = 0u;   // reset the ticket for the next launch
+        }
     }
     return true;
 }
@@ -322,6 +328,7 @@ __global__ void __launch_bounds__(CG_THREADS) k_npg_step(mjrl_shape s, const flo
     __shared__ double red[CG_THREADS / 64];
     const PackMap pm(s);
     double acc = 0.0;
+#pragma unroll 8
     for (int f = threadIdx.x; f < s.d; f += CG_THREADS) acc += (double)g[f] * (double)x[f];
     const float gx = (float)block_sum1024(acc, red);
     float alpha, dl = delta;
@@ -331,6 +338,7 @@ __global__ void __launch_bounds__(CG_THREADS) k_npg_step(mjrl_shape s, const flo
         alpha = alpha_in;
         if (const_lr) dl = __fmul_rn(alpha * alpha, gx);
     }
+#pragma unroll 8
     for (int f = threadIdx.x; f < s.d; f += CG_THREADS) {
         float v = __fadd_rn(theta[f], __fmul_rn(alpha, x[f]));
         int p1, p2;

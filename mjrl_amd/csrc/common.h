@@ -79,26 +79,43 @@ typedef short short8v __attribute__((ext_vector_type(8)));
 
 typedef unsigned uint4v __attribute__((ext_vector_type(4)));
 
-// lo = f16(y - hi) for a packed pair (hi2: two f16; y0, y1: f32): v_fma_mixlo_f16 /
+// lo = f16(y - hi) for 8 values (hi: 4 packed f16 pairs; y: f32): v_fma_mixlo_f16 /
 // v_fma_mixhi_f16 compute hi * -1 + y exactly in f32 and round once to f16 (y - hi is
-// exact, so this equals f16((float)(y - hi))), one instruction per value instead of
-// an f16 -> f32 conversion, a subtraction and a conversion back
+// exact, so this equals f16((float)(y - hi))), one instruction per value instead of an
+// f16 -> f32 conversion, a subtraction and a conversion back.  One asm statement; it
+// ends with the 2 wait states a VALU-written VGPR needs before an MFMA reads it (hipcc
+// pads nothing for an asm producer, cdna_hip_programming.md §5.7 item 2).
+__device__ __forceinline__ uint4v mix_lo8(const uint4v& h, const float8v& y) {
+    uint4v l;
+    asm("v_fma_mixlo_f16 %0, %4, -1.0, %8 op_sel_hi:[1,0,0]\n\t"
+        "v_fma_mixhi_f16 %0, %4, -1.0, %9 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+        "v_fma_mixlo_f16 %1, %5, -1.0, %10 op_sel_hi:[1,0,0]\n\t"
+        "v_fma_mixhi_f16 %1, %5, -1.0, %11 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+        "v_fma_mixlo_f16 %2, %6, -1.0, %12 op_sel_hi:[1,0,0]\n\t"
+        "v_fma_mixhi_f16 %2, %6, -1.0, %13 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+        "v_fma_mixlo_f16 %3, %7, -1.0, %14 op_sel_hi:[1,0,0]\n\t"
+        "v_fma_mixhi_f16 %3, %7, -1.0, %15 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+        "s_nop 1"
+        : "=&v"(l[0]), "=&v"(l[1]), "=&v"(l[2]), "=&v"(l[3])
+        : "v"(h[0]), "v"(h[1]), "v"(h[2]), "v"(h[3]), "v"(y[0]), "v"(y[1]), "v"(y[2]), "v"(y[3]), "v"(y[4]),
+          "v"(y[5]), "v"(y[6]), "v"(y[7]));
+    return l;
+}
+
+// the same for one pair (results feed VALU code only: no MFMA wait states needed)
 __device__ __forceinline__ unsigned mix_lo2(unsigned hi2, float y0, float y1) {
     unsigned t;
-    asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(t) : "v"(hi2), "v"(y0));
-    asm("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(t) : "v"(hi2), "v"(y1));
+    asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]\n\t"
+        "v_fma_mixhi_f16 %0, %1, -1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+        : "=&v"(t) : "v"(hi2), "v"(y0), "v"(y1));
     return t;
 }
 
-// hi / lo of y = v * s (packed v_cvt_pk_f16_f32, round to nearest; lo via mix_lo2)
+// hi / lo of y = v * s (packed v_cvt_pk_f16_f32, round to nearest; lo via mix_lo8)
 __device__ __forceinline__ void split8(const float8v& v, float s, half8& hi, half8& lo) {
     const float8v y = v * s;
     hi = __builtin_convertvector(y, half8);
-    const uint4v h = __builtin_bit_cast(uint4v, hi);
-    uint4v l;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) l[p] = mix_lo2(h[p], y[2 * p], y[2 * p + 1]);
-    lo = __builtin_bit_cast(half8, l);
+    lo = __builtin_bit_cast(half8, mix_lo8(__builtin_bit_cast(uint4v, hi), y));
 }
 
 // (float)hi + (float)lo for the two halves of packed f16 pairs (v_fma_mix_f32: hi * 1 + lo,

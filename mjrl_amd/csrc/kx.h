@@ -386,6 +386,22 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
     kx_acc_[17] = 1;
 #endif
 
+    // P1's xhat-image offsets (row r16, chunk kh*KH/8 + 4s + q, swizzled): tile-invariant,
+    // kept in KS registers instead of being recomputed per tile
+    int p1off[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) p1off[s] = r16 * L::RBYTES + 16 * ((kh * (KH / 8) + 4 * s + q) ^ chunk_swz(r16));
+    // and the transposed-read offsets of the gW0 sums (group g: rows 8q + tq, chunk
+    // kh*KH/8 + tp/2 + 2g, half tp & 1), kept for FVP (FWD has no registers to spare)
+    auto gw0_off = [&](int r_, int q_, int g) {
+        const int tq = r_ >> 2, tp = r_ & 3, row = 8 * q_ + tq;
+        return row * L::RBYTES + 16 * (((kh * KH) / 8 + (tp >> 1) + 2 * g) ^ chunk_swz(row)) + 8 * (tp & 1);
+    };
+    int g0off[MODE == FVP ? KG : 1];
+    if constexpr (MODE == FVP) {
+#pragma unroll
+        for (int g = 0; g < KG; ++g) g0off[g] = gw0_off(r16, q, g);
+    }
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         KX_STAMP(9);   // loop top (the wait on the previous tile's last barrier)
         // per-lane indices through an opaque zero: recomputed per tile rather than
@@ -453,13 +469,11 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
         // ---- P1: first layer, partial over this wave's observation half ----
         floatx4 acc1[2] = {zero4(), zero4()};
         {
-            const int swz1 = chunk_swz(lr16);
 #pragma unroll
             for (int s = 0; s < KS; ++s) {
-                const int ch = kh * (KH / 8) + 4 * s + lq;
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
-                    const int off = (i * 16 + lr16) * L::RBYTES + 16 * (ch ^ swz1);
+                    const int off = p1off[s] + i * 16 * L::RBYTES;   // row i*16 + r16: same swizzle
                     const half8 xh = *reinterpret_cast<const half8*>(XHb + off);
                     const half8 xl = *reinterpret_cast<const half8*>(XLb + off);
                     acc1[i] = mfma_x3(xh, xl, wh[s], wl[s], acc1[i]);
@@ -749,16 +763,14 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
             float s4[4];
             gdyn(D1, L::LDT, cb, lq, lr16, gh, gl, s4);   // G0T
             KX_STAMP(11);
-            const int tq = lr16 >> 2, tp = lr16 & 3;
-            const int cl = (kh * KH) / 8 + (tp >> 1);
 #pragma unroll
             for (int g = 0; g < KG; ++g) {
-                const int c0 = cl + 2 * g;
                 short4v th[2], tl[2];
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
-                    const int row = 8 * lq + 4 * h + tq;
-                    const int off = row * L::RBYTES + 16 * (c0 ^ chunk_swz(row)) + 8 * (tp & 1);
+                    // rows 8q + 4h + tq: the chunk swizzle ignores row bit 2, so h = 1 is
+                    // the h = 0 offset plus four rows
+                    const int off = (MODE == FVP ? g0off[g] : gw0_off(lr16, lq, g)) + h * 4 * L::RBYTES;
                     th[h] = ds_read_tr16(XHb + off);
                     tl[h] = ds_read_tr16(XLb + off);
                 }

@@ -295,8 +295,9 @@ def main():
             gat_name: dict(avg_ms=t_gat * 1e3, tflops=gat_fl * rows_rank / t_gat / 1e12)}
     dom = max(kern, key=lambda k: kern[k]["avg_ms"])
     traffic, tsrc = pmc_traffic(acc_key if dom == acc_name else gat_key)
-    if traffic is not None and world > 1:
-        traffic = traffic * rows_rank / T_total    # the committed PMC pass is the 1-GPU (1M-row) launch
+    if traffic is not None and rows_rank != N_PATHS * HORIZON:
+        # the committed PMC pass is the default 1-GPU launch (1M rows); scale per row
+        traffic = traffic * rows_rank / (N_PATHS * HORIZON)
     # the roofline that binds the dominant kernel: the larger of its ideal MFMA time
     # (algorithmic flops at the matrix peak of the form it computes in) and its ideal
     # HBM time (algorithmic bytes at 8 TB/s)

@@ -49,34 +49,52 @@ __global__ void __launch_bounds__(256) k_pack_batch(const double* __restrict__ o
 // max |xhat| (>= 1: the bias column) gives xu = 2^E with |xhat / xu| < 1; then
 // hi = f16(y), lo = f16(y - hi) (split8, common.h).  The xhat values are those of
 // k_pack_batch.
-constexpr int PS_MAXC = 8;   // columns per lane (np <= 512)
+constexpr int PS_MAXP = 4;   // column pairs per lane (np <= 512)
 __global__ void __launch_bounds__(256) k_pack_split(const double* __restrict__ obs, const double* __restrict__ act,
                                                     int64_t T, int n, int m, int np,
                                                     const float* __restrict__ in_shift,
                                                     const float* __restrict__ in_scale, _Float16* __restrict__ xs,
                                                     float* __restrict__ xu, float* __restrict__ act32) {
+    // lane l owns the column pairs (2l + 128j, 2l + 128j + 1): 16-byte loads of the f64
+    // row when n is even (8-byte otherwise), 4-byte hi / lo stores
     const int lane = threadIdx.x & 63;
     const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    const int nc = (np + 63) / 64;
+    const int npair = (np + 127) / 128;
+    const bool even = (n & 1) == 0 && (reinterpret_cast<uintptr_t>(obs) & 15) == 0;   // 16-byte pair loads
     for (int64_t row = wid; row < T; row += nw) {
         const double* src = obs + row * n;
-        float v[PS_MAXC];
+        float v[PS_MAXP][2];
         float mx = 0.f;
 #pragma unroll
-        for (int j = 0; j < PS_MAXC; ++j) {
-            const int c = lane + 64 * j;
-            float x = 0.f;
-            if (j < nc) {
-                if (c < n) {
-                    x = (float)src[c];                        // torch .float(): round to nearest
-                    if (in_shift) x = (x - in_shift[c]) / (in_scale[c] + 1e-8f);   // MuNet.forward:177
-                } else if (c == n) {
-                    x = 1.0f;                                 // bias column (zero padding after)
+        for (int j = 0; j < PS_MAXP; ++j) {
+            const int c = 2 * lane + 128 * j;
+            double d0 = 0.0, d1 = 0.0;
+            if (j < npair) {
+                if (even && c + 1 < n) {
+                    const double2 d = *reinterpret_cast<const double2*>(src + c);
+                    d0 = d.x;
+                    d1 = d.y;
+                } else {
+                    if (c < n) d0 = src[c];
+                    if (c + 1 < n) d1 = src[c + 1];
                 }
             }
-            v[j] = x;
-            mx = fmaxf(mx, fabsf(x));
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int ce = c + e;
+                float x = 0.f;
+                if (j < npair) {
+                    if (ce < n) {
+                        x = (float)(e ? d1 : d0);                    // torch .float(): round to nearest
+                        if (in_shift) x = (x - in_shift[ce]) / (in_scale[ce] + 1e-8f);   // MuNet.forward:177
+                    } else if (ce == n) {
+                        x = 1.0f;                                    // bias column (zero padding after)
+                    }
+                }
+                v[j][e] = x;
+                mx = fmaxf(mx, fabsf(x));
+            }
         }
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
@@ -84,13 +102,19 @@ __global__ void __launch_bounds__(256) k_pack_split(const double* __restrict__ o
         const float s = pow2_scale(mx, inv);
         _Float16* dst = xs + row * (2 * (int64_t)np);
 #pragma unroll
-        for (int j = 0; j < PS_MAXC; ++j) {
-            const int c = lane + 64 * j;
-            if (j < nc && c < np) {
-                const float y = v[j] * s;
-                const _Float16 h = (_Float16)y;
-                dst[c] = h;
-                dst[np + c] = (_Float16)(y - (float)h);
+        for (int j = 0; j < PS_MAXP; ++j) {
+            const int c = 2 * lane + 128 * j;
+            if (j < npair && c < np) {
+                typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+                half2v h, l;
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const float y = v[j][e] * s;
+                    h[e] = (_Float16)y;
+                    l[e] = (_Float16)(y - (float)h[e]);
+                }
+                *reinterpret_cast<half2v*>(dst + c) = h;
+                *reinterpret_cast<half2v*>(dst + np + c) = l;
             }
         }
         if (lane == 0) xu[row] = inv;
@@ -415,7 +439,7 @@ int mjrl_pack_batch_split(const double* obs, const double* act, int64_t T, const
                           void* stream) {
     if (!s || T < 0 || (T > 0 && (!obs || !act || !xs || !xu || !act32))) return MJRL_EINVAL;
     if ((in_shift == nullptr) != (in_scale == nullptr)) return MJRL_EINVAL;
-    if (s->np > 64 * PS_MAXC) return MJRL_ESHAPE;
+    if (s->np > 128 * PS_MAXP) return MJRL_ESHAPE;
     if (T == 0) return MJRL_OK;
     const int g = grid_for(T, 4, 8192);
     hipLaunchKernelGGL(k_pack_split, dim3(g), dim3(256), 0, (hipStream_t)stream, obs, act, T, s->n, s->m, s->np,

@@ -367,15 +367,18 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
     // 16 + 16 u: u < NP/128 hi chunks, the rest lo chunks)
     float4 xn[L::XPER];
     float un = 1.f;
-    auto xload = [&](int64_t t_, int tid_) {
+    // pieces u0 .. u1 - 1 (callers split the loads over two phases so the vector
+    // memory issue of the 48 KB tile does not stall one phase)
+    auto xload = [&](int64_t t_, int tid_, int u0 = 0, int u1 = L::XPER) {
         const int64_t rb_ = t_ * BT;
         const int row = tid_ >> 4, c16 = tid_ & 15;
         const bool ok = t_ < ntiles && rb_ + row < T;
         const char* src = reinterpret_cast<const char*>(a.xs) + (ok ? (rb_ + row) * (4 * NP) : 0);
 #pragma unroll
         for (int u = 0; u < L::XPER; ++u)
-            xn[u] = ok ? *reinterpret_cast<const float4*>(src + 16 * (c16 + 16 * u)) : make_float4(0.f, 0.f, 0.f, 0.f);
-        un = (tid_ < BT && t_ < ntiles && rb_ + tid_ < T) ? a.xu[rb_ + tid_] : 1.f;
+            if (u >= u0 && u < u1)
+                xn[u] = ok ? *reinterpret_cast<const float4*>(src + 16 * (c16 + 16 * u)) : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (u0 == 0) un = (tid_ < BT && t_ < ntiles && rb_ + tid_ < T) ? a.xu[rb_ + tid_] : 1.f;
     };
     xload(blockIdx.x, tid);
     __syncthreads();   // images and scales ready
@@ -392,13 +395,13 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
 #pragma unroll
     for (int s = 0; s < KS; ++s) p1off[s] = r16 * L::RBYTES + 16 * ((kh * (KH / 8) + 4 * s + q) ^ chunk_swz(r16));
     // and the transposed-read offsets of the gW0 sums (group g: rows 8q + tq, chunk
-    // kh*KH/8 + tp/2 + 2g, half tp & 1), kept for FVP (FWD has no registers to spare)
+    // kh*KH/8 + tp/2 + 2g, half tp & 1), kept in registers (FWD / FVP)
     auto gw0_off = [&](int r_, int q_, int g) {
         const int tq = r_ >> 2, tp = r_ & 3, row = 8 * q_ + tq;
         return row * L::RBYTES + 16 * (((kh * KH) / 8 + (tp >> 1) + 2 * g) ^ chunk_swz(row)) + 8 * (tp & 1);
     };
-    int g0off[MODE == FVP ? KG : 1];
-    if constexpr (MODE == FVP) {
+    int g0off[MODE != EVAL ? KG : 1];
+    if constexpr (MODE != EVAL) {
 #pragma unroll
         for (int g = 0; g < KG; ++g) g0off[g] = gw0_off(r16, q, g);
     }
@@ -464,7 +467,6 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
                 if (p) touch[0] = *p;
             }
         }
-        if (MODE == EVAL) xload(tile + gridDim.x, ltid);   // EVAL has no weight-gradient phase
 
         // ---- P1: first layer, partial over this wave's observation half ----
         floatx4 acc1[2] = {zero4(), zero4()};
@@ -507,6 +509,9 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
                 D0[((1 - kh) * 16 + 4 * lq + rr) * L::LD + cb * 16 + lr16] = kh ? acc1[0][rr] : acc1[1][rr];
             __syncthreads();
             KX_STAMP(1);
+            // EVAL has no weight-gradient phase: the next tile's xhat loads go here,
+            // after the first layer's image reads
+            if (MODE == EVAL) xload(tile + gridDim.x, ltid);
             {
                 const int col = cb * 16 + lr16;
                 float av[4];
@@ -659,6 +664,7 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
         }
         if (MODE == EVAL) continue;
 
+        xload(tile + gridDim.x, ltid, 0, L::XPER / 2);   // first half of the next tile's xhat
         // ---- P4: gu1 = (1 - a1^2) (gp W2), wave -> (rb = kh, cb) ----
         {
             const int hcol = cb * 16 + lr16;
@@ -686,7 +692,7 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
         // ---- P5: gu0 = (1 - a0^2) (gu1 W1), times the xhat row scale; beside it the
         // gW1 / gW2 sums (their operands are complete since P4) and the next tile's
         // xhat loads (consumed at the next publish) ----
-        xload(tile + gridDim.x, ltid);
+        xload(tile + gridDim.x, ltid, L::XPER / 2, L::XPER);
         {
             const int hcol = cb * 16 + lr16;
             half8 ah[2], al[2];
@@ -770,7 +776,7 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
                 for (int h = 0; h < 2; ++h) {
                     // rows 8q + 4h + tq: the chunk swizzle ignores row bit 2, so h = 1 is
                     // the h = 0 offset plus four rows
-                    const int off = (MODE == FVP ? g0off[g] : gw0_off(lr16, lq, g)) + h * 4 * L::RBYTES;
+                    const int off = g0off[g] + h * 4 * L::RBYTES;
                     th[h] = ds_read_tr16(XHb + off);
                     tl[h] = ds_read_tr16(XLb + off);
                 }

@@ -127,6 +127,17 @@ __device__ __forceinline__ float aval(const char* img, int f, int row) {
     return mix_add_lo(*reinterpret_cast<const unsigned short*>(img + off),
                       *reinterpret_cast<const unsigned short*>(img + AIMG_BYTES + off));
 }
+// a at (feature f, rows row0 .. row0 + 3), row0 % 4 == 0: one 8-byte read each of hi and lo
+__device__ __forceinline__ void aval4(const char* img, int f, int row0, float (&v)[4]) {
+    typedef unsigned uint2v __attribute__((ext_vector_type(2)));
+    const int off = aoff(f, row0);
+    const uint2v h = *reinterpret_cast<const uint2v*>(img + off);
+    const uint2v l = *reinterpret_cast<const uint2v*>(img + AIMG_BYTES + off);
+    v[0] = mix_add_lo(h[0], l[0]);
+    v[1] = mix_add_hi(h[0], l[0]);
+    v[2] = mix_add_lo(h[1], l[1]);
+    v[3] = mix_add_hi(h[1], l[1]);
+}
 // store 4 consecutive rows (row0..row0+3, row0 % 4 == 0) of feature f into an activation image
 __device__ __forceinline__ void astore4(char* img, int f, int row0, const float (&v)[4]) {
     typedef _Float16 half4 __attribute__((ext_vector_type(4)));
@@ -389,6 +400,9 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
     kx_acc_[17] = 1;
 #endif
 
+    // FVP: P1's partials carry the W1c column scale of their unit (both powers of two:
+    // exact), so P2 folds them without it
+    const float wsc1 = MODE == FVP ? wsc * sc1[cb * 16 + r16] : wsc;
     // P1's xhat-image offsets (row r16, chunk kh*KH/8 + 4s + q, swizzled): tile-invariant,
     // kept in KS registers instead of being recomputed per tile
     int p1off[KS];
@@ -485,7 +499,7 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
-                for (int rr = 0; rr < 4; ++rr) acc1[i][rr] *= Us[i * 16 + 4 * lq + rr] * wsc;
+                for (int rr = 0; rr < 4; ++rr) acc1[i][rr] *= Us[i * 16 + 4 * lq + rr] * wsc1;
         }
         if (MODE == FVP) {
             // FVP: both observation-half partials go to LDS whole (kh = 0 -> D0, kh = 1 ->
@@ -543,7 +557,7 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
                     arow(A0i, kh, s, lq, lr16, xh[s], xl[s]);
                     const int o = (kh * 16 + lr16) * L::LD + 32 * s + 8 * lq;
                     const float8v av = hilo8(xh[s], xl[s]);
-                    dv[s] = ((load8(D0 + o) + load8(D0B + o)) * (1.f - av * av)) * load8(sc1 + 32 * s + 8 * lq);
+                    dv[s] = (load8(D0 + o) + load8(D0B + o)) * (1.f - av * av);   // W1c column scale folded in P1
                     mx = fmaxf(mx, absmax8(dv[s]));
                 }
                 const float sc = pow2_scale(max_over_groups(mx), rinv);
@@ -677,11 +691,12 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
             wcol(S3, L::WIMG2, cb, 0, lq, lr16, bh, bl);
             const floatx4 acc = mfma_x3(ah[0], al[0], bh, bl, zero4());
             const float csc = sc3[hcol];
-            float gv[4];
+            float gv[4], a4[4];
+            if (MODE != FVP) aval4(A1i, hcol, kh * 16 + 4 * lq, a4);
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr) {
                 const int row = kh * 16 + 4 * lq + rr;
-                const float av = MODE == FVP ? pa1[rr] : aval(A1i, hcol, row);
+                const float av = MODE == FVP ? pa1[rr] : a4[rr];
                 gv[rr] = (1.f - av * av) * (acc[rr] * ri[rr] * csc);
                 D0[row * L::LD + hcol] = gv[rr];   // G1
             }
@@ -708,11 +723,12 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
                 acc = mfma_x3(ah[s], al[s], bh, bl, acc);
             }
             const float csc = sc1[hcol];
-            float gv[4];
+            float gv[4], a4[4];
+            aval4(A0i, hcol, kh * 16 + 4 * lq, a4);
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr) {
                 const int row = kh * 16 + 4 * lq + rr;
-                const float av = aval(A0i, hcol, row);
+                const float av = a4[rr];
                 gv[rr] = (1.f - av * av) * (acc[rr] * ri[rr] * csc) * Us[row];
             }
             *reinterpret_cast<float4*>(D1 + hcol * L::LDT + kh * 16 + 4 * lq) = make_float4(gv[0], gv[1], gv[2], gv[3]);

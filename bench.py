@@ -111,6 +111,17 @@ def baseline_coeffs():
     return b
 
 
+def initial_theta():
+    """The update's starting parameters: N(0, 0.05^2) weights from RandomState(0)
+    in trainable_params order, log_std 0."""
+    rs = np.random.RandomState(0)
+    theta = np.concatenate([(rs.randn(int(np.prod(s))) * 0.05).ravel()
+                            for s in [(HIDDEN[0], N_OBS), (HIDDEN[0],), (HIDDEN[1], HIDDEN[0]), (HIDDEN[1],),
+                                      (N_ACT, HIDDEN[1]), (N_ACT,), (N_ACT,)]]).astype(np.float32)
+    theta[-N_ACT:] = 0.0
+    return theta
+
+
 def stage_shard(p0, p1, device, base):
     from mjrl_amd.engine import DeviceBatch
     obs, act, rew = make_paths(p0, p1)
@@ -236,12 +247,7 @@ def main():
     T_total = args.paths * HORIZON
 
     eng = UpdateEngine(N_OBS, N_ACT, HIDDEN, device=device, comm=comm, precision=args.precision)
-    rs = np.random.RandomState(0)
-    theta = np.concatenate([(rs.randn(int(np.prod(s))) * 0.05).ravel()
-                            for s in [(HIDDEN[0], N_OBS), (HIDDEN[0],), (HIDDEN[1], HIDDEN[0]), (HIDDEN[1],),
-                                      (N_ACT, HIDDEN[1]), (N_ACT,), (N_ACT,)]]).astype(np.float32)
-    theta[-N_ACT:] = 0.0
-    th = torch.from_numpy(theta).to(device)
+    th = torch.from_numpy(initial_theta()).to(device)
     upd = dict(algo="npg", gamma=GAMMA, gae_lambda=LAM, n_step_size=DELTA, cg_iters=CG_ITERS, damping=DAMPING,
                T_global=float(T_total))
 

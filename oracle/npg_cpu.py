@@ -349,10 +349,52 @@ def cg_rows(c):
     return [np.random.choice(N, size=int(frac * N)) for _ in range(k)]
 
 
+def regen_inputs(seed, n, m, lengths):
+    """The synthetic paths of tests/golden/make_golden.py:make_paths, replayed from
+    np.random.RandomState(seed) (legacy stream, stable across numpy versions): per
+    path obs randn(H, n) and act randn(H, m) rounded to f32, then rewards randn(H)."""
+    rs = np.random.RandomState(int(seed))
+    obs, act, rew = [], [], []
+    for H in lengths:
+        obs.append(rs.randn(int(H), n).astype(np.float32))
+        act.append(rs.randn(int(H), m).astype(np.float32))
+        rew.append(rs.randn(int(H)))
+    return np.concatenate(obs), np.concatenate(act), np.concatenate(rew)
+
+
+def _sha(*arrs):
+    import hashlib
+    return hashlib.sha256(b"".join(np.ascontiguousarray(a).tobytes() for a in arrs)).hexdigest()
+
+
+_CASES = {}
+
+
 def load_case(path):
-    """Loads a golden fixture into oracle-ready arrays."""
+    """Loads a golden fixture into oracle-ready arrays (cached per path: treat the
+    returned arrays as read-only).
+
+    Large fixtures (gen_seed present) do not store their inputs: obs / act /
+    rewards are replayed with regen_inputs and checked against the stored
+    inputs_sha256; returns / advantages are recomputed by returns_and_advantages
+    and checked bit for bit against the hashes of the reference's own arrays."""
+    if path in _CASES:
+        return _CASES[path]
     z = np.load(path, allow_pickle=False)
     c = {k: z[k] for k in z.files}
+    if "gen_seed" in c:
+        n, m = int(c["n"]), int(c["m"])
+        c["obs"], c["act"], c["rewards"] = regen_inputs(c["gen_seed"], n, m, c["lengths"])
+        if _sha(c["obs"], c["act"], c["rewards"]) != str(c["inputs_sha256"]):
+            raise ValueError("%s: regenerated inputs do not match the fixture's checksum" % path)
+        lam = None if np.isnan(c["gae_lambda"]) else float(c["gae_lambda"])
+        c["returns"], c["advantages"] = returns_and_advantages(c["rewards"], c["baseline"], c["lengths"],
+                                                               c["terminated"].astype(bool), float(c["gamma"]),
+                                                               lam)
+        for k in ("returns", "advantages"):
+            if _sha(c[k]) != str(c[k + "_sha256"]):
+                raise ValueError("%s: recomputed %s differ from the reference's" % (path, k))
+        c["_regen_keys"] = np.array(["obs", "act", "rewards", "returns", "advantages"])
     c["obs64"] = c["obs"].astype(np.float64)
     c["act64"] = c["act"].astype(np.float64)
     hidden = tuple(int(h) for h in c["hidden"])
@@ -361,6 +403,7 @@ def load_case(path):
     if "in_shift" in c:
         tr = (c["in_shift"], c["in_scale"], c["out_shift"], c["out_scale"])
     c["transforms"] = tr
+    _CASES[path] = c
     return c
 
 

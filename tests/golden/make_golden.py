@@ -57,7 +57,7 @@ import mjrl.utils.process_samples as process_samples  # noqa: E402
 from mjrl.utils.cg_solve import cg_solve as ref_cg_solve  # noqa: E402
 
 OUT = os.path.dirname(os.path.abspath(__file__))
-CG_KEEP = 3
+MEAN_ROWS = 2000   # regenerated cases keep the first MEAN_ROWS rows of mean0 / ll0
 
 
 def make_paths(rs, n, m, lengths, terminated):
@@ -77,7 +77,7 @@ def make_paths(rs, n, m, lengths, terminated):
 class Recorder:
     """Wraps agent methods / cg_solve to record what the reference computes."""
 
-    def __init__(self, agent, modules):
+    def __init__(self, agent, modules, exact_ls=False):
         self.agent = agent
         self.surr = []
         self.kl = []
@@ -112,6 +112,16 @@ class Recorder:
 
             def f(p):
                 z = f_Ax(p)
+                if exact_ls:
+                    # the log-std block of the reference's double-backprop HVP is the
+                    # closed-form curvature c(sigma) plus f32
+                    # rounding of its T-row sums (+-5e-7 per element at T = 60k);
+                    # this variant puts the exact c(sigma) there, nothing else changes
+                    m_ = len(a.policy.log_std_val)
+                    s2 = np.exp(2.0 * np.asarray(a.policy.log_std_val, np.float64))
+                    cs = np.float32(4 * s2 * (2 * s2 - 1e-8) / (2 * s2 + 1e-8) ** 2)
+                    z = np.array(z, copy=True)
+                    z[-m_:] = cs * p[-m_:] + np.float32(a.FIM_invert_args["damping"]) * p[-m_:]
                 trace["p"].append(np.array(p, copy=True))
                 trace["z"].append(np.array(z, copy=True))
                 return z
@@ -138,18 +148,27 @@ ONLY = set(sys.argv[1:])   # optional: regenerate only the named cases
 
 
 def run_case(name, reverse_alt=True, **kw):
-    """Runs the reference at 1 torch thread (the fixture), again at 8 threads, and
-    again at 1 thread with the path order reversed (the same batch, every sum over
-    timesteps reordered).  The largest difference to the fixture (the reference's
-    own reduction-order sensitivity) is stored as spread_*
-    and calibrates the end-to-end tolerances of the GPU parity tests."""
+    """Runs the reference at 1 torch thread (the fixture), again at 8 and at 3
+    threads, and again at 1 thread with the path order reversed and with two
+    random path permutations (the same batch, every sum over timesteps
+    reordered).  The largest difference to the fixture (the reference's own
+    reduction-order sensitivity) is stored as spread_* and
+    calibrates the end-to-end tolerances of the GPU parity tests."""
     if ONLY and name not in ONLY:
         return None
-    torch.set_num_threads(8)
-    alts = [_run(None, **kw)]
+    alts = []
+    for threads in (8, 3):
+        torch.set_num_threads(threads)
+        alts.append(_run(None, **kw))
     torch.set_num_threads(1)
-    if reverse_alt:   # (a subsampled Fisher draws other rows once reversed: no reversal there)
+    if reverse_alt:   # (a subsampled Fisher draws other rows once reordered: no reordering there)
         alts.append(_run(None, reverse=True, **kw))
+        for ps in (1, 2):
+            alts.append(_run(None, perm_seed=ps, **kw))
+    # the reference's own CG on its own FVP, with the exact log-std curvature in place
+    # of the f32-rounded one: the fp32 CG amplifies that rounding (DESIGN.md §5), so an
+    # implementation with an exact log-std block lands this far from the reference
+    alts.append(_run(None, exact_ls=True, **kw))
     out = _run(name, alt=alts, **kw)
     _err64(name, out)
     return out
@@ -170,8 +189,9 @@ def _err64(name, out):
     r = O.update(pol, c["obs64"], c["act64"], c["advantages"], c["rewards"], c["lengths"], **kw)
     rel = lambda a, b: abs(float(a) / float(b) - 1.0) if float(b) != 0 else abs(float(a))
     z = dict(c)
-    for k in ("obs64", "act64", "hidden_t", "transforms"):
+    for k in ("obs64", "act64", "hidden_t", "transforms") + tuple(str(k) for k in c.get("_regen_keys", ())):
         z.pop(k)
+    z.pop("_regen_keys", None)
     z["err64_x"] = _nrel(c["cg_x"], r["npg_grad"])
     z["err64_theta"] = _nrel(c["theta1"], r["theta1"])
     z["err64_alpha"] = rel(c["log_alpha"], r["alpha"])
@@ -191,7 +211,7 @@ def _nrel(a, b):
 def _run(name, *, n, m, hidden, lengths, terminated, algo, algo_kwargs,
          gamma=0.995, gae_lambda=0.97, seed=123, policy_seed=0,
          log_std=None, transforms=None, demo=None, linear=False,
-         baseline_fit=True, alt=None, reverse=False, np_seed=None):
+         baseline_fit=True, alt=None, reverse=False, np_seed=None, regen=False, perm_seed=None, exact_ls=False):
     rs = np.random.RandomState(seed)
     spec = EnvSpec(n, m, max(lengths), 1)
     if linear:
@@ -213,6 +233,9 @@ def _run(name, *, n, m, hidden, lengths, terminated, algo, algo_kwargs,
     if reverse:
         paths = paths[::-1]
         demo_paths = demo_paths[::-1] if demo_paths is not None else None
+    if perm_seed is not None:
+        order = np.random.RandomState(1000 + perm_seed).permutation(len(paths))
+        paths = [paths[i] for i in order]
     baseline = LinearBaseline(spec)
     if baseline_fit:
         process_samples.compute_returns(paths, gamma)
@@ -240,7 +263,7 @@ def _run(name, *, n, m, hidden, lengths, terminated, algo, algo_kwargs,
     # the update proper (batch_reinforce.py:86-91 minus sampling and fit)
     process_samples.compute_returns(paths, gamma)
     process_samples.compute_advantages(paths, baseline, gamma, gae_lambda)
-    rec = Recorder(agent, [npg_mod, trpo_mod, dapg_mod])
+    rec = Recorder(agent, [npg_mod, trpo_mod, dapg_mod], exact_ls=exact_ls)
     if np_seed is not None:
         np.random.seed(np_seed)
     try:
@@ -248,7 +271,6 @@ def _run(name, *, n, m, hidden, lengths, terminated, algo, algo_kwargs,
     finally:
         rec.restore()
     theta1 = policy.get_param_values()
-    keep = len(rec.cg["p"]) if policy.d <= 10000 else CG_KEEP
 
     out = dict(
         spread_x=max(_nrel(a["cg_x"], rec.cg["x"]) for a in alt) if alt else 0.0,
@@ -274,13 +296,30 @@ def _run(name, *, n, m, hidden, lengths, terminated, algo, algo_kwargs,
         hvp_v=hvp_v, hvp_out=hvp_out,
         surr_calls=np.array(rec.surr), kl_calls=np.array(rec.kl),
         vpg_grad=rec.vpg[0],
-        # large-d cases keep the first CG_KEEP iterations of the trace (fixture size)
-        cg_b=rec.cg["b"], cg_p=np.array(rec.cg["p"][:keep]), cg_z=np.array(rec.cg["z"][:keep]),
+        # the whole CG trace: every iteration is teacher-forced by the parity tests
+        cg_b=rec.cg["b"], cg_p=np.array(rec.cg["p"]), cg_z=np.array(rec.cg["z"]),
         cg_iters_run=len(rec.cg["p"]),
         cg_x=rec.cg["x"],
         base_stats=np.array(base_stats, dtype=np.float64),
         running_score=agent.running_score,
     )
+    if regen:
+        # large cases: the inputs are NOT stored.  oracle.npg_cpu.regen_inputs replays
+        # make_paths' RandomState stream from gen_seed and load_case checks the
+        # result against inputs_sha256; returns / advantages are recomputed by the
+        # pinned oracle and checked bit for bit against the reference's hashes
+        import hashlib
+        sha = lambda *arrs: hashlib.sha256(b"".join(np.ascontiguousarray(a).tobytes() for a in arrs)).hexdigest()
+        out["gen_seed"] = np.int64(seed)
+        out["inputs_sha256"] = np.array(sha(out["obs"], out["act"], out["rewards"]))
+        for k in ("returns", "advantages"):
+            out[k + "_sha256"] = np.array(sha(out[k]))
+            out[k + "_head"] = out[k][:256]
+            del out[k]
+        for k in ("obs", "act", "rewards"):
+            del out[k]
+        out["mean0"] = out["mean0"][:MEAN_ROWS]
+        out["ll0"] = out["ll0"][:MEAN_ROWS]
     if np_seed is not None:
         out["np_seed"] = np.int64(np_seed)
         out["hvp_np_seed"] = np.int64(np_seed + 1)
@@ -348,10 +387,12 @@ def main():
              lengths=[300] * 4, terminated=[False] * 4, algo="trpo",
              algo_kwargs=dict(kl_dist=2.0), seed=77,
              log_std=np.linspace(-1.0, 0.5, 6))
-    # C4: Humanoid shape (obs 376, act 17), reduced to 4 x 250
+    # C4: Humanoid shape (obs 376, act 17), 60 x 1000 rows: T = 60,000 >= 2 d
+    # (d = 29,410), so the Fisher is well conditioned and the reference's own
+    # end-to-end spread is small (the 4 x 250 case of round 1 had T < d)
     run_case("c4_humanoid", n=376, m=17, hidden=(64, 64),
-             lengths=[250] * 4, terminated=[False] * 4, algo="npg",
-             algo_kwargs=dict(normalized_step_size=0.01))
+             lengths=[1000] * 60, terminated=[False] * 60, algo="npg",
+             algo_kwargs=dict(normalized_step_size=0.01), regen=True)
     # C5: door shape, DAPG with BC-style in/out transformations and demos
     rs = np.random.RandomState(9)
     n, m = 39, 28

@@ -50,7 +50,7 @@ def make_policy(c):
 
 
 def tol(c, key, floor):
-    return max(floor, 3.0 * float(c["spread_" + key]), 2.0 * float(c["err64_" + key]))
+    return max(floor, 3.0 * float(c["spread_" + key]))
 
 
 def make_agent(name, c, pol, spec):

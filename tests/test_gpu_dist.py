@@ -82,7 +82,7 @@ def test_two_rank_update(name):
     th0, th1 = out[0][0], out[1][0]
     assert np.array_equal(th0, th1)                     # replicated parameters
     np.testing.assert_allclose(out[0][1], c["base_stats"], rtol=1e-10)
-    tol = max(1e-3, 3 * float(c["spread_theta"]), 2 * float(c["err64_theta"]))
+    tol = max(1e-3, 3 * float(c["spread_theta"]))
     assert np.linalg.norm(th0 - c["theta1"]) / np.linalg.norm(c["theta1"]) < tol
-    ktol = max(2e-3, 3 * float(c["spread_kl"]), 2 * float(c["err64_kl"]))
+    ktol = max(2e-3, 3 * float(c["spread_kl"]))
     np.testing.assert_allclose(out[0][2], c["log_kl_dist"], rtol=ktol)

@@ -11,13 +11,17 @@ Tolerances (the bar written per stage):
   post-step eval (teacher-forced) surrogate / KL at OUR new params vs the oracle
                                 evaluated at those same params: rtol 1e-4
   end-to-end npg_grad / theta / alpha / kl / surr improvement vs the reference:
-      tol = max(floor, 3 x spread_*, 2 x err64_*) where, stored in each fixture,
-        spread_* = the reference's own change between 1 and 8 torch threads and
-                   between path orders (same batch, reordered sums), and
-        err64_*  = the reference's own distance to an fp64 evaluation of the update;
-      floors: npg_grad / theta 1e-3, alpha / kl / surr 2e-3.  The fp32 CG amplifies
-      reduction-order noise by the conditioning of F: on the
-      reduced c4 fixture (T=1000 < d) the reference's npg_grad is 14% from fp64.
+      tol = max(floor, 3 x spread_*) where spread_* (stored in each fixture) is the
+      reference's own change between 1 and 8 torch threads and between path
+      orders (the same batch, every sum over timesteps reordered); floors:
+      npg_grad / theta 1e-3, alpha / kl / surr 2e-3.  The fp32 CG amplifies
+      reduction-order noise by the conditioning of F, so only
+      c1_pointmass_mlp32 and c2_ragged (the reference's own spread is 0.5-6 %)
+      get a tolerance above the floor.  The fp64 evaluation of the update is NOT
+      a tolerance source: on c4_humanoid (60 x 1000 rows, T >= 2d) the noise-free
+      fp64 CG lands 15 % from the reference while the reference, an fp32 CG on an
+      fp64 FVP, and an fp64 CG on an FVP with 1e-7 relative noise all agree to
+      1e-4..4e-4 — the reference's answer is the robust one.
 """
 import os
 
@@ -112,7 +116,7 @@ def test_update_matches_reference(name, precision):
                                atol=1e-7)
     g = eng.vec["g"].cpu().numpy()
     assert nrel(g, c["cg_b"]) < 1e-5, nrel(g, c["cg_b"])
-    tol = lambda key, floor: max(floor, 3.0 * float(c["spread_" + key]), 2.0 * float(c["err64_" + key]))
+    tol = lambda key, floor: max(floor, 3.0 * float(c["spread_" + key]))
     x = eng.vec["x"].cpu().numpy() if kw["algo"] != "vpg" else g
     assert nrel(x, c["cg_x"]) < tol("x", 1e-3), nrel(x, c["cg_x"])
     th1 = eng.vec["theta_new"].cpu().numpy()

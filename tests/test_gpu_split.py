@@ -141,3 +141,36 @@ def test_split_eval_matches_f32():
         out[prec] = eng.eval_pass(torch.from_numpy(theta1).cuda(), T)
     np.testing.assert_allclose(out["split"][0], out["f32"][0], rtol=1e-5, atol=1e-8)
     np.testing.assert_allclose(out["split"][1], out["f32"][1], rtol=1e-4, atol=1e-9)
+
+
+def test_split_accuracy_vs_fp64_bench_workload():
+    """The bench's own workload (Humanoid shape, 1,000 paths x 1,000 steps, the
+    same seeded synthetic obs / act and the same initial parameters as bench.py):
+    VPG and F v of the split-f16 kernels against fp64 truth at the full 1M rows,
+    beside the exact-f32 kernels' error on the same data."""
+    import bench
+    from mjrl_amd.engine import UpdateEngine
+    obs, act, _ = bench.make_paths(0, bench.N_PATHS)
+    obs = np.concatenate(obs)
+    act = np.concatenate(act)
+    T = obs.shape[0]
+    assert T == 1_000_000
+    rs = np.random.RandomState(3)
+    adv = rs.randn(T)
+    theta = bench.initial_theta()
+    v = (rs.randn(theta.size) * 1e-3).astype(np.float32)
+    vpg64, fv64 = _truth(obs, act, adv, theta, v, 1e-4)
+    errs = {}
+    for prec in ("f32", "split"):
+        eng = UpdateEngine(N, M, H, device="cuda:0", precision=prec)
+        eng.load_rows(obs, act, adv)
+        g = eng.forward_pass(torch.from_numpy(theta).cuda(), T).cpu().numpy()
+        fv = eng.fvp(torch.from_numpy(v).cuda(), damping=1e-4, T=T).cpu().numpy()
+        errs[prec] = (nrel(g, vpg64), nrel(fv, fv64))
+        del eng
+        torch.cuda.empty_cache()
+    print("1M split vs fp64:", errs)
+    for i, what in enumerate(("vpg", "fvp")):
+        e32, esp = errs["f32"][i], errs["split"][i]
+        assert esp < 1e-6, (what, errs)
+        assert esp < 4 * e32 + 2e-8, (what, errs)

@@ -68,7 +68,8 @@ def test_policy_forward_and_grads(name):
     pol = O.Policy(int(c["n"]), int(c["m"]), c["hidden_t"], c["theta0"], c["transforms"])
     assert pol.d == c["theta0"].size
     assert list(pol.sizes) == list(c["param_sizes"])
-    mu, ll = pol.mean_ll(pol.new, c["obs64"], c["act64"])
+    k = len(c["mean0"])   # regenerated (large) fixtures keep the first rows only
+    mu, ll = pol.mean_ll(pol.new, c["obs64"][:k], c["act64"][:k])
     assert nrel(mu.detach().numpy(), c["mean0"]) < 1e-6
     assert nrel(ll.detach().numpy(), c["ll0"]) < 1e-6
     kw = O.case_kwargs(c)

@@ -6,13 +6,23 @@ host CPUs with the reference's samplers, returns + GAE, the policy update, then
 baseline.fit on the paths.  Here the paths are staged into HBM once; the GAE
 scan, the whole update and the statistics run on the GPU; returns / baseline /
 advantages are written back into the path dicts for baseline.fit.
+
+Several GPUs (one process per GPU, e.g. an unchanged train_agent script under
+`torchrun --nproc-per-node 8`): the communicator comes from comm.auto_comm();
+rank r samples its ceil(N / world) share of the N paths with the pegasus seed
+offset of that share (the per-worker split of trajectory_sampler.py:37-45), the
+update all-reduces its sums over RCCL, every rank ends with the same
+parameters, and the baseline is fitted on the union of the shards.
 """
 import logging
 import time as timer
 
+import multiprocessing as mp
+
 import numpy as np
 import torch
 
+from ..comm import LocalComm, auto_comm, partition_paths, shard_count
 from ..engine import DeviceBatch, UpdateEngine
 from ..utils.logger import DataLog
 
@@ -54,14 +64,27 @@ class BatchREINFORCE:
         d = dict(self.__dict__)
         d["_engine"] = None
         d["_last_batch"] = None   # device tensors
+        if not isinstance(d.get("_comm"), (LocalComm, type(None))):
+            d["_comm"] = None     # a process group does not pickle; re-resolved on use
         return d
 
     def engine(self):
         if self._engine is None:
-            self._engine = UpdateEngine(self.policy.n, self.policy.m, self.policy.hidden, device=self._device,
-                                        comm=self._comm, min_log_std=self.policy.min_log_std)
+            comm = self.comm()
+            device = self._device
+            if device is None:   # the current device (auto_comm made cuda:LOCAL_RANK current)
+                device = torch.device("cuda", torch.cuda.current_device())
+            self._engine = UpdateEngine(self.policy.n, self.policy.m, self.policy.hidden, device=device,
+                                        comm=comm, min_log_std=self.policy.min_log_std)
         self._engine.set_transformations(*self.policy.transformations())
         return self._engine
+
+    def comm(self):
+        """The agent's communicator: the one passed in, else comm.auto_comm()
+        (torch.distributed's group under torchrun, LocalComm otherwise)."""
+        if self._comm is None:
+            self._comm = auto_comm()
+        return self._comm
 
     def _theta(self, old=False):
         params = self.policy.old_params if old else self.policy.trainable_params
@@ -103,8 +126,12 @@ class BatchREINFORCE:
             print("sample_mode in NPG must be either 'trajectories' or 'samples'")
             quit()
         trajectory_sampler, batch_sampler = _samplers()
+        comm = self.comm()
         ts = timer.time()
-        if sample_mode == "trajectories":
+        if comm.world_size > 1:
+            paths = self._sample_shard(trajectory_sampler, batch_sampler, comm, N, sample_mode, env_name, T,
+                                       num_cpu)
+        elif sample_mode == "trajectories":
             paths = trajectory_sampler.sample_paths_parallel(N, self.policy, T, env_name, self.seed, num_cpu)
         else:
             paths = batch_sampler.sample_paths(N, self.policy, T, env_name=env_name, pegasus_seed=self.seed,
@@ -125,15 +152,45 @@ class BatchREINFORCE:
             self._fit_baseline(paths)
         return eval_statistics
 
+    def _sample_shard(self, trajectory_sampler, batch_sampler, comm, N, sample_mode, env_name, T, num_cpu):
+        """This rank's share of the sampling.  'trajectories': shard_count(N) paths
+        with pegasus seed `seed + first` (the offset trajectory_sampler.py:40-44
+        gives worker i); 'samples': ceil(N / world) timesteps with seed `seed + r N`
+        (disjoint per rank: batch_sampler.py:41-48 advances its seed by at most
+        the paths it draws, fewer than N).  num_cpu='max' becomes this rank's share
+        of the host cores."""
+        if num_cpu is None or num_cpu == "max":
+            num_cpu = max(1, mp.cpu_count() // comm.world_size)
+        if sample_mode == "trajectories":
+            n_r, first = shard_count(N, comm.world_size, comm.rank)
+            if n_r == 0:
+                raise ValueError("train_step(N=%d) on %d ranks: every rank needs at least one path"
+                                 % (N, comm.world_size))
+            seed = self.seed + first if self.seed is not None else None
+            return trajectory_sampler.sample_paths_parallel(n_r, self.policy, T, env_name, seed, num_cpu)
+        n_r = int(np.ceil(N / comm.world_size))
+        seed = self.seed + comm.rank * N if self.seed is not None else None
+        return batch_sampler.sample_paths(n_r, self.policy, T, env_name=env_name, pegasus_seed=seed,
+                                          num_cpu=num_cpu)
+
     def _fit_baseline(self, paths, return_errors=False):
         """baseline.fit(paths) (batch_reinforce.py:93-101).  A LinearBaseline is
         fitted on the device from the batch still in HBM (its Gram products are
-        the T x k work); other baselines fit on the host."""
+        the T x k work); other baselines fit on the host.
+        Sharded (world > 1), every rank fits on the union of all ranks' paths:
+        the LinearBaseline Gram is all-reduced on device, a baseline with ridge
+        normal equations (_features / _reg_coeff: Quadratic) all-reduces its
+        host F^T F, F^T y and error sums, a device MLPBaseline all-reduces its
+        minibatch gradients, and any other baseline gets the union of the paths
+        (all_gather of observations / rewards / returns)."""
         batch = getattr(self, "_last_batch", None)
+        self._last_batch = None
+        comm = self.comm()
         if batch is not None and type(self.baseline).__name__ == "LinearBaseline" \
                 and hasattr(self.baseline, "_reg_coeff") and batch.T == sum(len(p["rewards"]) for p in paths):
-            self._last_batch = None
             return self.engine().fit_linear_baseline(batch, self.baseline, return_errors=return_errors)
+        if comm.world_size > 1:
+            return _fit_sharded(self.baseline, paths, comm, return_errors)
         return self.baseline.fit(paths, return_errors=return_errors) if return_errors else self.baseline.fit(paths)
 
     def train_from_samples(self, paths, gamma, gae_lambda):
@@ -163,6 +220,16 @@ class BatchREINFORCE:
     # ---- hooks for subclasses ---------------------------------------------------
     def _demo_paths(self):
         return None
+
+    def _rank_share(self, paths):
+        """This rank's contiguous share of paths every rank holds (DAPG demos):
+        partition_paths by length, so the demo rows enter the all-reduced VPG sum
+        once, not world-size times (dapg.py:68-70, 97-98)."""
+        comm = self.comm()
+        if not paths or comm.world_size <= 1:
+            return paths
+        p0, p1 = partition_paths([len(p["observations"]) for p in paths], comm.world_size)[comm.rank]
+        return paths[p0:p1]
 
     def _update_args(self):
         return dict(algo="vpg", learn_rate=self.alpha)
@@ -209,3 +276,60 @@ class BatchREINFORCE:
         self.logger.log_kv("stoc_pol_std", np.std(path_returns))
         self.logger.log_kv("stoc_pol_max", np.amax(path_returns))
         self.logger.log_kv("stoc_pol_min", np.amin(path_returns))
+
+
+def _fit_sharded(baseline, paths, comm, return_errors):
+    """baseline.fit on the union of every rank's paths (see _fit_baseline)."""
+    if hasattr(baseline, "fit_sharded"):
+        return baseline.fit_sharded(paths, comm, return_errors=return_errors)
+    if hasattr(baseline, "_features") and hasattr(baseline, "_reg_coeff") and hasattr(baseline, "_coeffs"):
+        return _fit_normal_equations(baseline, paths, comm, return_errors)
+    import torch.distributed as dist
+    keep = ("observations", "rewards", "returns", "terminated")
+    mine = [{k: p[k] for k in keep if k in p} for p in paths]
+    parts = [None] * comm.world_size
+    dist.all_gather_object(parts, mine, group=comm.group)
+    union = [p for part in parts for p in part]
+    return baseline.fit(union, return_errors=return_errors) if return_errors else baseline.fit(union)
+
+
+def _fit_normal_equations(baseline, paths, comm, return_errors):
+    """Ridge normal-equation baselines (linear_baseline.py:20-44,
+    quadratic_baseline.py:40-65): F^T F, F^T y, y^T y and the error sums are sums
+    over timesteps, all-reduced in fp64; then the reference's lstsq retry loop."""
+    feats = baseline._features(paths) if _features_take_paths(baseline) else \
+        np.concatenate([baseline._features(p) for p in paths])
+    y = np.concatenate([p["returns"] for p in paths])
+    k = feats.shape[1]
+    dev = _comm_device(comm)
+    pre = feats.dot(baseline._coeffs) if (return_errors and baseline._coeffs is not None) else np.zeros_like(y)
+    st = np.concatenate([feats.T.dot(feats).ravel(), feats.T.dot(y), [y.dot(y), ((y - pre) ** 2).sum()]])
+    t = torch.from_numpy(st).to(dev)
+    comm.allreduce_sum(t)
+    st = t.cpu().numpy()
+    FtF, Fty, yy, sse0 = st[:k * k].reshape(k, k), st[k * k:k * k + k], st[-2], st[-1]
+    reg = baseline._reg_coeff
+    for _ in range(10):
+        c = np.linalg.lstsq(FtF + reg * np.identity(k), Fty, rcond=None)[0]
+        baseline._coeffs = c
+        if not np.any(np.isnan(c)):
+            break
+        reg *= 10
+    if return_errors:
+        t = torch.tensor([((y - feats.dot(baseline._coeffs)) ** 2).sum()], dtype=torch.float64, device=dev)
+        comm.allreduce_sum(t)
+        return sse0 / yy, float(t.item()) / yy
+
+
+def _features_take_paths(baseline):
+    """Quadratic / MLP baselines take a list of paths, Linear one path."""
+    return type(baseline).__name__ != "LinearBaseline"
+
+
+def _comm_device(comm):
+    """Where collective buffers live: the current GPU under RCCL, CPU under gloo."""
+    try:
+        backend = comm.dist.get_backend(comm.group)
+    except Exception:
+        backend = "gloo"
+    return torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")

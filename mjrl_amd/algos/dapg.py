@@ -35,7 +35,9 @@ class DAPG(NPG):
         return self.demo_paths is not None and self.lam_0 > 0.0
 
     def _demo_paths(self):
-        return self.demo_paths if self._use_demos() else None
+        """The demonstrations this rank stages: all of them on one process, its
+        share under several ranks (each demo row enters the all-reduced sum once)."""
+        return self._rank_share(self.demo_paths) if self._use_demos() else None
 
     def _update_args(self):
         args = dict(algo="dapg", kl_dist=self.kl_dist, cg_iters=self.FIM_invert_args["iters"],

@@ -73,6 +73,57 @@ def default_comm():
     return LocalComm()
 
 
+def launched_world():
+    """(rank, world_size, local_rank) from a torchrun-style environment, or None
+    when the process was not launched as one of several ranks."""
+    import os
+    try:
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+    except ValueError:
+        return None
+    if world <= 1 or "RANK" not in os.environ:
+        return None
+    return int(os.environ["RANK"]), world, int(os.environ.get("LOCAL_RANK", os.environ["RANK"]))
+
+
+def auto_comm(backend=None):
+    """The communicator an agent uses when the caller passed none.
+
+    - torch.distributed already initialised with world size > 1: that group;
+    - launched by torchrun (RANK / WORLD_SIZE / MASTER_ADDR in the environment)
+      but not initialised: initialise it here — RCCL ("nccl") on cuda:LOCAL_RANK
+      when a GPU is visible, gloo otherwise — so an unchanged training script
+      (mjrl/utils/train_agent.py) runs sharded under
+      `torchrun --nproc-per-node N script.py`;
+    - otherwise LocalComm (one process, the whole batch)."""
+    import os
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        return DistComm() if dist.get_world_size() > 1 else LocalComm()
+    lw = launched_world()
+    if lw is None or not dist.is_available() or "MASTER_ADDR" not in os.environ:
+        return LocalComm()
+    rank, world, local = lw
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend == "nccl":
+        torch.cuda.set_device(local % max(torch.cuda.device_count(), 1))
+        dist.init_process_group("nccl", device_id=torch.device("cuda", torch.cuda.current_device()))
+    else:
+        dist.init_process_group(backend)
+    return DistComm()
+
+
+def shard_count(N, world, rank):
+    """Paths rank `rank` samples out of N (train_step): ceil(N / world) each, the
+    last ranks fewer, as trajectory_sampler.sample_paths_parallel splits N over its
+    workers (mjrl/samplers/trajectory_sampler.py:37-45).  Returns (count, first
+    global path index) — the first index is also the rank's pegasus seed offset."""
+    per = int(np.ceil(N / world))
+    first = min(rank * per, N)
+    return max(0, min(per, N - first)), first
+
+
 def partition_paths(lengths, world_size):
     """Contiguous path ranges per rank, balanced by timestep count.
 

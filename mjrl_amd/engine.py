@@ -12,6 +12,7 @@ mjrl/algos/trpo.py:54-145, mjrl/algos/dapg.py:54-141,
 mjrl/algos/batch_reinforce.py:106-164, mjrl/utils/process_samples.py:3-44.
 """
 import ctypes as C
+import functools
 import math
 import os
 
@@ -71,6 +72,17 @@ class _PinnedStaging:
 _STAGING = _PinnedStaging()
 
 
+def _on_device(fn):
+    """Runs an UpdateEngine method with self.device current, so torch's current
+    stream (the one every kernel is launched on, _lib.stream_ptr) belongs to the
+    device that holds the workspace, whatever device the caller has current."""
+    @functools.wraps(fn)
+    def wrapped(self, *args, **kwargs):
+        with torch.cuda.device(self.device):
+            return fn(self, *args, **kwargs)
+    return wrapped
+
+
 class DeviceBatch:
     """One shard of trajectories in HBM — the hot path's input.
 
@@ -97,6 +109,11 @@ class DeviceBatch:
         copy per array (np.concatenate of npg_cg.py:87-89 without the extra
         temporary).  Baseline predictions come from the caller's baseline object,
         per path, as compute_advantages does (process_samples.py:23)."""
+        with torch.cuda.device(device):
+            return cls._from_paths(paths, device, baseline, use_advantages, demo_paths)
+
+    @classmethod
+    def _from_paths(cls, paths, device, baseline, use_advantages, demo_paths):
         lengths = np.array([len(p["rewards"]) for p in paths], dtype=np.int64)
         T = int(lengths.sum())
         n = paths[0]["observations"].shape[1]
@@ -226,12 +243,15 @@ class UpdateEngine:
         self.scratch_slices = sl.value
         self.cap_T, self.cap_P = T_all, P
 
-    def _scratch(self, T):
+    def _scratch(self, T, ws=None):
+        """Scratch of a pass over T rows, in ws (default: the main workspace; the
+        caller guarantees ws holds mjrl_scratch_size(T)'s wpart / rpart)."""
+        ws = self.ws if ws is None else ws
         wf, rd, sl = C.c_int64(), C.c_int64(), C.c_int32()
         self.lib.mjrl_scratch_size(C.byref(self.shape), T, C.byref(wf), C.byref(rd), C.byref(sl))
         sc = _lib.Scratch()
-        sc.wpart = self.ws["wpart"].data_ptr()
-        sc.rpart = self.ws["rpart"].data_ptr()
+        sc.wpart = ws["wpart"].data_ptr()
+        sc.rpart = ws["rpart"].data_ptr()
         sc.slices = sl.value
         return sc
 
@@ -291,6 +311,7 @@ class UpdateEngine:
             self._side = torch.cuda.Stream(device=self.device)
         return self._side
 
+    @_on_device
     def returns_advantages(self, batch, gamma, gae_lambda, stream=None):
         """process_samples.compute_returns + compute_advantages on device (a1-a3).
         Leaves f64 returns / advantages in ws['ret'] / ws['adv64'].  `stream`: run on
@@ -301,13 +322,23 @@ class UpdateEngine:
         self._ensure(batch.T + batch.T_demo, batch.P)
         w = self.ws
         use_gae = not (gae_lambda is None or gae_lambda < 0.0 or gae_lambda > 1.0)
-        base = batch.baseline if batch.baseline is not None else torch.zeros_like(batch.rewards)
+        base = self._baseline_of(batch)
         _lib.check(self.lib.mjrl_gae(
             _lib.ptr(batch.rewards), _lib.ptr(base), _lib.ptr(batch.path_off), _lib.ptr(batch.terminated),
             batch.P, float(gamma), float(gae_lambda) if use_gae else 0.0, int(use_gae),
             _lib.ptr(w["ret"]), _lib.ptr(w["adv64"]), _lib.ptr(w["path_ret"]), st), "mjrl_gae")
         return w["ret"][:batch.T], w["adv64"][:batch.T]
 
+    @staticmethod
+    def _baseline_of(batch):
+        """The batch's baseline predictions; a missing one becomes zeros, allocated
+        on the current stream and kept on the batch (update() calls this before its
+        side stream forks, so the scan never reads the buffer before the fill)."""
+        if batch.baseline is None:
+            batch.baseline = torch.zeros_like(batch.rewards)
+        return batch.baseline
+
+    @_on_device
     def normalize_advantages(self, T):
         """The `normalize` option of compute_advantages (process_samples.py:14-19,30-35)."""
         w = self.ws
@@ -318,6 +349,7 @@ class UpdateEngine:
                                         _lib.ptr(w["w64"]), self.st), "mjrl_whiten")
         return w["w64"][:T]
 
+    @_on_device
     def update(self, batch, theta, *, algo="npg", gamma=0.995, gae_lambda=0.98, n_step_size=0.01,
                const_lr=None, kl_dist=None, cg_iters=10, damping=1e-4, residual_tol=1e-10,
                demo_coef=None, learn_rate=0.01, T_global=None, trpo_verbose=True, skip_gae=False,
@@ -347,7 +379,9 @@ class UpdateEngine:
         sub = None
         if hvp_sample_frac is not None and hvp_sample_frac < 0.99 and algo != "vpg":
             sub = self._hvp_draws(float(hvp_sample_frac), int(round(T_global)), T, int(cg_iters))
-        self._ensure(max(T_all, sub["max"]) if sub else T_all, P)
+        # a subsampled Fisher's rows live in ws_sub (_subsample_rows), so the main
+        # workspace keeps its size and the GAE outputs already in it
+        self._ensure(T_all, P)
         w = self.ws
         v = self.vec
         sp = C.byref(s)
@@ -359,6 +393,7 @@ class UpdateEngine:
         # batch assembly and joins before the moments.
         main = torch.cuda.current_stream(self.device)
         side = self._side_stream()
+        self._baseline_of(batch)
         side.wait_stream(main)
         adv64 = w["adv64"]
         if batch.advantages is not None:
@@ -542,6 +577,7 @@ class UpdateEngine:
         return result
 
     # ------------------------------------------------------------------
+    @_on_device
     def fit_linear_baseline(self, batch, baseline, returns=None, return_errors=False):
         """LinearBaseline.fit (baselines/linear_baseline.py:20-44) on the batch's
         RL rows already in HBM: the Gram products [F y]^T [F y] on the device
@@ -627,6 +663,11 @@ class UpdateEngine:
         f32 = dict(dtype=torch.float32, device=self.device)
         ws = self.__dict__.setdefault("ws_sub", {})
         if "a0s" not in ws or ws["a0s"].shape[0] < cap:
+            wf, rd, sl = C.c_int64(), C.c_int64(), C.c_int32()
+            _lib.check(self.lib.mjrl_scratch_size(C.byref(s), cap, C.byref(wf), C.byref(rd), C.byref(sl)),
+                       "mjrl_scratch_size")
+            ws["wpart"] = torch.empty(max(wf.value, 1), **f32)
+            ws["rpart"] = torch.zeros(max(rd.value, 1), dtype=torch.float64, device=self.device)
             if self.split:
                 ws["xss"] = torch.empty((cap, 2 * s.np), dtype=torch.float16, device=self.device)
                 ws["xus"] = torch.empty(cap, **f32)
@@ -634,6 +675,10 @@ class UpdateEngine:
                 ws["xhs"] = torch.empty((cap, s.np), **f32)
             ws["a0s"] = torch.empty((cap, max(s.h0, 1)), **f32)
             ws["a1s"] = torch.empty((cap, max(s.h1, 1)), **f32)
+            # per-row upstream gradients the k_rows FVP writes for k_wgrad
+            ws["gu0s"] = torch.empty((cap, max(s.h0, 1)), **f32)
+            ws["gu1s"] = torch.empty((cap, max(s.h1, 1)), **f32)
+            ws["gps"] = torch.empty((cap, s.mp), **f32)
         pairs = [("xs", "xss", s.np), ("xu", "xus", 1)] if self.split else [("xhat", "xhs", s.np)]
         if s.h0:
             pairs += [("a0", "a0s", s.h0), ("a1", "a1s", s.h1)]
@@ -642,13 +687,15 @@ class UpdateEngine:
             _lib.check(self.lib.mjrl_gather_rows(_lib.ptr(w[src]), 4 * width, ip, n_k, _lib.ptr(ws[dst]), self.st),
                        "mjrl_gather_rows")
             setattr(rows, src, ws[dst].data_ptr())
-        return rows, self._scratch(n_k), n_k
+        rows.gu0, rows.gu1, rows.gp = ws["gu0s"].data_ptr(), ws["gu1s"].data_ptr(), ws["gps"].data_ptr()
+        return rows, self._scratch(n_k, ws), n_k
 
     def accumulate_path(self):
         """Accumulate kernel the dispatcher runs for this shape: 2 = K-split
         persistent (k_ks), 1 = fused persistent (k_fused), 0 = k_rows + k_wgrad."""
         return int(self.lib.mjrl_fused_path(C.byref(self.shape)))
 
+    @_on_device
     def fvp(self, v, damping=1e-4, T=None, idx=None):
         """F v + damping v at the parameters of the last update's forward pass
         (the caches a0/a1/mu0 and packed_theta of that pass) — NPG.HVP
@@ -666,7 +713,6 @@ class UpdateEngine:
         if idx is not None:
             n = int(idx.numel())
             sub = dict(idx=idx.contiguous(), counts=[n], offs=[0], max=n)
-            self._ensure(max(self.cap_T, n), self.cap_P)
             rows, scratch, T = self._subsample_rows(sub, 0, self.ws["adv32"])
             T_global = float(n)
         else:
@@ -689,6 +735,7 @@ class UpdateEngine:
     # kl_old_new / flat_vpg / HVP called directly, batch_reinforce.py:37-55,
     # npg_cg.py:55-74); the update above never goes through these.  Local to
     # this process (no collectives).
+    @_on_device
     def load_rows(self, obs, act, adv=None):
         """Stages f64 obs / act (and f64 advantages, cast to f32 as
         batch_reinforce.py:38 does) as the current rows."""
@@ -706,6 +753,7 @@ class UpdateEngine:
             self.ws["adv32"][:T].zero_()
         return T
 
+    @_on_device
     def forward_pass(self, theta, T):
         """Forward + VPG sums at theta over the loaded rows; fills the caches.
         Returns the flat VPG mean (device) = sum / T."""
@@ -725,6 +773,7 @@ class UpdateEngine:
                    "mjrl_scale_vec")
         return self.vec["g"]
 
+    @_on_device
     def eval_pass(self, theta_new, T):
         """(surrogate, KL) at theta_new against the caches of the last forward_pass."""
         L, s = self.lib, self.shape

@@ -245,10 +245,13 @@ def cg_solve(f_Ax, b, iters=10, tol=1e-10, trace=None):
 # --------------------------------------------------------------------------
 def update(policy, obs, act, adv_raw, rewards, lengths, algo="npg", *,
            n_step_size=0.01, const_lr=None, kl_dist=None, cg_iters=10, damping=1e-4,
-           demo_obs=None, demo_act=None, demo_coef=None, trace=None, hvp_sample_frac=None, np_seed=None):
+           demo_obs=None, demo_act=None, demo_coef=None, trace=None, hvp_sample_frac=None, np_seed=None,
+           learn_rate=0.01):
     """Runs the policy update on concatenated arrays and returns a result dict.
 
-    algo: 'npg'  (npg_cg.py:84-165), 'trpo' (trpo.py:54-145), 'dapg' (dapg.py:54-141).
+    algo: 'npg'  (npg_cg.py:84-165), 'trpo' (trpo.py:54-145), 'dapg' (dapg.py:54-141),
+    'vpg' (BatchREINFORCE.train_from_paths, batch_reinforce.py:106-164: theta +
+    learn_rate * vpg_grad in f32, then surr_after / kl).
     For 'npg' with kl_dist set, n_step_size = 2*kl_dist (npg_cg.py:47).
     For 'dapg', demo_coef = lam_0 * lam_1**iter_count (dapg.py:65).
     hvp_sample_frac < 0.99: every Fisher-vector product runs on
@@ -272,6 +275,15 @@ def update(policy, obs, act, adv_raw, rewards, lengths, algo="npg", *,
     else:
         g = policy.flat_vpg(obs, act, adv)
     res["vpg_grad"] = g
+    if algo == "vpg":
+        theta = policy.get_params()
+        new = theta + learn_rate * g   # f32 numpy (batch_reinforce.py:139-140)
+        policy.set_params(new, set_new=True, set_old=False)
+        res["surr_after"] = float(policy.surrogate(obs, act, adv).detach().numpy())
+        res["kl_dist"] = float(policy.kl(obs, act).detach().numpy())
+        policy.set_params(new, set_new=True, set_old=True)
+        res.update(npg_grad=g, cg_trace=[], alpha=learn_rate, delta=None, theta1=policy.get_params())
+        return res
 
     cg_trace = [] if trace else None
     def f_Ax(v):
@@ -427,6 +439,8 @@ def case_kwargs(c):
             kw["kl_dist"] = float(c["kw_kl_dist"])
     elif algo == "trpo":
         kw["kl_dist"] = float(c["kw_kl_dist"]) if "kw_kl_dist" in c else 0.01
+    elif algo == "vpg":
+        kw["learn_rate"] = float(c["kw_learn_rate"]) if "kw_learn_rate" in c else 0.01
     elif algo == "dapg":
         kw["kl_dist"] = float(c["kw_kl_dist"]) if "kw_kl_dist" in c else 0.5 * 0.01
         kw["demo_obs"] = c["demo_obs"].astype(np.float64)

@@ -47,6 +47,7 @@ from mjrl.utils.gym_env import EnvSpec  # noqa: E402
 from mjrl.policies.gaussian_mlp import MLP  # noqa: E402
 from mjrl.policies.gaussian_linear import LinearPolicy  # noqa: E402
 from mjrl.baselines.linear_baseline import LinearBaseline  # noqa: E402
+from mjrl.algos.batch_reinforce import BatchREINFORCE  # noqa: E402
 from mjrl.algos.npg_cg import NPG  # noqa: E402
 from mjrl.algos.trpo import TRPO  # noqa: E402
 from mjrl.algos.dapg import DAPG  # noqa: E402
@@ -247,6 +248,8 @@ def _run(name, *, n, m, hidden, lengths, terminated, algo, algo_kwargs,
         agent = TRPO(None, policy, baseline, save_logs=True, **algo_kwargs)
     elif algo == "dapg":
         agent = DAPG(None, policy, baseline, demo_paths=demo_paths, save_logs=True, **algo_kwargs)
+    elif algo == "vpg":
+        agent = BatchREINFORCE(None, policy, baseline, save_logs=True, **algo_kwargs)
     else:
         raise ValueError(algo)
 
@@ -258,7 +261,10 @@ def _run(name, *, n, m, hidden, lengths, terminated, algo, algo_kwargs,
     hvp_v = vrs.randn(policy.d).astype(np.float32)
     if np_seed is not None:   # the subsampled HVP draws from numpy's global RNG (npg_cg.py:58-62)
         np.random.seed(np_seed + 1)
-    hvp_out = agent.HVP(obs, act, hvp_v)
+    if algo == "vpg":   # BatchREINFORCE has no HVP: the NPG one at the same parameters
+        hvp_out = NPG(None, policy, baseline).HVP(obs, act, hvp_v)
+    else:
+        hvp_out = agent.HVP(obs, act, hvp_v)
 
     # the update proper (batch_reinforce.py:86-91 minus sampling and fit)
     process_samples.compute_returns(paths, gamma)
@@ -271,12 +277,15 @@ def _run(name, *, n, m, hidden, lengths, terminated, algo, algo_kwargs,
     finally:
         rec.restore()
     theta1 = policy.get_param_values()
+    if rec.cg is None:   # BatchREINFORCE: no CG, the step direction is the VPG itself
+        rec.cg = dict(b=rec.vpg[0], p=np.zeros((0, policy.d), np.float32), z=np.zeros((0, policy.d), np.float32),
+                      x=rec.vpg[0])
 
     out = dict(
         spread_x=max(_nrel(a["cg_x"], rec.cg["x"]) for a in alt) if alt else 0.0,
         spread_theta=max(_nrel(a["theta1"], theta1) for a in alt) if alt else 0.0,
         spread_kl=max(abs(a["log_kl_dist"] / agent.logger.log["kl_dist"][-1] - 1) for a in alt) if alt else 0.0,
-        spread_alpha=max(abs(a["log_alpha"] / agent.logger.log["alpha"][-1] - 1) for a in alt) if alt else 0.0,
+        spread_alpha=max(abs(float(a["log_alpha"]) / agent.logger.log["alpha"][-1] - 1) for a in alt) if alt else 0.0,
         spread_surr=max(abs(a["log_surr_improvement"] / agent.logger.log["surr_improvement"][-1] - 1)
                         for a in alt) if alt else 0.0,
         n=n, m=m, hidden=np.array(hidden if not linear else (0, 0)), linear=int(linear),
@@ -378,6 +387,9 @@ def main():
              terminated=[False] * 20, algo="npg",
              algo_kwargs=dict(normalized_step_size=0.1, hvp_sample_frac=0.5), seed=31, np_seed=2024,
              reverse_alt=False)
+    # C2v: BatchREINFORCE (vanilla policy gradient, batch_reinforce.py:106-164)
+    run_case("c2_vpg", n=8, m=2, hidden=(64, 64), lengths=[200] * 10,
+             terminated=[False] * 10, algo="vpg", algo_kwargs=dict(learn_rate=0.05), seed=41)
     # C3: HalfCheetah shape, TRPO (reduced to 10 x 1000)
     run_case("c3_halfcheetah_trpo", n=17, m=6, hidden=(128, 128),
              lengths=[1000] * 10, terminated=[False] * 10, algo="trpo",

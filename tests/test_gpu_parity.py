@@ -92,6 +92,8 @@ def run_case(name, precision=None):
     if algo == "npg":
         args.update(n_step_size=kw.get("n_step_size", 0.01), const_lr=kw.get("const_lr"),
                     kl_dist=kw.get("kl_dist"))
+    elif algo == "vpg":   # BatchREINFORCE (batch_reinforce.py:106-164)
+        args.update(learn_rate=kw["learn_rate"])
     else:
         args.update(kl_dist=kw["kl_dist"])
     if algo == "dapg":

@@ -154,6 +154,17 @@ int mjrl_moments(const double* x, int64_t N, const double* center, double* rpart
 int mjrl_moments_f32(const float* x, int64_t N, const double* center, double* rpart,
                      double* out, void* stream);
 
+/* One-launch forms (the last workgroup folds the block partials in fixed order):
+ * mjrl_moments2: the moments of x1 [N1] and x2 [N2] together (out1 / out2 as
+ * mjrl_moments; out2 may be null to do x1 alone); mjrl_whiten_moments: mjrl_whiten
+ * (adv32 required) plus the moments of the f32 whitened values into out[6].
+ * rpart: MJRL_MOM_SCRATCH doubles (zero-filled before the first use). */
+#define MJRL_MOM_SCRATCH 2056
+int mjrl_moments2(const double* x1, int64_t N1, const double* c1, const double* x2, int64_t N2,
+                  const double* c2, double* rpart, double* out1, double* out2, void* stream);
+int mjrl_whiten_moments(const double* adv, int64_t T, const double* m1, const double* m2, double eps,
+                        float* adv32, double* w64, double* rpart, double* out, void* stream);
+
 /* w = (adv[t] - mean) / (std + eps), mean = m1[0]/m1[2], std = sqrt(m2[1]/m1[2]);
  * adv32[t] = float(w) (eps = 1e-6: npg_cg.py:91 then the .float() of
  * batch_reinforce.py:38) and/or w64[t] = w (eps = 1e-8: the `normalize` option of
@@ -235,6 +246,20 @@ int mjrl_cg_step(const mjrl_shape* s, const float* gsum, double inv_T, float dam
                  float* packed_p, float* cg, int32_t* done, float residual_tol,
                  void* stream);
 
+/* The same iteration with the gradient gather fused in (one process, no
+ * all-reduce between the gather and the step): mjrl_gather_cg_z folds the
+ * accumulate slabs (as mjrl_gather_grads, with_log_std = 0, also writing gsum)
+ * and, in the same launch, forms z = gsum * inv_T + c(sigma) * p_logstd +
+ * damping * p and p.z -> cg[4], v -> cg[2]; mjrl_cg_step_xr_p then updates x, r,
+ * rdotr, mu, done and p / packed_p.  Same arithmetic as mjrl_cg_step (the p.z
+ * partials are folded per 64 parameters instead of per 1024).  Needs
+ * d <= 64 * (MJRL_CG_STATE - 16) / 2 (else MJRL_EINVAL: use the unfused pair). */
+int mjrl_gather_cg_z(const mjrl_shape* s, const mjrl_rows* rows, int64_t T, const mjrl_scratch* sc,
+                     const int32_t* done, float* gsum, double inv_T, float damping,
+                     const float* packed_theta, const float* p, float* z, float* cg, void* stream);
+int mjrl_cg_step_xr_p(const mjrl_shape* s, float* x, float* r, float* p, const float* z,
+                      float* packed_p, float* cg, int32_t* done, float residual_tol, void* stream);
+
 /* Generic CG (cg_solve.py:3-22 with a caller-supplied operator): init from b,
  * then one update per z = A p the caller computed.  Same scalar arithmetic and
  * residual_tol break as mjrl_cg_step. */
@@ -250,7 +275,9 @@ int mjrl_scale_vec(const float* gsum, int32_t d, double scale, float* g, void* s
  * mode 0: alpha = sqrt(|delta / (g.x + 1e-20)|);  mode 1: alpha = alpha_in
  * (const learn-rate or a TRPO backtrack trial); out[0] = alpha, out[1] = g.x,
  * out[2] = delta (mode 1 with const_lr: alpha^2 * g.x).
- * theta_new = clamp_logstd(theta + alpha * x); packs theta_new. */
+ * theta_new = clamp_logstd(theta + alpha * x); packs theta_new.
+ * out holds MJRL_STEP_OUT floats (out[8..] is the multi-workgroup g.x scratch). */
+#define MJRL_STEP_OUT 1024
 int mjrl_npg_step(const mjrl_shape* s, const float* g, const float* x, const float* theta,
                   int32_t mode, float delta, float alpha_in, int32_t const_lr,
                   float min_log_std, float* theta_new, float* packed_new, float* out,

@@ -20,6 +20,8 @@ MJRL_OK = 0
 MJRL_EINVAL = -1
 MJRL_ESHAPE = -2
 CG_STATE = 1024   # MJRL_CG_STATE: floats of the device CG state
+STEP_OUT = 1024   # MJRL_STEP_OUT: floats of mjrl_npg_step's out buffer
+MOM_SCRATCH = 2056   # MJRL_MOM_SCRATCH: doubles of the one-launch moments scratch
 
 
 class Shape(C.Structure):
@@ -54,6 +56,8 @@ SIGNATURES = {
     "mjrl_linear_baseline": [P, I64, I32, P, I64, P, P, P],
     "mjrl_moments": [P, I64, P, P, P, P],
     "mjrl_moments_f32": [P, I64, P, P, P, P],
+    "mjrl_moments2": [P, I64, P, P, I64, P, P, P, P, P],
+    "mjrl_whiten_moments": [P, I64, P, P, F64, P, P, P, P, P],
     "mjrl_whiten": [P, I64, P, P, F64, P, P, P],
     "mjrl_dapg_adv": [P, I64, P, P, I64, F64, P, P],
     "mjrl_pack_params": [SP, P, P, I32, F32, P],
@@ -66,6 +70,8 @@ SIGNATURES = {
     "mjrl_fused_path": [SP],
     "mjrl_cg_init": [SP, P, P, P, P, P, P, P, P],
     "mjrl_cg_step": [SP, P, F64, F32, P, P, P, P, P, P, P, P, F32, P],
+    "mjrl_gather_cg_z": [SP, C.POINTER(Rows), I64, C.POINTER(Scratch), P, P, F64, F32, P, P, P, P, P],
+    "mjrl_cg_step_xr_p": [SP, P, P, P, P, P, P, P, F32, P],
     "mjrl_cg_init_vec": [I32, P, P, P, P, P, P, P],
     "mjrl_cg_update": [I32, P, P, P, P, P, P, F32, P],
     "mjrl_scale_vec": [P, I32, F64, P, P],

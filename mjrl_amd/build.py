@@ -31,26 +31,27 @@ def _deps():
     return max(os.path.getmtime(h) for h in hdrs)
 
 
-def _compile(src, force, prof=False):
+def _compile(src, force, prof=False, tag="", extra=()):
     s = os.path.join(CSRC, src)
-    o = os.path.join(OUTDIR, src.replace(".hip", "_prof.o" if prof else ".o"))
+    o = os.path.join(OUTDIR, src.replace(".hip", ("_prof" if prof else "") + tag + ".o"))
     if not force and os.path.exists(o) and os.path.getmtime(o) >= max(os.path.getmtime(s), _deps()):
         return o
-    cmd = [HIPCC] + FLAGS + (["-DMJRL_KX_PROF"] if prof else []) + ["-c", s, "-o", o]
+    cmd = [HIPCC] + FLAGS + list(extra) + (["-DMJRL_KX_PROF"] if prof else []) + ["-c", s, "-o", o]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError("hipcc failed for %s:\n%s\n%s" % (src, " ".join(cmd), r.stderr[-8000:]))
     return o
 
 
-def build(force=False, jobs=None, prof=False):
+def build(force=False, jobs=None, prof=False, tag="", extra=()):
     """prof=True builds the phase-profiling variant lib/libmjrl_amd_prof.so
-    (-DMJRL_KX_PROF; select it with MJRL_AMD_LIB=<path>)."""
+    (-DMJRL_KX_PROF; select it with MJRL_AMD_LIB=<path>).  tag / extra: an
+    experimental variant lib/libmjrl_amd<tag>.so built with extra hipcc flags."""
     os.makedirs(OUTDIR, exist_ok=True)
     jobs = jobs or min(len(SOURCES), os.cpu_count() or 1, 16)
-    lib = LIB.replace(".so", "_prof.so") if prof else LIB
+    lib = LIB.replace(".so", ("_prof" if prof else "") + tag + ".so")
     with cf.ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, force, prof), SOURCES))
+        objs = list(ex.map(lambda s: _compile(s, force, prof, tag, extra), SOURCES))
     if force or not os.path.exists(lib) or os.path.getmtime(lib) < max(os.path.getmtime(o) for o in objs):
         cmd = [HIPCC, "-shared", "--offload-arch=" + ARCH, "-fPIC"] + objs + ["-o", lib]
         r = subprocess.run(cmd, capture_output=True, text=True)
@@ -64,5 +65,7 @@ if __name__ == "__main__":
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", type=int, default=None)
     ap.add_argument("--prof", action="store_true", help="phase-profiling variant (libmjrl_amd_prof.so)")
+    ap.add_argument("--tag", default="", help="variant suffix: lib/libmjrl_amd<tag>.so")
+    ap.add_argument("--extra", default="", help="extra hipcc flags of the variant (space separated)")
     args = ap.parse_args()
-    print(build(args.force, args.j, args.prof))
+    print(build(args.force, args.j, args.prof, args.tag, args.extra.split()))

@@ -330,6 +330,168 @@ __global__ void __launch_bounds__(64) k_moments_final(const double* __restrict__
     }
 }
 
+// ---------------------------------------------------------------------------
+// One-launch statistics: the per-block partials of k_moments_part, then the LAST
+// workgroup folds them in block order (common.h last_wg_fold, no grid barrier).
+// Layout of rpart (MJRL_MOM_SCRATCH doubles): 4 partials per block, then the
+// ticket word at MOM2_TICKET.
+// ---------------------------------------------------------------------------
+constexpr int MOM2_MAXB = 512;
+constexpr int MOM2_TICKET = 4 * MOM2_MAXB;
+
+// block partial (s1, s2, min, max) of x[i0 + k * stride_blocks...] for one array
+template <typename T>
+__device__ __forceinline__ void mom_block(const T* __restrict__ x, int64_t N, double c, int blk, int nblk,
+                                          double* red, double (&o)[4]) {
+    double s1 = 0.0, s2 = 0.0, mn = __builtin_inf(), mx = -__builtin_inf();
+    const int64_t stride = (int64_t)nblk * blockDim.x;
+    for (int64_t i = (int64_t)blk * blockDim.x + threadIdx.x; i < N; i += stride) {
+        const double v = (double)x[i];
+        const double dv = v - c;
+        s1 += dv;
+        s2 += dv * dv;
+        mn = fmin(mn, v);
+        mx = fmax(mx, v);
+    }
+    o[0] = block_sum<MOM_THREADS>(s1, red);
+    o[1] = block_sum<MOM_THREADS>(s2, red);
+#pragma unroll
+    for (int k = 32; k > 0; k >>= 1) {
+        mn = fmin(mn, __shfl_xor(mn, k, 64));
+        mx = fmax(mx, __shfl_xor(mx, k, 64));
+    }
+    __shared__ double mm[2][MOM_THREADS / 64];
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) {
+        mm[0][threadIdx.x >> 6] = mn;
+        mm[1][threadIdx.x >> 6] = mx;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < MOM_THREADS / 64; ++i) {
+        mn = fmin(mn, mm[0][i]);
+        mx = fmax(mx, mm[1][i]);
+    }
+    o[2] = mn;
+    o[3] = mx;
+}
+
+// the last workgroup (wave 0) folds blocks [b0, b1) of the partials into out[6]
+__device__ __forceinline__ void mom_fold(const double* part, int b0, int b1, int64_t N, double* out) {
+    const int lane = threadIdx.x & 63;
+    double s1 = 0.0, s2 = 0.0, mn = __builtin_inf(), mx = -__builtin_inf();
+    for (int b = b0 + lane; b < b1; b += 64) {
+        s1 += __hip_atomic_load(part + 4 * b + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s2 += __hip_atomic_load(part + 4 * b + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        mn = fmin(mn, __hip_atomic_load(part + 4 * b + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        mx = fmax(mx, __hip_atomic_load(part + 4 * b + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mn = fmin(mn, __shfl_xor(mn, o, 64));
+        mx = fmax(mx, __shfl_xor(mx, o, 64));
+    }
+    if (lane == 0) {
+        out[0] = s1;
+        out[1] = s2;
+        out[2] = (double)N;
+        out[3] = mn;
+        out[4] = mx;
+        out[5] = -mn;
+    }
+}
+
+// publish this block's partial, take a ticket; true in the last block (wave 0)
+__device__ __forceinline__ bool mom_publish(double* part, const double (&o)[4], int nb) {
+    __shared__ unsigned tk;
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) part[4 * blockIdx.x + k] = o[k];
+        __threadfence();
+        tk = atomicAdd(reinterpret_cast<unsigned*>(part + MOM2_TICKET), 1u);
+    }
+    __syncthreads();
+    if (tk != (unsigned)(nb - 1)) return false;
+    __threadfence();
+    return threadIdx.x < 64;
+}
+
+// two arrays in one launch: blocks [0, nb1) take x1, [nb1, nb1 + nb2) take x2;
+// centres c1 / c2 are moments outputs (mean = c[0] / c[2]) or null (0)
+__global__ void __launch_bounds__(MOM_THREADS) k_moments2(const double* __restrict__ x1, int64_t N1,
+                                                          const double* __restrict__ c1, const double* __restrict__ x2,
+                                                          int64_t N2, const double* __restrict__ c2, int nb1, int nb2,
+                                                          double* part, double* __restrict__ out1,
+                                                          double* __restrict__ out2) {
+    __shared__ double red[MOM_THREADS / 64];
+    double o[4];
+    const int b = blockIdx.x;
+    if (b < nb1) {
+        mom_block(x1, N1, c1 ? c1[0] / c1[2] : 0.0, b, nb1, red, o);
+    } else {
+        mom_block(x2, N2, c2 ? c2[0] / c2[2] : 0.0, b - nb1, nb2, red, o);
+    }
+    if (mom_publish(part, o, nb1 + nb2)) {
+        mom_fold(part, 0, nb1, N1, out1);
+        if (out2) mom_fold(part, nb1, nb1 + nb2, N2, out2);
+        if (threadIdx.x == 0) *reinterpret_cast<unsigned*>(part + MOM2_TICKET) = 0u;
+    }
+}
+
+// whitening (k_whiten) and, in the same launch, the moments of the f32 output
+// (the surr_before numerator, npg_cg.py:113 with LR == 1)
+__global__ void __launch_bounds__(MOM_THREADS) k_whiten_mom(const double* __restrict__ adv, int64_t T,
+                                                            const double* __restrict__ m1,
+                                                            const double* __restrict__ m2, double eps,
+                                                            float* __restrict__ adv32, double* __restrict__ w64,
+                                                            double* part, double* __restrict__ out) {
+    __shared__ double red[MOM_THREADS / 64];
+    const double mean = m1[0] / m1[2];
+    const double sd = sqrt(m2[1] / m1[2]);
+    const double den = sd + eps;
+    double s1 = 0.0, s2 = 0.0, mn = __builtin_inf(), mx = -__builtin_inf();
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < T; i += stride) {
+        const double w = (adv[i] - mean) / den;
+        const float wf = (float)w;
+        adv32[i] = wf;
+        if (w64) w64[i] = w;
+        const double v = (double)wf;
+        s1 += v;
+        s2 += v * v;
+        mn = fmin(mn, v);
+        mx = fmax(mx, v);
+    }
+    double o[4];
+    o[0] = block_sum<MOM_THREADS>(s1, red);
+    o[1] = block_sum<MOM_THREADS>(s2, red);
+#pragma unroll
+    for (int k = 32; k > 0; k >>= 1) {
+        mn = fmin(mn, __shfl_xor(mn, k, 64));
+        mx = fmax(mx, __shfl_xor(mx, k, 64));
+    }
+    __shared__ double mm[2][MOM_THREADS / 64];
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) {
+        mm[0][threadIdx.x >> 6] = mn;
+        mm[1][threadIdx.x >> 6] = mx;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < MOM_THREADS / 64; ++i) {
+        mn = fmin(mn, mm[0][i]);
+        mx = fmax(mx, mm[1][i]);
+    }
+    o[2] = mn;
+    o[3] = mx;
+    if (mom_publish(part, o, gridDim.x)) {
+        mom_fold(part, 0, gridDim.x, T, out);
+        if (threadIdx.x == 0) *reinterpret_cast<unsigned*>(part + MOM2_TICKET) = 0u;
+    }
+}
+
 // adv32 = float((adv - mean) / (std + 1e-6)) (npg_cg.py:91; .float() at batch_reinforce.py:38)
 __global__ void __launch_bounds__(256) k_whiten(const double* __restrict__ adv, int64_t T,
                                                 const double* __restrict__ m1, const double* __restrict__ m2,
@@ -471,6 +633,25 @@ static int moments_impl(bool f32, const void* x, int64_t N, const double* center
         hipLaunchKernelGGL(k_moments_part<double>, dim3(nb), dim3(MOM_THREADS), 0, (hipStream_t)stream,
                            (const double*)x, N, center, rpart);
     hipLaunchKernelGGL(k_moments_final, dim3(1), dim3(64), 0, (hipStream_t)stream, rpart, nb, N, out);
+    return err(hipGetLastError());
+}
+
+int mjrl_moments2(const double* x1, int64_t N1, const double* c1, const double* x2, int64_t N2, const double* c2,
+                  double* rpart, double* out1, double* out2, void* stream) {
+    if (N1 < 0 || N2 < 0 || !rpart || !out1 || (N1 > 0 && !x1) || (out2 && N2 > 0 && !x2)) return MJRL_EINVAL;
+    const int nb1 = grid_for(N1, MOM_THREADS * 4, MOM2_MAXB / 2);
+    const int nb2 = out2 ? grid_for(N2, MOM_THREADS * 4, MOM2_MAXB / 2) : 0;
+    hipLaunchKernelGGL(k_moments2, dim3(nb1 + nb2), dim3(MOM_THREADS), 0, (hipStream_t)stream, x1, N1, c1, x2, N2, c2,
+                       nb1, nb2, rpart, out1, out2);
+    return err(hipGetLastError());
+}
+
+int mjrl_whiten_moments(const double* adv, int64_t T, const double* m1, const double* m2, double eps, float* adv32,
+                        double* w64, double* rpart, double* out, void* stream) {
+    if (T < 0 || !adv || !m1 || !m2 || !adv32 || !rpart || !out) return MJRL_EINVAL;
+    const int nb = grid_for(T, MOM_THREADS * 4, MOM2_MAXB);
+    hipLaunchKernelGGL(k_whiten_mom, dim3(nb), dim3(MOM_THREADS), 0, (hipStream_t)stream, adv, T, m1, m2, eps, adv32,
+                       w64, rpart, out);
     return err(hipGetLastError());
 }
 

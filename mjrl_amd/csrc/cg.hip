@@ -318,7 +318,90 @@ __global__ void __launch_bounds__(CGM_T) k_cgm_p(mjrl_shape s, const float* __re
     }
 }
 
-// Step size and parameter update (npg_cg.py:128-141).
+// cg_solve.py:4-7 over many workgroups: x = 0, r = p = b (and packed p), rdotr
+// = b.b folded in fixed order by the last workgroup.
+__global__ void __launch_bounds__(CGM_T) k_cgm_init(mjrl_shape s, const float* __restrict__ b, float* __restrict__ x,
+                                                    float* __restrict__ r, float* __restrict__ p,
+                                                    float* __restrict__ packed_p, float* cg, int32_t* __restrict__ done) {
+    __shared__ double red[CGM_T / 64];
+    const PackMap pm(s);
+    double acc = 0.0;
+#pragma unroll
+    for (int u = 0; u < CGM_U; ++u) {
+        const int f = blockIdx.x * CGM_WG + u * CGM_T + threadIdx.x;
+        if (f >= s.d) continue;
+        const float v = b[f];
+        x[f] = 0.f;
+        r[f] = v;
+        p[f] = v;
+        pack_one(pm, f, v, packed_p, false, 0.f);
+        acc += (double)v * (double)v;
+    }
+    const double blk = block_sum<CGM_T>(acc, red);
+    double t;
+    if (threadIdx.x < 64 &&
+        last_wg_fold(blk, reinterpret_cast<double*>(cg + 16), reinterpret_cast<unsigned*>(cg + 8), gridDim.x, t) &&
+        threadIdx.x == 0) {
+        cg[0] = (float)t;   // rdotr
+        cg[1] = 0.f;        // iterations run
+        *done = 0;
+    }
+}
+
+// Step size and parameter update (npg_cg.py:128-141), over many workgroups:
+// k_npgm_dot folds g.x (fixed order, last workgroup) and sets alpha / delta;
+// k_npgm_apply writes theta + alpha x (log-std clamp) and its packed copy.
+// out[MJRL_STEP_OUT]: out[0..2] results, out[8] ticket, out + 16 double partials.
+__global__ void __launch_bounds__(CGM_T) k_npgm_dot(int d, const float* __restrict__ g, const float* __restrict__ x,
+                                                    int mode, float delta, float alpha_in, int const_lr,
+                                                    float* out) {
+    __shared__ double red[CGM_T / 64];
+    double acc = 0.0;
+#pragma unroll
+    for (int u = 0; u < CGM_U; ++u) {
+        const int f = blockIdx.x * CGM_WG + u * CGM_T + threadIdx.x;
+        if (f < d) acc += (double)g[f] * (double)x[f];
+    }
+    const double blk = block_sum<CGM_T>(acc, red);
+    double t;
+    if (threadIdx.x < 64 &&
+        last_wg_fold(blk, reinterpret_cast<double*>(out + 16), reinterpret_cast<unsigned*>(out + 8), gridDim.x, t) &&
+        threadIdx.x == 0) {
+        const float gx = (float)t;
+        float alpha, dl = delta;
+        if (mode == 0) {
+            alpha = sqrtf(fabsf(delta / __fadd_rn(gx, 1e-20f)));
+        } else {
+            alpha = alpha_in;
+            if (const_lr) dl = __fmul_rn(alpha * alpha, gx);
+        }
+        out[0] = alpha;
+        out[1] = gx;
+        out[2] = dl;
+    }
+}
+
+__global__ void __launch_bounds__(CGM_T) k_npgm_apply(mjrl_shape s, const float* __restrict__ x,
+                                                      const float* __restrict__ theta, float min_ls,
+                                                      float* __restrict__ theta_new, float* __restrict__ packed_new,
+                                                      const float* __restrict__ out) {
+    const PackMap pm(s);
+    const float alpha = out[0];
+#pragma unroll
+    for (int u = 0; u < CGM_U; ++u) {
+        const int f = blockIdx.x * CGM_WG + u * CGM_T + threadIdx.x;
+        if (f >= s.d) continue;
+        float v = __fadd_rn(theta[f], __fmul_rn(alpha, x[f]));
+        int p1, p2;
+        if (pm.map(f, p1, p2) >= 0) v = v < min_ls ? min_ls : v;   // set_param_values clamp
+        theta_new[f] = v;
+        packed_new[p1] = v;
+        if (p2 >= 0) packed_new[p2] = v;
+    }
+}
+
+// Step size and parameter update (npg_cg.py:128-141), one workgroup (d beyond the
+// multi-workgroup partials).
 __global__ void __launch_bounds__(CG_THREADS) k_npg_step(mjrl_shape s, const float* __restrict__ g,
                                                          const float* __restrict__ x,
                                                          const float* __restrict__ theta, int mode, float delta,
@@ -425,8 +508,25 @@ int mjrl_pack_params(const mjrl_shape* s, const float* theta, float* packed, int
 int mjrl_cg_init(const mjrl_shape* s, const float* b, float* x, float* r, float* p, float* packed_p, float* cg,
                  int32_t* done, void* stream) {
     if (!s || !b || !x || !r || !p || !packed_p || !cg || !done) return MJRL_EINVAL;
+    const int nwg = (s->d + CGM_WG - 1) / CGM_WG;
+    if (nwg <= CGM_MAXWG && nwg > 0) {
+        hipLaunchKernelGGL(k_cgm_init, dim3(nwg), dim3(CGM_T), 0, (hipStream_t)stream, *s, b, x, r, p, packed_p, cg,
+                           done);
+        return err(hipGetLastError());
+    }
     hipLaunchKernelGGL(k_cg_init, dim3(1), dim3(CG_THREADS), 0, (hipStream_t)stream, *s, b, x, r, p, packed_p, cg,
                        done);
+    return err(hipGetLastError());
+}
+
+int mjrl_cg_step_xr_p(const mjrl_shape* s, float* x, float* r, float* p, const float* z, float* packed_p, float* cg,
+                      int32_t* done, float residual_tol, void* stream) {
+    if (!s || !x || !r || !p || !z || !packed_p || !cg || !done) return MJRL_EINVAL;
+    const int nwg = (s->d + CGM_WG - 1) / CGM_WG;
+    if (nwg > CGM_MAXWG) return MJRL_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_cgm_xr, dim3(nwg), dim3(CGM_T), 0, st, s->d, p, z, x, r, cg, done, residual_tol);
+    hipLaunchKernelGGL(k_cgm_p, dim3(nwg), dim3(CGM_T), 0, st, *s, r, p, packed_p, cg, done);
     return err(hipGetLastError());
 }
 
@@ -466,8 +566,16 @@ int mjrl_npg_step(const mjrl_shape* s, const float* g, const float* x, const flo
                   float alpha_in, int32_t const_lr, float min_log_std, float* theta_new, float* packed_new,
                   float* out, void* stream) {
     if (!s || !g || !x || !theta || !theta_new || !packed_new || !out) return MJRL_EINVAL;
-    hipLaunchKernelGGL(k_npg_step, dim3(1), dim3(CG_THREADS), 0, (hipStream_t)stream, *s, g, x, theta, mode, delta,
-                       alpha_in, const_lr, min_log_std, theta_new, packed_new, out);
+    const int nwg = (s->d + CGM_WG - 1) / CGM_WG;
+    hipStream_t st = (hipStream_t)stream;
+    if (nwg <= (MJRL_STEP_OUT - 16) / 2 && nwg > 0) {
+        hipLaunchKernelGGL(k_npgm_dot, dim3(nwg), dim3(CGM_T), 0, st, s->d, g, x, mode, delta, alpha_in, const_lr, out);
+        hipLaunchKernelGGL(k_npgm_apply, dim3(nwg), dim3(CGM_T), 0, st, *s, x, theta, min_log_std, theta_new,
+                           packed_new, (const float*)out);
+        return err(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_npg_step, dim3(1), dim3(CG_THREADS), 0, st, *s, g, x, theta, mode, delta, alpha_in, const_lr,
+                       min_log_std, theta_new, packed_new, out);
     return err(hipGetLastError());
 }
 

@@ -254,6 +254,85 @@ __device__ __forceinline__ double block_sum(double v, double* red /* LDS, >= NT/
 
 __host__ __device__ __forceinline__ int round_up(int x, int m) { return (x + m - 1) / m * m; }
 
+// ---------------------------------------------------------------------------
+// Grid-wide fixed-order fold without a grid barrier: every workgroup stores its
+// (already block-reduced) partial, and the LAST workgroup to take a ticket folds
+// all nwg partials in index order (lane l: partials l, l + 64, ... then a fixed
+// shuffle tree) — the same order on every run, whatever the scheduling.  Called
+// by the 64 lanes of ONE wave per workgroup with the same value b in every lane.
+// Returns true in the last workgroup (total valid in every lane of that wave);
+// the ticket is reset there for the next launch.  Visibility: release fence
+// before the ticket, acquire fence after it (MI355X_MICROARCH.md, inter-workgroup
+// visibility).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool last_wg_fold(double b, double* parts, unsigned* ticket, int nwg, double& total) {
+    const int lane = threadIdx.x & 63;
+    unsigned tk = 0;
+    if (lane == 0) {
+        parts[blockIdx.x] = b;
+        __threadfence();
+        tk = atomicAdd(ticket, 1u);
+    }
+    tk = __shfl(tk, 0, 64);
+    if (tk != (unsigned)(nwg - 1)) return false;
+    __threadfence();
+    double t = 0.0;
+    for (int i = lane; i < nwg; i += 64) t += __hip_atomic_load(parts + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    total = wave_sum(t);
+    if (lane == 0) *ticket = 0u;
+    return true;
+}
+
+// The z step of a CG iteration (cg_solve.py:11, npg_cg.py:73-74) fused into the
+// epilogue of a gradient gather: z[f] = gsum[f] / T + damping p[f] on the mean
+// block, c(sigma) p[f] + damping p[f] on the log-std block (closed form, DESIGN.md
+// §2), and the partial of p.z.  p == nullptr: off.
+struct CgZ {
+    const float* p;
+    float* z;
+    float* cg;            // CG state (mjrl_cg_*): cg[8] ticket, cg + 16 double partials
+    const float* ls;      // packed log_std
+    double inv_T;
+    float damping;
+    int ls0;              // first log-std flat index (d - m)
+};
+
+__device__ __forceinline__ float cg_logstd_curv(float log_std) {
+    const float sg = expf(log_std);
+    const double uu = (double)sg * (double)sg;
+    return (float)(4.0 * uu * (2.0 * uu - 1e-8) / ((2.0 * uu + 1e-8) * (2.0 * uu + 1e-8)));
+}
+
+// wave 0 of a gather workgroup: lane -> flat parameter f (< d), gs = the folded
+// (f32-rounded) gradient sum of f.  Writes z, folds p.z, and in the last workgroup
+// sets cg[4] = p.z and cg[2] = v = rdotr / p.z (cg_solve.py:12).
+__device__ __forceinline__ void cgz_epilogue(const CgZ& c, int f, int d, float gs) {
+    double pz = 0.0;
+    if (f < d) {
+        const float pf = c.p[f];
+        float hv;
+        if (f >= c.ls0) {
+            const float sg = expf(c.ls[f - c.ls0]);
+            const double uu = (double)sg * (double)sg;
+            const double cc = 4.0 * uu * (2.0 * uu - 1e-8) / ((2.0 * uu + 1e-8) * (2.0 * uu + 1e-8));
+            hv = (float)(cc * (double)pf);
+        } else {
+            hv = (float)((double)gs * c.inv_T);
+        }
+        const float zf = __fadd_rn(hv, __fmul_rn(c.damping, pf));   // hvp_flat + regu_coef * vector
+        c.z[f] = zf;
+        pz = (double)pf * (double)zf;
+    }
+    pz = wave_sum(pz);
+    double t;
+    if (last_wg_fold(pz, reinterpret_cast<double*>(c.cg + 16), reinterpret_cast<unsigned*>(c.cg + 8), gridDim.x, t) &&
+        (threadIdx.x & 63) == 0) {
+        const float pzf = (float)t;
+        c.cg[4] = pzf;
+        c.cg[2] = c.cg[0] / pzf;
+    }
+}
+
 // Offsets (in floats) of the packed parameter set — see pack_params.
 struct Packed {
     int W0, W1, b1, W2, b2, W1T, W2T, ls, total;

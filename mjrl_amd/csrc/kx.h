@@ -708,7 +708,7 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
         // gW1 / gW2 sums (their operands are complete since P4) and the next tile's
         // xhat loads (consumed at the next publish) ----
         xload(tile + gridDim.x, ltid, L::XPER / 2, L::XPER);
-        {
+        auto p5_gu0 = [&]() __attribute__((always_inline)) {
             const int hcol = cb * 16 + lr16;
             half8 ah[2], al[2];
             const float rinv = adyn<2>(D0, L::LD, kh, lq, lr16, nullptr, ah, al);
@@ -732,8 +732,8 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
                 gv[rr] = (1.f - av * av) * (acc[rr] * ri[rr] * csc) * Us[row];
             }
             *reinterpret_cast<float4*>(D1 + hcol * L::LDT + kh * 16 + 4 * lq) = make_float4(gv[0], gv[1], gv[2], gv[3]);
-        }
-        {
+        };
+        auto p5_gw = [&]() __attribute__((always_inline)) {
             half8 gh, gl;
             float s4[4];
             // gW1[jb = cb][kb = kh + 2jj] += gu1^T a0;  gb1 = row sums of gu1 (waves kh = 0)
@@ -773,7 +773,16 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) g2[rr] += t[rr] * s4[rr];
             }
-        }
+        };
+#ifdef MJRL_KX_P5SWAP
+        // the two waves of a SIMD (kh = 0 / 1) run the phase's two halves in opposite
+        // order, so one issues the weight-gradient MFMAs while the other is in the
+        // VALU-heavy gu0 epilogue
+        if (kh == 0) { p5_gu0(); p5_gw(); } else { p5_gw(); p5_gu0(); }
+#else
+        p5_gu0();
+        p5_gw();
+#endif
         __syncthreads();
         KX_STAMP(7);
 

@@ -594,6 +594,7 @@ struct GArgs {
     int G;
     float* gsum;
     const int32_t* done;
+    CgZ cz;   // fused CG z step (cz.p == nullptr: plain gather)
 };
 
 // Block = 16 waves over 64 consecutive flat parameters: lane -> parameter, wave w
@@ -665,11 +666,16 @@ __global__ void __launch_bounds__(64 * GATHER_WAVES) k_gather(GArgs a) {
     }
     part[w][lane] = acc;
     __syncthreads();
-    if (w == 0 && f < a.d) {
-        double t = part[0][lane];
+    if (w == 0) {
+        float gs = 0.f;
+        if (f < a.d) {
+            double t = part[0][lane];
 #pragma unroll
-        for (int j = 1; j < GATHER_WAVES; ++j) t += part[j][lane];
-        a.gsum[f] = (float)t;
+            for (int j = 1; j < GATHER_WAVES; ++j) t += part[j][lane];
+            gs = (float)t;
+            a.gsum[f] = gs;
+        }
+        if (a.cz.p) cgz_epilogue(a.cz, f, a.d, gs);
     }
 }
 
@@ -679,7 +685,7 @@ __global__ void __launch_bounds__(64 * GATHER_WAVES) k_gather(GArgs a) {
 __global__ void __launch_bounds__(64 * GATHER_WAVES) k_gather_flat(const float* __restrict__ wpart, int S, int d_mu,
                                                                    int d, const double* __restrict__ lspart, int G,
                                                                    int mp, float* __restrict__ gsum,
-                                                                   const int32_t* __restrict__ done) {
+                                                                   const int32_t* __restrict__ done, CgZ cz) {
     if (done && *done) return;
     __shared__ double part[GATHER_WAVES][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -704,11 +710,16 @@ __global__ void __launch_bounds__(64 * GATHER_WAVES) k_gather_flat(const float* 
     }
     part[w][lane] = acc;
     __syncthreads();
-    if (w == 0 && f < d) {
-        double t = part[0][lane];
+    if (w == 0) {
+        float gs = 0.f;
+        if (f < d) {
+            double t = part[0][lane];
 #pragma unroll
-        for (int j = 1; j < GATHER_WAVES; ++j) t += part[j][lane];
-        gsum[f] = (float)t;
+            for (int j = 1; j < GATHER_WAVES; ++j) t += part[j][lane];
+            gs = (float)t;
+            gsum[f] = gs;
+        }
+        if (cz.p) cgz_epilogue(cz, f, d, gs);
     }
 }
 
@@ -999,12 +1010,12 @@ int run_fused(int mode, const mjrl_shape* s, const mjrl_rows* r, int64_t T, cons
 }
 
 int run_gather(const mjrl_shape* s, const mjrl_rows* r, int64_t T, const mjrl_scratch* sc, const double* lspart,
-               const int32_t* done, float* gsum, hipStream_t st) {
+               const int32_t* done, float* gsum, hipStream_t st, CgZ cz = CgZ{}) {
     const int S = grad_slices(s, T);
     if (acc_path(s, T) == 2 && r->xs && !first_layer_only()) {   // k_kx: flat slab layout
         const int d_mu = s->d - s->m;
         hipLaunchKernelGGL(k_gather_flat, dim3((s->d + 63) / 64), dim3(64 * GATHER_WAVES), 0, st, sc->wpart, S, d_mu,
-                           s->d, lspart, ks_grid(T), s->mp, gsum, done);
+                           s->d, lspart, ks_grid(T), s->mp, gsum, done, cz);
         return (int)hipGetLastError();
     }
     JobSet js = make_jobs(s, r, S);
@@ -1023,6 +1034,7 @@ int run_gather(const mjrl_shape* s, const mjrl_rows* r, int64_t T, const mjrl_sc
     }
     ga.gsum = gsum;
     ga.done = done;
+    ga.cz = cz;
     hipLaunchKernelGGL(k_gather, dim3((s->d + 63) / 64), dim3(64 * GATHER_WAVES), 0, st, ga);
     return (int)hipGetLastError();
 }
@@ -1169,6 +1181,18 @@ int mjrl_policy_fvp(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_fvp, c
     int e = mjrl_fvp_accumulate(s, rows, T_fvp, packed_theta, packed_v, out_scale, done, sc, stream);
     if (e) return e;
     return mjrl_gather_grads(s, rows, T_fvp, sc, 0, done, gsum, stream);
+}
+
+int mjrl_gather_cg_z(const mjrl_shape* s, const mjrl_rows* rows, int64_t T, const mjrl_scratch* sc,
+                     const int32_t* done, float* gsum, double inv_T, float damping, const float* packed_theta,
+                     const float* p, float* z, float* cg, void* stream) {
+    if (!rows_ok(s, rows) || !sc || !gsum || !packed_theta || !p || !z || !cg || T < 0 || T > rows->T)
+        return MJRL_EINVAL;
+    if (!shape_supported(s->h0, s->h1, s->mp)) return MJRL_ESHAPE;
+    if ((s->d + 63) / 64 > (MJRL_CG_STATE - 16) / 2) return MJRL_EINVAL;   // partials beyond the CG state
+    const Packed pk(s->h0, s->h1, s->np, s->mp);
+    CgZ cz{p, z, cg, packed_theta + pk.ls, inv_T, damping, s->d - s->m};
+    return run_gather(s, rows, T, sc, nullptr, done, gsum, (hipStream_t)stream, cz);
 }
 
 int mjrl_fused_path(const mjrl_shape* s) { return s ? acc_path(s, 1) : 0; }

@@ -177,9 +177,10 @@ class UpdateEngine:
         self.vec = {k: torch.zeros(s.d, **f32) for k in ("g", "gsum", "x", "r", "p", "z", "theta_new")}
         self.cg = torch.zeros(_lib.CG_STATE, **f32)   # MJRL_CG_STATE
         self.done = torch.zeros(1, dtype=torch.int32, device=dev)
-        self.out = torch.zeros(4, **f32)
+        self.out = torch.zeros(_lib.STEP_OUT, **f32)     # MJRL_STEP_OUT (results + step scratch)
         self.stats = torch.zeros(N_STATS, dtype=torch.float64, device=dev)
         self.mom_part = torch.zeros(4 * 256 + 16, dtype=torch.float64, device=dev)
+        self.mom2_part = torch.zeros(_lib.MOM_SCRATCH, dtype=torch.float64, device=dev)   # one-launch moments
         self.transforms = (None, None, None, None)
         self.kernel_timing = None   # list -> (start, accumulate done, gather done) events per FVP
         self.fused = bool(self.lib.mjrl_fused_path(C.byref(self.shape)))
@@ -372,10 +373,12 @@ class UpdateEngine:
         T, T_demo, P = batch.T, batch.T_demo, batch.P
         T_all = T + T_demo
         # global row count (all ranks): scales every mean
-        if T_global is None:
+        if T_global is None and self.comm.world_size > 1:
             tg = torch.tensor([float(T)], dtype=torch.float64, device=self.device)
             self.comm.allreduce_sum(tg)
-            T_global = float(tg.item()) if self.comm.world_size > 1 else float(T)
+            T_global = float(tg.item())
+        elif T_global is None:
+            T_global = float(T)
         sub = None
         if hvp_sample_frac is not None and hvp_sample_frac < 0.99 and algo != "vpg":
             sub = self._hvp_draws(float(hvp_sample_frac), int(round(T_global)), T, int(cg_iters))
@@ -406,26 +409,32 @@ class UpdateEngine:
         self._pack(batch.obs, batch.act, T_all, st)
         main.wait_stream(side)
         # whitening (npg_cg.py:91) and path-return statistics (npg_cg.py:97-102):
-        # two-pass fp64 moments; when sharded, each pass's sums of both quantities
-        # share one all-reduce (plus one MAX for the path-return extrema)
-        self._moments(adv64, T, S_M1, reduce=False)
-        self._moments(w["path_ret"], P, S_PM1, reduce=False)
+        # two-pass fp64 moments, both quantities in one launch per pass; when
+        # sharded, each pass's sums share one all-reduce (plus one MAX for the
+        # path-return extrema)
+        sp_ = lambda slot: C.c_void_p(self.stats[slot:].data_ptr())
+        mp2 = _lib.ptr(self.mom2_part)
+        _lib.check(L.mjrl_moments2(_lib.ptr(adv64), T, None, _lib.ptr(w["path_ret"]), P, None, mp2, sp_(S_M1),
+                                   sp_(S_PM1), st), "mjrl_moments2")
         self._allreduce_slots([(S_M1, 3), (S_PM1, 3)])
         self.comm.allreduce_max(self.stats[S_PM1 + 4:S_PM1 + 6])
-        self._moments(adv64, T, S_M2, center_slot=S_M1, reduce=False)
-        self._moments(w["path_ret"], P, S_PM2, center_slot=S_PM1, reduce=False)
+        _lib.check(L.mjrl_moments2(_lib.ptr(adv64), T, sp_(S_M1), _lib.ptr(w["path_ret"]), P, sp_(S_PM1), mp2,
+                                   sp_(S_M2), sp_(S_PM2), st), "mjrl_moments2")
         self._allreduce_slots([(S_M2, 3), (S_PM2, 3)])
         dapg = algo == "dapg" and demo_coef is not None
-        _lib.check(L.mjrl_whiten(_lib.ptr(adv64), T, C.c_void_p(self.stats[S_M1:].data_ptr()),
-                                 C.c_void_p(self.stats[S_M2:].data_ptr()), 1e-6, _lib.ptr(w["adv32"]),
-                                 _lib.ptr(w["w64"]) if dapg else None, st), "mjrl_whiten")
-        # surr_before = mean(LR * adv) with LR == 1 (npg_cg.py:113); its all-reduce rides
-        # with the first post-step evaluation's
-        self._moments(w["adv32"], T, S_MS, f32=True, reduce=False)
+        # whitening + surr_before = mean(LR * adv) with LR == 1 (npg_cg.py:113) in one
+        # launch; the surr_before all-reduce rides with the first post-step evaluation's
+        _lib.check(L.mjrl_whiten_moments(_lib.ptr(adv64), T, sp_(S_M1), sp_(S_M2), 1e-6, _lib.ptr(w["adv32"]),
+                                         _lib.ptr(w["w64"]) if dapg else None, mp2, sp_(S_MS), st),
+                   "mjrl_whiten_moments")
         ms_pending = [True]
         if dapg:
-            self._moments(w["w64"], T, S_MW1)
-            self._moments(w["w64"], T, S_MW2, center_slot=S_MW1)
+            _lib.check(L.mjrl_moments2(_lib.ptr(w["w64"]), T, None, None, 0, None, mp2, sp_(S_MW1), None, st),
+                       "mjrl_moments2")
+            self._allreduce_slots([(S_MW1, 3)])
+            _lib.check(L.mjrl_moments2(_lib.ptr(w["w64"]), T, sp_(S_MW1), None, 0, None, mp2, sp_(S_MW2), None, st),
+                       "mjrl_moments2")
+            self._allreduce_slots([(S_MW2, 3)])
             _lib.check(L.mjrl_dapg_adv(_lib.ptr(w["w64"]), T, C.c_void_p(self.stats[S_MW1:].data_ptr()),
                                        C.c_void_p(self.stats[S_MW2:].data_ptr()), T_demo, float(demo_coef),
                                        _lib.ptr(w["adv_vpg"]), st), "mjrl_dapg_adv")
@@ -461,6 +470,9 @@ class UpdateEngine:
                        "mjrl_cg_init")
             prof = self.kernel_timing
             inv_T_fvp = inv_T if sub is None else 1.0 / max(sub["Ts"], 1)
+            # gather + CG z fused when no all-reduce sits between them and the CG
+            # state holds one p.z partial per 64 parameters
+            fuse_cg = self.comm.world_size == 1 and (s.d + 63) // 64 <= (_lib.CG_STATE - 16) // 2
             for k in range(int(cg_iters)):
                 rows_k, sc_k, T_k = rows_fvp, sc_fvp, T
                 if sub is not None:
@@ -473,11 +485,23 @@ class UpdateEngine:
                                                  C.byref(sc_k), st), "mjrl_fvp_accumulate")
                 if prof is not None:
                     e1.record()
-                _lib.check(L.mjrl_gather_grads(sp, C.byref(rows_k), T_k, C.byref(sc_k), 0, _lib.ptr(self.done),
-                                               _lib.ptr(v["gsum"]), st), "mjrl_gather_grads")
+                if fuse_cg:
+                    # one process: the slab gather and the z step of the CG iteration in one launch
+                    _lib.check(L.mjrl_gather_cg_z(sp, C.byref(rows_k), T_k, C.byref(sc_k), _lib.ptr(self.done),
+                                                  _lib.ptr(v["gsum"]), inv_T_fvp, float(damping),
+                                                  _lib.ptr(self.packed_theta), _lib.ptr(v["p"]), _lib.ptr(v["z"]),
+                                                  _lib.ptr(self.cg), st), "mjrl_gather_cg_z")
+                else:
+                    _lib.check(L.mjrl_gather_grads(sp, C.byref(rows_k), T_k, C.byref(sc_k), 0, _lib.ptr(self.done),
+                                                   _lib.ptr(v["gsum"]), st), "mjrl_gather_grads")
                 if prof is not None:
                     e2.record()
                     prof.append((e0, e1, e2))
+                if fuse_cg:
+                    _lib.check(L.mjrl_cg_step_xr_p(sp, _lib.ptr(v["x"]), _lib.ptr(v["r"]), _lib.ptr(v["p"]),
+                                                   _lib.ptr(v["z"]), _lib.ptr(self.packed_p), _lib.ptr(self.cg),
+                                                   _lib.ptr(self.done), float(residual_tol), st), "mjrl_cg_step_xr_p")
+                    continue
                 self.comm.allreduce_sum(v["gsum"])
                 _lib.check(L.mjrl_cg_step(sp, _lib.ptr(v["gsum"]), inv_T_fvp, float(damping),
                                           _lib.ptr(self.packed_theta),
@@ -544,11 +568,9 @@ class UpdateEngine:
                 evaluate()
         timing[3].record()
 
-        # single readback
-        torch.cuda.current_stream().synchronize()
-        stats = self.stats.cpu().numpy()
-        out = self.out.cpu().numpy()
-        cg = self.cg.cpu().numpy()
+        # single readback: the statistics, the step results and the CG counters in
+        # three async copies into one pinned buffer, one synchronisation
+        stats, out, cg = self._readback()
         if sub is not None and sub["rng"] is not None:
             # the reference stops drawing when its CG exits early: replay only the
             # draws of the FVPs that ran, so numpy's global RNG ends in the same state
@@ -577,6 +599,18 @@ class UpdateEngine:
         return result
 
     # ------------------------------------------------------------------
+    def _readback(self):
+        h = getattr(self, "_host_res", None)
+        if h is None:
+            h = self._host_res = (torch.empty(N_STATS, dtype=torch.float64, pin_memory=True),
+                                  torch.empty(8, dtype=torch.float32, pin_memory=True),
+                                  torch.empty(8, dtype=torch.float32, pin_memory=True))
+        h[0].copy_(self.stats, non_blocking=True)
+        h[1].copy_(self.out[:8], non_blocking=True)
+        h[2].copy_(self.cg[:8], non_blocking=True)
+        torch.cuda.current_stream(self.device).synchronize()
+        return h[0].numpy().copy(), h[1].numpy().copy(), h[2].numpy().copy()
+
     @_on_device
     def fit_linear_baseline(self, batch, baseline, returns=None, return_errors=False):
         """LinearBaseline.fit (baselines/linear_baseline.py:20-44) on the batch's

@@ -218,6 +218,8 @@ def main():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only to rehearse the N > 1 "
                          "path with several ranks on one GPU)")
+    ap.add_argument("--graph", action=argparse.BooleanOptionalAction, default=True,
+                    help="replay each update as one captured hipGraph (one GPU; default on)")
     ap.add_argument("--precision", default=None, choices=["auto", "split", "f32"],
                     help="first-layer MFMA form (UpdateEngine precision; default: split where supported)")
     args = ap.parse_args()
@@ -251,14 +253,17 @@ def main():
     upd = dict(algo="npg", gamma=GAMMA, gae_lambda=LAM, n_step_size=DELTA, cg_iters=CG_ITERS, damping=DAMPING,
                T_global=float(T_total))
 
-    def step():
+    eng.graphs = args.graph and world == 1
+    eng.kernel_timing = []   # per-FVP (start, accumulate done, gather done) events
+
+    def step(graph=None):
         nonlocal th
-        eng.update(batch, th, **upd)
+        eng.update(batch, th, graph=graph, **upd)
         th = eng.vec["theta_new"].clone()
 
     for _ in range(args.warmup):
         step()
-    eng.kernel_timing = []
+    eng.kernel_timing.clear()
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -274,10 +279,33 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # dominant-kernel roofline from the live events of the timed region
-    ev = eng.kernel_timing
-    t_acc = np.mean([a.elapsed_time(b) for a, b, _ in ev]) / 1e3
-    t_gat = np.mean([b.elapsed_time(c) for _, b, c in ev]) / 1e3
+    # dominant-kernel roofline from live HIP events on the launch stream.  Eager
+    # steps record them around every FVP of the timed region; a replayed hipGraph
+    # holds them as captured event nodes (valid after each replay completes), read
+    # over three more replays
+    graphed = eng.graph_kernel_timing() is not None
+    samples = [(a.elapsed_time(b), b.elapsed_time(c)) for a, b, c in eng.kernel_timing]
+    eager_ms = None
+    if graphed:
+        for _ in range(3):
+            step()
+            torch.cuda.synchronize()
+            samples += [(a.elapsed_time(b), b.elapsed_time(c)) for a, b, c in eng.graph_kernel_timing()]
+        # the same update without the graph, for reference
+        torch.cuda.synchronize()
+        te = time.perf_counter()
+        for _ in range(2):
+            step(graph=False)
+        torch.cuda.synchronize()
+        eager_ms = (time.perf_counter() - te) / 2 * 1e3
+        samples = [sm for sm in samples if np.isfinite(sm[0])]
+    if not samples:   # no events available: time the accumulate / gather pair alone
+        eng.kernel_timing = []
+        step(graph=False)
+        samples = [(a.elapsed_time(b), b.elapsed_time(c)) for a, b, c in eng.kernel_timing]
+    t_acc = np.mean([a for a, _ in samples]) / 1e3
+    t_gat = np.mean([b for _, b in samples]) / 1e3
+    ev = samples
     fl = flops_per_row(N_OBS, N_ACT, *HIDDEN)
     rows_rank = batch.T
     path = eng.accumulate_path()
@@ -346,6 +374,7 @@ def main():
                    config=dict(workload="humanoid_npg_1M", obs_dim=N_OBS, act_dim=N_ACT, hidden=list(HIDDEN),
                                timesteps=T_total, paths=args.paths, horizon=HORIZON, cg_iters=CG_ITERS,
                                parallelism="dp%d" % world),
+                   hipgraph=bool(graphed), eager_ms_per_step=None if eager_ms is None else round(eager_ms, 3),
                    roofline=roof)
         if world == 1 and not args.no_e2e:
             out["e2e_from_host"] = e2e_from_host((p0, p1), eng, th, base, upd, device)

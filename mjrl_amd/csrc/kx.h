@@ -774,15 +774,10 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
                 for (int rr = 0; rr < 4; ++rr) g2[rr] += t[rr] * s4[rr];
             }
         };
-#ifdef MJRL_KX_P5SWAP
-        // the two waves of a SIMD (kh = 0 / 1) run the phase's two halves in opposite
-        // order, so one issues the weight-gradient MFMAs while the other is in the
-        // VALU-heavy gu0 epilogue
-        if (kh == 0) { p5_gu0(); p5_gw(); } else { p5_gw(); p5_gu0(); }
-#else
+        // (running the two halves in opposite orders on the two waves of a SIMD,
+        // kh = 0 / 1, measured 0.5 %: the phase is issue-bound, not latency-bound)
         p5_gu0();
         p5_gw();
-#endif
         __syncthreads();
         KX_STAMP(7);
 

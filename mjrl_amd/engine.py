@@ -72,6 +72,15 @@ class _PinnedStaging:
 _STAGING = _PinnedStaging()
 
 
+class _NoEvent:
+    """Stand-in timing event for graph captures that cannot hold event records."""
+    def record(self, stream=None):
+        pass
+
+    def elapsed_time(self, other):
+        return float("nan")
+
+
 def _on_device(fn):
     """Runs an UpdateEngine method with self.device current, so torch's current
     stream (the one every kernel is launched on, _lib.stream_ptr) belongs to the
@@ -183,6 +192,8 @@ class UpdateEngine:
         self.mom2_part = torch.zeros(_lib.MOM_SCRATCH, dtype=torch.float64, device=dev)   # one-launch moments
         self.transforms = (None, None, None, None)
         self.kernel_timing = None   # list -> (start, accumulate done, gather done) events per FVP
+        self.graphs = False         # capture / replay whole updates as hipGraphs (one process)
+        self._gstate = {}
         self.fused = bool(self.lib.mjrl_fused_path(C.byref(self.shape)))
         prec = precision or os.environ.get("MJRL_AMD_PRECISION", "auto")
         if prec not in ("auto", "split", "f32"):
@@ -354,7 +365,7 @@ class UpdateEngine:
     def update(self, batch, theta, *, algo="npg", gamma=0.995, gae_lambda=0.98, n_step_size=0.01,
                const_lr=None, kl_dist=None, cg_iters=10, damping=1e-4, residual_tol=1e-10,
                demo_coef=None, learn_rate=0.01, T_global=None, trpo_verbose=True, skip_gae=False,
-               hvp_sample_frac=None):
+               hvp_sample_frac=None, graph=None):
         """One policy update.  `theta`: f32 device tensor [d] (flat params, reference
         order).  algo in {'npg', 'trpo', 'dapg', 'vpg'}.
 
@@ -366,6 +377,9 @@ class UpdateEngine:
         np.random.choice(T_global, int(frac T_global)) rows from numpy's global RNG
         (npg_cg.py:58-62); rank 0 draws, the draw is broadcast, and after the update
         the RNG is left where the reference's early-exiting CG would leave it.
+        graph (default self.graphs): replay a captured hipGraph of the update when
+        the batch, shape and arguments repeat (npg / vpg, one process, no
+        subsampled Fisher; see _maybe_capture).
         Returns host scalars plus the new device theta (self.vec['theta_new'])."""
         L = self.lib
         s = self.shape
@@ -389,160 +403,185 @@ class UpdateEngine:
         v = self.vec
         sp = C.byref(s)
         ins, isc, osh, osc = self.transforms
-        timing = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        use_graph = ((self.graphs if graph is None else graph) and self.comm.world_size == 1 and sub is None
+                     and algo in ("npg", "vpg"))
+        if use_graph:
+            key = self._graph_key(batch, T_global, (algo, gamma, gae_lambda, n_step_size, const_lr, kl_dist, cg_iters,
+                                                    damping, residual_tol, learn_rate, skip_gae))
+            gs = self._gstate
+            if gs.get("graph") is not None and gs["key"] == key:
+                # replay: the whole update is one graph launch; theta enters through
+                # the captured input buffer
+                gs["theta_in"].copy_(theta)
+                gs["graph"].replay()
+                self.last_T, self.last_T_global = T, T_global
+                return self._finish(algo, const_lr, gs["delta"], T_global, None, [], gs["timing"])
 
-        # a1-a3: returns / advantages.  The scan is a serial fp64 chain per path
-        # (latency-bound, few waves): it runs on a side stream beside the HBM-bound
-        # batch assembly and joins before the moments.
-        main = torch.cuda.current_stream(self.device)
-        side = self._side_stream()
-        self._baseline_of(batch)
-        side.wait_stream(main)
-        adv64 = w["adv64"]
-        if batch.advantages is not None:
-            adv64 = batch.advantages
-            # path returns still come from the rewards (npg_cg.py:97)
-            self.returns_advantages(batch, gamma, None, stream=C.c_void_p(side.cuda_stream))
-        elif not skip_gae:
-            self.returns_advantages(batch, gamma, gae_lambda, stream=C.c_void_p(side.cuda_stream))
-        # a5: batch assembly (f64 -> f32, input normalisation, bias column)
-        self._pack(batch.obs, batch.act, T_all, st)
-        main.wait_stream(side)
-        # whitening (npg_cg.py:91) and path-return statistics (npg_cg.py:97-102):
-        # two-pass fp64 moments, both quantities in one launch per pass; when
-        # sharded, each pass's sums share one all-reduce (plus one MAX for the
-        # path-return extrema)
-        sp_ = lambda slot: C.c_void_p(self.stats[slot:].data_ptr())
-        mp2 = _lib.ptr(self.mom2_part)
-        _lib.check(L.mjrl_moments2(_lib.ptr(adv64), T, None, _lib.ptr(w["path_ret"]), P, None, mp2, sp_(S_M1),
-                                   sp_(S_PM1), st), "mjrl_moments2")
-        self._allreduce_slots([(S_M1, 3), (S_PM1, 3)])
-        self.comm.allreduce_max(self.stats[S_PM1 + 4:S_PM1 + 6])
-        _lib.check(L.mjrl_moments2(_lib.ptr(adv64), T, sp_(S_M1), _lib.ptr(w["path_ret"]), P, sp_(S_PM1), mp2,
-                                   sp_(S_M2), sp_(S_PM2), st), "mjrl_moments2")
-        self._allreduce_slots([(S_M2, 3), (S_PM2, 3)])
-        dapg = algo == "dapg" and demo_coef is not None
-        # whitening + surr_before = mean(LR * adv) with LR == 1 (npg_cg.py:113) in one
-        # launch; the surr_before all-reduce rides with the first post-step evaluation's
-        _lib.check(L.mjrl_whiten_moments(_lib.ptr(adv64), T, sp_(S_M1), sp_(S_M2), 1e-6, _lib.ptr(w["adv32"]),
-                                         _lib.ptr(w["w64"]) if dapg else None, mp2, sp_(S_MS), st),
-                   "mjrl_whiten_moments")
-        ms_pending = [True]
-        if dapg:
-            _lib.check(L.mjrl_moments2(_lib.ptr(w["w64"]), T, None, None, 0, None, mp2, sp_(S_MW1), None, st),
-                       "mjrl_moments2")
-            self._allreduce_slots([(S_MW1, 3)])
-            _lib.check(L.mjrl_moments2(_lib.ptr(w["w64"]), T, sp_(S_MW1), None, 0, None, mp2, sp_(S_MW2), None, st),
-                       "mjrl_moments2")
-            self._allreduce_slots([(S_MW2, 3)])
-            _lib.check(L.mjrl_dapg_adv(_lib.ptr(w["w64"]), T, C.c_void_p(self.stats[S_MW1:].data_ptr()),
-                                       C.c_void_p(self.stats[S_MW2:].data_ptr()), T_demo, float(demo_coef),
-                                       _lib.ptr(w["adv_vpg"]), st), "mjrl_dapg_adv")
-            adv_vpg = w["adv_vpg"]
-            T_vpg = T_all
-        else:
-            adv_vpg = w["adv32"]
-            T_vpg = T
-        inv_T = 1.0 / T_global
-        self.last_T, self.last_T_global = T, T_global
+        def launch(theta, ev):
+            """Every device launch of the update up to the first evaluation (the
+            TRPO line search continues on the host); `ev` makes timing events.
+            Under graph capture the current stream is the capture stream."""
+            st = _lib.stream_ptr()
+            self.st = st
+            timing = [ev() for _ in range(4)]
 
-        # a6-a11: forward + VPG (caches a0, a1, mu0, ll0)
-        _lib.check(L.mjrl_pack_params(sp, _lib.ptr(theta), _lib.ptr(self.packed_theta), 1, self.min_log_std, st),
-                   "mjrl_pack_params")
-        sc = self._scratch(T_vpg)
-        rows = self._rows(T_vpg, adv_vpg)
-        timing[0].record()
-        _lib.check(L.mjrl_policy_vpg(sp, C.byref(rows), _lib.ptr(self.packed_theta), _lib.ptr(osh), _lib.ptr(osc),
-                                     C.byref(sc), _lib.ptr(v["gsum"]), st), "mjrl_policy_vpg")
-        self.comm.allreduce_sum(v["gsum"])
-        _lib.check(L.mjrl_scale_vec(_lib.ptr(v["gsum"]), s.d, inv_T, _lib.ptr(v["g"]), st), "mjrl_scale_vec")
-        timing[1].record()
-
-        # a12-a13: conjugate gradient with the device FVP
-        rows_fvp = self._rows(T, adv_vpg)
-        sc_fvp = self._scratch(T) if T_vpg != T else sc
-        if algo == "vpg":
-            x = v["g"]
-            cg_iters_run = 0
-        else:
-            _lib.check(L.mjrl_cg_init(sp, _lib.ptr(v["g"]), _lib.ptr(v["x"]), _lib.ptr(v["r"]), _lib.ptr(v["p"]),
-                                      _lib.ptr(self.packed_p), _lib.ptr(self.cg), _lib.ptr(self.done), st),
-                       "mjrl_cg_init")
-            prof = self.kernel_timing
-            inv_T_fvp = inv_T if sub is None else 1.0 / max(sub["Ts"], 1)
-            # gather + CG z fused when no all-reduce sits between them and the CG
-            # state holds one p.z partial per 64 parameters
-            fuse_cg = self.comm.world_size == 1 and (s.d + 63) // 64 <= (_lib.CG_STATE - 16) // 2
-            for k in range(int(cg_iters)):
-                rows_k, sc_k, T_k = rows_fvp, sc_fvp, T
-                if sub is not None:
-                    rows_k, sc_k, T_k = self._subsample_rows(sub, k, adv_vpg)
-                if prof is not None:
-                    e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
-                    e0.record()
-                _lib.check(L.mjrl_fvp_accumulate(sp, C.byref(rows_k), T_k, _lib.ptr(self.packed_theta),
-                                                 _lib.ptr(self.packed_p), _lib.ptr(osc), _lib.ptr(self.done),
-                                                 C.byref(sc_k), st), "mjrl_fvp_accumulate")
-                if prof is not None:
-                    e1.record()
-                if fuse_cg:
-                    # one process: the slab gather and the z step of the CG iteration in one launch
-                    _lib.check(L.mjrl_gather_cg_z(sp, C.byref(rows_k), T_k, C.byref(sc_k), _lib.ptr(self.done),
-                                                  _lib.ptr(v["gsum"]), inv_T_fvp, float(damping),
-                                                  _lib.ptr(self.packed_theta), _lib.ptr(v["p"]), _lib.ptr(v["z"]),
-                                                  _lib.ptr(self.cg), st), "mjrl_gather_cg_z")
-                else:
-                    _lib.check(L.mjrl_gather_grads(sp, C.byref(rows_k), T_k, C.byref(sc_k), 0, _lib.ptr(self.done),
-                                                   _lib.ptr(v["gsum"]), st), "mjrl_gather_grads")
-                if prof is not None:
-                    e2.record()
-                    prof.append((e0, e1, e2))
-                if fuse_cg:
-                    _lib.check(L.mjrl_cg_step_xr_p(sp, _lib.ptr(v["x"]), _lib.ptr(v["r"]), _lib.ptr(v["p"]),
-                                                   _lib.ptr(v["z"]), _lib.ptr(self.packed_p), _lib.ptr(self.cg),
-                                                   _lib.ptr(self.done), float(residual_tol), st), "mjrl_cg_step_xr_p")
-                    continue
-                self.comm.allreduce_sum(v["gsum"])
-                _lib.check(L.mjrl_cg_step(sp, _lib.ptr(v["gsum"]), inv_T_fvp, float(damping),
-                                          _lib.ptr(self.packed_theta),
-                                          _lib.ptr(v["x"]), _lib.ptr(v["r"]), _lib.ptr(v["p"]), _lib.ptr(v["z"]),
-                                          _lib.ptr(self.packed_p), _lib.ptr(self.cg), _lib.ptr(self.done),
-                                          float(residual_tol), st), "mjrl_cg_step")
-            x = v["x"]
-            cg_iters_run = None
-        timing[2].record()
-
-        # a14: step size + update; a16 TRPO backtracking
-        def step(mode, delta, alpha_in, const):
-            _lib.check(L.mjrl_npg_step(sp, _lib.ptr(v["g"]), _lib.ptr(x), _lib.ptr(theta), mode, float(delta),
-                                       float(alpha_in), int(const), self.min_log_std, _lib.ptr(v["theta_new"]),
-                                       _lib.ptr(self.packed_new), _lib.ptr(self.out), st), "mjrl_npg_step")
-
-        def evaluate():
-            _lib.check(L.mjrl_policy_eval(sp, C.byref(rows_fvp), T, _lib.ptr(self.packed_new),
-                                          _lib.ptr(self.packed_theta), _lib.ptr(osh), _lib.ptr(osc),
-                                          C.byref(sc_fvp), C.c_void_p(self.stats[S_EVAL:].data_ptr()), st),
-                       "mjrl_policy_eval")
-            if ms_pending[0]:
-                self._allreduce_slots([(S_MS, 3), (S_EVAL, 2)])
-                ms_pending[0] = False
+            # a1-a3: returns / advantages.  The scan is a serial fp64 chain per path
+            # (latency-bound, few waves): it runs on a side stream beside the HBM-bound
+            # batch assembly and joins before the moments.
+            main = torch.cuda.current_stream(self.device)
+            side = self._side_stream()
+            self._baseline_of(batch)
+            side.wait_stream(main)
+            adv64 = w["adv64"]
+            if batch.advantages is not None:
+                adv64 = batch.advantages
+                # path returns still come from the rewards (npg_cg.py:97)
+                self.returns_advantages(batch, gamma, None, stream=C.c_void_p(side.cuda_stream))
+            elif not skip_gae:
+                self.returns_advantages(batch, gamma, gae_lambda, stream=C.c_void_p(side.cuda_stream))
+            # a5: batch assembly (f64 -> f32, input normalisation, bias column)
+            self._pack(batch.obs, batch.act, T_all, st)
+            main.wait_stream(side)
+            # whitening (npg_cg.py:91) and path-return statistics (npg_cg.py:97-102):
+            # two-pass fp64 moments, both quantities in one launch per pass; when
+            # sharded, each pass's sums share one all-reduce (plus one MAX for the
+            # path-return extrema)
+            sp_ = lambda slot: C.c_void_p(self.stats[slot:].data_ptr())
+            mp2 = _lib.ptr(self.mom2_part)
+            _lib.check(L.mjrl_moments2(_lib.ptr(adv64), T, None, _lib.ptr(w["path_ret"]), P, None, mp2, sp_(S_M1),
+                                       sp_(S_PM1), st), "mjrl_moments2")
+            self._allreduce_slots([(S_M1, 3), (S_PM1, 3)])
+            self.comm.allreduce_max(self.stats[S_PM1 + 4:S_PM1 + 6])
+            _lib.check(L.mjrl_moments2(_lib.ptr(adv64), T, sp_(S_M1), _lib.ptr(w["path_ret"]), P, sp_(S_PM1), mp2,
+                                       sp_(S_M2), sp_(S_PM2), st), "mjrl_moments2")
+            self._allreduce_slots([(S_M2, 3), (S_PM2, 3)])
+            dapg = algo == "dapg" and demo_coef is not None
+            # whitening + surr_before = mean(LR * adv) with LR == 1 (npg_cg.py:113) in one
+            # launch; the surr_before all-reduce rides with the first post-step evaluation's
+            _lib.check(L.mjrl_whiten_moments(_lib.ptr(adv64), T, sp_(S_M1), sp_(S_M2), 1e-6, _lib.ptr(w["adv32"]),
+                                             _lib.ptr(w["w64"]) if dapg else None, mp2, sp_(S_MS), st),
+                       "mjrl_whiten_moments")
+            ms_pending = [True]
+            if dapg:
+                _lib.check(L.mjrl_moments2(_lib.ptr(w["w64"]), T, None, None, 0, None, mp2, sp_(S_MW1), None, st),
+                           "mjrl_moments2")
+                self._allreduce_slots([(S_MW1, 3)])
+                _lib.check(L.mjrl_moments2(_lib.ptr(w["w64"]), T, sp_(S_MW1), None, 0, None, mp2, sp_(S_MW2), None, st),
+                           "mjrl_moments2")
+                self._allreduce_slots([(S_MW2, 3)])
+                _lib.check(L.mjrl_dapg_adv(_lib.ptr(w["w64"]), T, C.c_void_p(self.stats[S_MW1:].data_ptr()),
+                                           C.c_void_p(self.stats[S_MW2:].data_ptr()), T_demo, float(demo_coef),
+                                           _lib.ptr(w["adv_vpg"]), st), "mjrl_dapg_adv")
+                adv_vpg = w["adv_vpg"]
+                T_vpg = T_all
             else:
-                self._allreduce_slots([(S_EVAL, 2)])
+                adv_vpg = w["adv32"]
+                T_vpg = T
+            inv_T = 1.0 / T_global
+            self.last_T, self.last_T_global = T, T_global
 
+            # a6-a11: forward + VPG (caches a0, a1, mu0, ll0)
+            _lib.check(L.mjrl_pack_params(sp, _lib.ptr(theta), _lib.ptr(self.packed_theta), 1, self.min_log_std, st),
+                       "mjrl_pack_params")
+            sc = self._scratch(T_vpg)
+            rows = self._rows(T_vpg, adv_vpg)
+            timing[0].record()
+            _lib.check(L.mjrl_policy_vpg(sp, C.byref(rows), _lib.ptr(self.packed_theta), _lib.ptr(osh), _lib.ptr(osc),
+                                         C.byref(sc), _lib.ptr(v["gsum"]), st), "mjrl_policy_vpg")
+            self.comm.allreduce_sum(v["gsum"])
+            _lib.check(L.mjrl_scale_vec(_lib.ptr(v["gsum"]), s.d, inv_T, _lib.ptr(v["g"]), st), "mjrl_scale_vec")
+            timing[1].record()
+
+            # a12-a13: conjugate gradient with the device FVP
+            rows_fvp = self._rows(T, adv_vpg)
+            sc_fvp = self._scratch(T) if T_vpg != T else sc
+            if algo == "vpg":
+                x = v["g"]
+                cg_iters_run = 0
+            else:
+                _lib.check(L.mjrl_cg_init(sp, _lib.ptr(v["g"]), _lib.ptr(v["x"]), _lib.ptr(v["r"]), _lib.ptr(v["p"]),
+                                          _lib.ptr(self.packed_p), _lib.ptr(self.cg), _lib.ptr(self.done), st),
+                           "mjrl_cg_init")
+                prof = self.kernel_timing
+                inv_T_fvp = inv_T if sub is None else 1.0 / max(sub["Ts"], 1)
+                # gather + CG z fused when no all-reduce sits between them and the CG
+                # state holds one p.z partial per 64 parameters
+                fuse_cg = self.comm.world_size == 1 and (s.d + 63) // 64 <= (_lib.CG_STATE - 16) // 2
+                for k in range(int(cg_iters)):
+                    rows_k, sc_k, T_k = rows_fvp, sc_fvp, T
+                    if sub is not None:
+                        rows_k, sc_k, T_k = self._subsample_rows(sub, k, adv_vpg)
+                    if prof is not None:
+                        e0, e1, e2 = (ev() for _ in range(3))
+                        e0.record()
+                    _lib.check(L.mjrl_fvp_accumulate(sp, C.byref(rows_k), T_k, _lib.ptr(self.packed_theta),
+                                                     _lib.ptr(self.packed_p), _lib.ptr(osc), _lib.ptr(self.done),
+                                                     C.byref(sc_k), st), "mjrl_fvp_accumulate")
+                    if prof is not None:
+                        e1.record()
+                    if fuse_cg:
+                        # one process: the slab gather and the z step of the CG iteration in one launch
+                        _lib.check(L.mjrl_gather_cg_z(sp, C.byref(rows_k), T_k, C.byref(sc_k), _lib.ptr(self.done),
+                                                      _lib.ptr(v["gsum"]), inv_T_fvp, float(damping),
+                                                      _lib.ptr(self.packed_theta), _lib.ptr(v["p"]), _lib.ptr(v["z"]),
+                                                      _lib.ptr(self.cg), st), "mjrl_gather_cg_z")
+                    else:
+                        _lib.check(L.mjrl_gather_grads(sp, C.byref(rows_k), T_k, C.byref(sc_k), 0, _lib.ptr(self.done),
+                                                       _lib.ptr(v["gsum"]), st), "mjrl_gather_grads")
+                    if prof is not None:
+                        e2.record()
+                        prof.append((e0, e1, e2))
+                    if fuse_cg:
+                        _lib.check(L.mjrl_cg_step_xr_p(sp, _lib.ptr(v["x"]), _lib.ptr(v["r"]), _lib.ptr(v["p"]),
+                                                       _lib.ptr(v["z"]), _lib.ptr(self.packed_p), _lib.ptr(self.cg),
+                                                       _lib.ptr(self.done), float(residual_tol), st), "mjrl_cg_step_xr_p")
+                        continue
+                    self.comm.allreduce_sum(v["gsum"])
+                    _lib.check(L.mjrl_cg_step(sp, _lib.ptr(v["gsum"]), inv_T_fvp, float(damping),
+                                              _lib.ptr(self.packed_theta),
+                                              _lib.ptr(v["x"]), _lib.ptr(v["r"]), _lib.ptr(v["p"]), _lib.ptr(v["z"]),
+                                              _lib.ptr(self.packed_p), _lib.ptr(self.cg), _lib.ptr(self.done),
+                                              float(residual_tol), st), "mjrl_cg_step")
+                x = v["x"]
+                cg_iters_run = None
+            timing[2].record()
+
+            # a14: step size + update; a16 TRPO backtracking
+            def step(mode, delta, alpha_in, const):
+                _lib.check(L.mjrl_npg_step(sp, _lib.ptr(v["g"]), _lib.ptr(x), _lib.ptr(theta), mode, float(delta),
+                                           float(alpha_in), int(const), self.min_log_std, _lib.ptr(v["theta_new"]),
+                                           _lib.ptr(self.packed_new), _lib.ptr(self.out), st), "mjrl_npg_step")
+
+            def evaluate():
+                _lib.check(L.mjrl_policy_eval(sp, C.byref(rows_fvp), T, _lib.ptr(self.packed_new),
+                                              _lib.ptr(self.packed_theta), _lib.ptr(osh), _lib.ptr(osc),
+                                              C.byref(sc_fvp), C.c_void_p(self.stats[S_EVAL:].data_ptr()), st),
+                           "mjrl_policy_eval")
+                if ms_pending[0]:
+                    self._allreduce_slots([(S_MS, 3), (S_EVAL, 2)])
+                    ms_pending[0] = False
+                else:
+                    self._allreduce_slots([(S_EVAL, 2)])
+
+            if algo == "vpg":
+                step(1, 0.0, np.float32(learn_rate), 0)
+                delta = None
+            elif algo == "npg" and const_lr is not None:
+                step(1, 0.0, np.float32(const_lr), 1)
+                delta = None
+            elif algo == "npg":
+                delta = n_step_size if kl_dist is None else 2.0 * kl_dist
+                step(0, delta, 0.0, 0)
+            else:   # trpo / dapg: delta = 2 kl_dist
+                delta = 2.0 * kl_dist
+                step(0, delta, 0.0, 0)
+            evaluate()
+            if algo != "trpo":
+                timing[3].record()
+            return step, evaluate, delta, x, timing, inv_T
+
+        step, evaluate, delta, x, timing, inv_T = launch(theta, lambda: torch.cuda.Event(enable_timing=True))
         trials = []
-        if algo == "vpg":
-            step(1, 0.0, np.float32(learn_rate), 0)
-            delta = None
-        elif algo == "npg" and const_lr is not None:
-            step(1, 0.0, np.float32(const_lr), 1)
-            delta = None
-        elif algo == "npg":
-            delta = n_step_size if kl_dist is None else 2.0 * kl_dist
-            step(0, delta, 0.0, 0)
-        else:   # trpo / dapg: delta = 2 kl_dist
-            delta = 2.0 * kl_dist
-            step(0, delta, 0.0, 0)
-        evaluate()
 
         if algo == "trpo":
             res = self.stats[S_EVAL:S_EVAL + 2].cpu().numpy()
@@ -566,10 +605,64 @@ class UpdateEngine:
             if float(alpha) != trials[-1][0]:   # final re-evaluation (trpo.py:120-123)
                 step(1, delta, alpha, 0)
                 evaluate()
-        timing[3].record()
+            timing[3].record()
+        result = self._finish(algo, const_lr, delta, T_global, sub, trials, timing)
+        if use_graph:
+            self._maybe_capture(key, launch, theta, delta, T_global)
+        return result
 
+    # ------------------------------------------------------------------
+    # hipGraph replay of whole updates (one process): the second consecutive
+    # update with the same batch buffers, shape and arguments is captured, later
+    # ones replay it as ONE graph launch (the ~60 kernel launches of an update
+    # then cost no host time and leave no launch gaps).  Theta enters through a
+    # captured device buffer; everything else the graph reads is the batch and
+    # the engine workspace, whose addresses are part of the key.
+    def _graph_key(self, batch, T_global, args):
+        ptrs = tuple(0 if t is None else t.data_ptr() for t in (
+            batch.obs, batch.act, batch.rewards, batch.baseline, batch.path_off, batch.terminated, batch.advantages)
+            + tuple(self.transforms))
+        return (ptrs, batch.T, batch.T_demo, batch.P, float(T_global), id(self.ws), self.kernel_timing is not None,
+                tuple(args))
+
+    def _maybe_capture(self, key, launch, theta, delta, T_global):
+        gs = self._gstate
+        if gs.get("seen") != key:          # first sighting: remember, stay eager
+            gs.clear()
+            gs["seen"] = key
+            return
+        theta_in = torch.empty_like(theta)
+        theta_in.copy_(theta)
+        prof_saved = self.kernel_timing
+        for ev in (lambda: torch.cuda.Event(enable_timing=True, external=True), _NoEvent):
+            if prof_saved is not None:
+                self.kernel_timing = []    # the capture's own per-FVP events
+            g = torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.graph(g):
+                    out = launch(theta_in, ev)
+            except Exception as e:         # timing events inside a capture unsupported: capture without
+                err = e
+                continue
+            finally:
+                graph_prof = self.kernel_timing
+                self.kernel_timing = prof_saved
+            gs.update(key=key, graph=g, theta_in=theta_in, timing=out[4], delta=delta, prof=graph_prof)
+            return
+        import warnings
+        warnings.warn("mjrl_amd: hipGraph capture of the update failed (%s); staying eager" % (err,))
+        self.graphs = False
+        gs.clear()
+
+    def graph_kernel_timing(self):
+        """(start, accumulate done, gather done) external events of every FVP of the
+        captured graph, valid after a replay has completed; None without a graph."""
+        return self._gstate.get("prof")
+
+    def _finish(self, algo, const_lr, delta, T_global, sub, trials, timing):
         # single readback: the statistics, the step results and the CG counters in
         # three async copies into one pinned buffer, one synchronisation
+        inv_T = 1.0 / T_global
         stats, out, cg = self._readback()
         if sub is not None and sub["rng"] is not None:
             # the reference stops drawing when its CG exits early: replay only the

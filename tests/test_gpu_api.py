@@ -411,3 +411,38 @@ def test_train_step_baseline_fit_path():
     hb, ha = host.fit(paths, return_errors=True)
     np.testing.assert_allclose([eb, ea], [hb, ha], rtol=1e-9)
     np.testing.assert_allclose(base._coeffs, host._coeffs, rtol=1e-7, atol=1e-9)
+
+
+@pytest.mark.parametrize("name", ["c2_swimmer", "c4_humanoid"])
+def test_graph_replay_matches_eager(name):
+    """UpdateEngine.graphs: the second identical update is captured as a hipGraph
+    and later ones replay it; the replayed update must equal the eager one bit
+    for bit (same kernels, same order, same reductions)."""
+    from oracle import npg_cpu as O
+    from mjrl_amd.engine import UpdateEngine
+    import test_gpu_parity as P
+    c = O.load_case(os.path.join(GOLDEN, name + ".npz"))
+    dev = torch.device("cuda:0")
+    eng = UpdateEngine(int(c["n"]), int(c["m"]), c["hidden_t"], device=dev)
+    batch = P.make_batch(c, dev)
+    th = torch.from_numpy(c["theta0"].astype(np.float32)).to(dev)
+    args = dict(algo="npg", gamma=float(c["gamma"]), gae_lambda=float(c["gae_lambda"]), n_step_size=0.05)
+    ref = eng.update(batch, th, graph=False, **args)
+    ref_theta = eng.vec["theta_new"].cpu().numpy()
+    eng.graphs = True
+    outs = []
+    for _ in range(4):
+        res = eng.update(batch, th, **args)
+        outs.append((res, eng.vec["theta_new"].cpu().numpy()))
+    assert eng._gstate.get("graph") is not None
+    for res, theta in outs:
+        assert np.array_equal(theta, ref_theta)
+        for k in ("alpha", "kl_dist", "surr_after", "surr_before", "cg_iters"):
+            assert res[k] == ref[k], k
+        np.testing.assert_array_equal(res["base_stats"], ref["base_stats"])
+    # a different theta through the captured input buffer
+    th2 = th * 1.01
+    eng.update(batch, th2, graph=False, **args)
+    ref2 = eng.vec["theta_new"].cpu().numpy()
+    eng.update(batch, th2, **args)
+    assert np.array_equal(eng.vec["theta_new"].cpu().numpy(), ref2)

@@ -1,17 +1,23 @@
 """Benchmark: NPG update throughput (timesteps/s) on the Humanoid 1M-step batch.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-Workload (BASELINE.json configs[3]): obs 376, act 17, MLP(64,64),
-NPG with 10 CG iterations, damping 1e-4, delta 0.01, gamma 0.995, lambda 0.97;
-1000 paths x 1000 steps = 1,000,000 timesteps per update, split by paths over
-the N ranks (strong scaling: the batch is fixed).  Synthetic data: obs / act /
-rewards ~ N(0,1) from a per-path seeded generator; LinearBaseline fitted once on
-20 paths and frozen.  A step = one full update from the device-resident f64
-paths: batch assembly, GAE, whitening, forward + VPG, 10 Fisher-vector products
-+ CG, step, post-step surrogate / KL, host readback of the statistics.
+Default workload (BASELINE.json configs[3]; --config c4): obs 376,
+act 17, MLP(64,64), NPG with 10 CG iterations, damping 1e-4, delta 0.01,
+gamma 0.995, lambda 0.97; 1000 paths x 1000 steps = 1,000,000 timesteps per
+update, split by paths over the N ranks (strong scaling: the batch is fixed).
+Synthetic data: obs / act / rewards ~ N(0,1) from a per-path seeded generator;
+LinearBaseline fitted once on 20 paths and frozen.  A step = one full update
+from the device-resident f64 paths: batch assembly, GAE, whitening, forward +
+VPG, 10 Fisher-vector products + CG, step, post-step surrogate / KL, host
+readback of the statistics.  On one GPU the update is replayed as one captured
+hipGraph (--no-graph: eager launches; both times are reported).
+
+--config c2 / c3 / c5 runs the other BASELINE.json GPU shapes (Swimmer NPG,
+HalfCheetah TRPO with its line search, door DAPG with demonstrations) with their
+own metric names: per-config evidence, not the headline.
 
 Rank 0 prints one JSON line.  `roofline` is measured live with HIP events on the
 stream the kernels run on, `cpu_baseline` times the oracle (the CPU restatement
@@ -30,9 +36,24 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "NPG train_step timesteps/sec, Humanoid 1M-step batch @ 1/2/4/8 MI355X"
+GAMMA, LAM, CG_ITERS, DAMPING = 0.995, 0.97, 10, 1e-4
+CONFIGS = {
+    "c4": dict(workload="humanoid_npg_1M", metric=METRIC, n=376, m=17, hidden=(64, 64), paths=1000, horizon=1000,
+               algo="npg", step=dict(n_step_size=0.01)),
+    "c2": dict(workload="swimmer_npg_12.5k", metric="NPG update timesteps/sec, Swimmer-v2 shape 25 x 500, 1 MI355X",
+               n=8, m=2, hidden=(64, 64), paths=25, horizon=500, algo="npg", step=dict(n_step_size=0.01)),
+    "c3": dict(workload="halfcheetah_trpo_100k",
+               metric="TRPO update timesteps/sec, HalfCheetah-v2 shape 100 x 1000, 1 MI355X",
+               n=17, m=6, hidden=(128, 128), paths=100, horizon=1000, algo="trpo", step=dict(kl_dist=0.01)),
+    "c5": dict(workload="door_dapg_40k",
+               metric="DAPG update timesteps/sec, door-v0 shape 200 x 200 + 25 demos x 200, 1 MI355X",
+               n=39, m=28, hidden=(256, 256), paths=200, horizon=200, algo="dapg",
+               step=dict(kl_dist=0.005, demo_coef=1.0), demos=25),
+}
+# the default workload as module constants (used by tests)
 N_OBS, N_ACT, HIDDEN = 376, 17, (64, 64)
 N_PATHS, HORIZON = 1000, 1000
-GAMMA, LAM, DELTA, CG_ITERS, DAMPING = 0.995, 0.97, 0.01, 10, 1e-4
+DELTA = 0.01
 PEAK_F32_MFMA = 157.3   # TFLOP/s, MI355X dense fp32 matrix (MI355X_MICROARCH.md)
 PEAK_F16_MFMA = 2500.0  # TFLOP/s, dense f16 / bf16 matrix (no sparsity)
 PEAK_SPLIT = PEAK_F16_MFMA / 3   # f32-equivalent rate of the split-f16 products (3 f16 MFMAs each)
@@ -66,6 +87,14 @@ def cpu_model():
     return "unknown"
 
 
+def host_cores():
+    """CPU cores this process may run on (affinity), as the CPU baseline uses them."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
 def pmc_traffic(kernel_key):
     """HBM bytes per launch of a kernel from the newest committed PMC summary
     (profiles/r*/pmc_traffic.json, written from separate rocprofv3 --pmc passes
@@ -82,22 +111,25 @@ def pmc_traffic(kernel_key):
     return None, None
 
 
-def make_paths(p0, p1, seed=123):
+def make_paths(p0, p1, seed=123, cfg=None):
     """Paths p0..p1-1 of the synthetic batch, each from its own seeded stream
     (so a rank generates only its shard and N does not change the data)."""
+    cfg = cfg or CONFIGS["c4"]
+    H, n, m = cfg["horizon"], cfg["n"], cfg["m"]
     obs, act, rew = [], [], []
     for p in range(p0, p1):
         g = np.random.Generator(np.random.PCG64(seed * 100003 + p))
-        obs.append(g.standard_normal((HORIZON, N_OBS), dtype=np.float32))
-        act.append(g.standard_normal((HORIZON, N_ACT), dtype=np.float32))
-        rew.append(g.standard_normal(HORIZON))
+        obs.append(g.standard_normal((H, n), dtype=np.float32))
+        act.append(g.standard_normal((H, m), dtype=np.float32))
+        rew.append(g.standard_normal(H))
     return obs, act, rew
 
 
-def baseline_coeffs():
+def baseline_coeffs(cfg=None):
     from mjrl_amd.utils.gym_env import EnvSpec
     from mjrl_amd.baselines.linear_baseline import LinearBaseline
-    obs, _, rew = make_paths(0, 20)
+    cfg = cfg or CONFIGS["c4"]
+    obs, _, rew = make_paths(0, min(20, cfg["paths"]), cfg=cfg)
     paths = []
     for o, r in zip(obs, rew):
         ret = np.zeros_like(r)
@@ -106,95 +138,149 @@ def baseline_coeffs():
             acc = r[t] + GAMMA * acc
             ret[t] = acc
         paths.append(dict(observations=o.astype(np.float64), rewards=r, returns=ret))
-    b = LinearBaseline(EnvSpec(N_OBS, N_ACT, HORIZON, 1))
+    b = LinearBaseline(EnvSpec(cfg["n"], cfg["m"], cfg["horizon"], 1))
     b.fit(paths)
     return b
 
 
-def initial_theta():
+def param_shapes(cfg):
+    h0, h1 = cfg["hidden"]
+    n, m = cfg["n"], cfg["m"]
+    return [(h0, n), (h0,), (h1, h0), (h1,), (m, h1), (m,), (m,)]
+
+
+def initial_theta(cfg=None):
     """The update's starting parameters: N(0, 0.05^2) weights from RandomState(0)
     in trainable_params order, log_std 0."""
+    cfg = cfg or CONFIGS["c4"]
     rs = np.random.RandomState(0)
-    theta = np.concatenate([(rs.randn(int(np.prod(s))) * 0.05).ravel()
-                            for s in [(HIDDEN[0], N_OBS), (HIDDEN[0],), (HIDDEN[1], HIDDEN[0]), (HIDDEN[1],),
-                                      (N_ACT, HIDDEN[1]), (N_ACT,), (N_ACT,)]]).astype(np.float32)
-    theta[-N_ACT:] = 0.0
+    theta = np.concatenate([(rs.randn(int(np.prod(s))) * 0.05).ravel() for s in param_shapes(cfg)]).astype(np.float32)
+    theta[-cfg["m"]:] = 0.0
     return theta
 
 
-def stage_shard(p0, p1, device, base):
+def demo_share(cfg, rank, world):
+    """This rank's demonstration paths (DAPG): a contiguous share, each demo row
+    staged once over all ranks (DAPG._rank_share)."""
+    nd = cfg.get("demos", 0)
+    if not nd:
+        return None
+    from mjrl_amd.comm import partition_paths
+    d0, d1 = partition_paths(np.full(nd, cfg["horizon"]), world)[rank]
+    o, a, _ = make_paths(d0, d1, seed=977, cfg=cfg)
+    return o, a
+
+
+def stage_shard(p0, p1, device, base, cfg=None, demos=None):
     from mjrl_amd.engine import DeviceBatch
-    obs, act, rew = make_paths(p0, p1)
+    cfg = cfg or CONFIGS["c4"]
+    H, n, m = cfg["horizon"], cfg["n"], cfg["m"]
+    obs, act, rew = make_paths(p0, p1, cfg=cfg)
     P = p1 - p0
-    T = P * HORIZON
-    ho = torch.empty((T, N_OBS), dtype=torch.float64, pin_memory=True)
+    T = P * H
+    T_demo = 0
+    if demos is not None:
+        obs, act = obs + demos[0], act + demos[1]
+        T_demo = sum(len(o) for o in demos[0])
+    ho = torch.empty((T + T_demo, n), dtype=torch.float64, pin_memory=True)
     np.concatenate(obs, out=ho.numpy())
-    ha = torch.empty((T, N_ACT), dtype=torch.float64, pin_memory=True)
+    ha = torch.empty((T + T_demo, m), dtype=torch.float64, pin_memory=True)
     np.concatenate(act, out=ha.numpy())
     rw = np.concatenate(rew)
-    bl = np.concatenate([base.predict(dict(observations=o.astype(np.float64), rewards=r)) for o, r in zip(obs, rew)])
-    off = (np.arange(P + 1, dtype=np.int64) * HORIZON)
+    bl = np.concatenate([base.predict(dict(observations=o.astype(np.float64), rewards=r))
+                         for o, r in zip(obs[:P], rew)])
+    off = (np.arange(P + 1, dtype=np.int64) * H)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)
-    return DeviceBatch(ho.to(device), ha.to(device), t(rw), t(bl), t(off), t(np.zeros(P, np.uint8)))
+    return DeviceBatch(ho.to(device), ha.to(device), t(rw), t(bl), t(off), t(np.zeros(P, np.uint8)), T_demo=T_demo)
 
 
-def cpu_baseline(rows, base, reps=3):
-    """The oracle (CPU restatement of the reference update) on `rows` timesteps:
-    one warm-up update on a tenth of the sample, then the median of `reps`."""
+def update_args(cfg, T_total):
+    upd = dict(algo=cfg["algo"], gamma=GAMMA, gae_lambda=LAM, cg_iters=CG_ITERS, damping=DAMPING,
+               T_global=float(T_total), trpo_verbose=False)
+    upd.update(cfg["step"])
+    return upd
+
+
+def cpu_baseline(rows, base, reps=3, cfg=None):
+    """The oracle (CPU restatement of the reference update) on `rows` timesteps,
+    torch on all the host cores this process may use: one warm-up update on a
+    tenth of the sample, then the median of `reps`."""
     from oracle import npg_cpu as O
-    P = rows // HORIZON
-    obs, act, rew = make_paths(0, P)
+    cfg = cfg or CONFIGS["c4"]
+    H, n, m, hidden = cfg["horizon"], cfg["n"], cfg["m"], cfg["hidden"]
+    cores = host_cores()
+    torch.set_num_threads(cores)
+    P = max(1, rows // H)
+    obs, act, rew = make_paths(0, P, cfg=cfg)
     obs = np.concatenate(obs).astype(np.float64)
     act = np.concatenate(act).astype(np.float64)
     rew = np.concatenate(rew)
-    lengths = np.full(P, HORIZON)
+    lengths = np.full(P, H)
     bl = np.concatenate([base.predict(dict(observations=o, rewards=r))
                          for o, r in zip(O.split(obs, lengths), O.split(rew, lengths))])
-    theta = np.concatenate([(np.random.RandomState(1).randn(int(np.prod(s))) * 0.05).ravel()
-                            for s in O.param_shapes(N_OBS, N_ACT, HIDDEN)]).astype(np.float32)
-    theta[-N_ACT:] = 0.0
+    theta = initial_theta(cfg)
+    kw = dict(algo=cfg["algo"], cg_iters=CG_ITERS, damping=DAMPING)
+    if cfg["algo"] == "npg":
+        kw["n_step_size"] = cfg["step"]["n_step_size"]
+    else:
+        kw["kl_dist"] = cfg["step"]["kl_dist"]
+    if cfg["algo"] == "dapg":
+        dmo = demo_share(cfg, 0, 1)
+        kw.update(demo_obs=np.concatenate(dmo[0]).astype(np.float64),
+                  demo_act=np.concatenate(dmo[1]).astype(np.float64), demo_coef=cfg["step"]["demo_coef"])
 
     def one(r):
-        pol = O.Policy(N_OBS, N_ACT, HIDDEN, theta.astype(np.float64), None)
-        Pr = r // HORIZON
+        pol = O.Policy(n, m, hidden, theta.astype(np.float64), None)
+        Pr = max(1, r // H)
+        r = Pr * H
         t0 = time.perf_counter()
         ret, adv = O.returns_and_advantages(rew[:r], bl[:r], lengths[:Pr], np.zeros(Pr, bool), GAMMA, LAM)
-        O.update(pol, obs[:r], act[:r], adv, rew[:r], lengths[:Pr], algo="npg", n_step_size=DELTA,
-                 cg_iters=CG_ITERS, damping=DAMPING)
+        O.update(pol, obs[:r], act[:r], adv, rew[:r], lengths[:Pr], **kw)
         return time.perf_counter() - t0
 
-    one(max(HORIZON, (rows // 10) // HORIZON * HORIZON))
-    ts = sorted(one(P * HORIZON) for _ in range(reps))
+    one(max(H, (P * H // 10) // H * H))
+    ts = sorted(one(P * H) for _ in range(reps))
     dt = ts[len(ts) // 2]
-    return dict(value=P * HORIZON / dt, unit="timesteps/s", cores=torch.get_num_threads(), kind="port",
-                cpu=cpu_model(),
-                sample="%d paths x %d steps (%d timesteps) of the same Humanoid-shape workload, one update "
-                       "(returns + GAE + train_from_paths), oracle/npg_cpu.py on %d torch threads: median of %d "
-                       "updates %.2f s (all: %s)" % (P, HORIZON, P * HORIZON, torch.get_num_threads(), reps, dt,
-                                                    ", ".join("%.2f" % t for t in ts)))
+    return dict(value=round(P * H / dt, 1), unit="timesteps/s", cores=cores, kind="port", cpu=cpu_model(),
+                sample="%d paths x %d steps (%d timesteps) of the same %s workload, one update "
+                       "(returns + GAE + train_from_paths), oracle/npg_cpu.py on %d torch threads (the process's "
+                       "CPU affinity): median of %d updates %.2f s (all: %s)"
+                       % (P, H, P * H, cfg["workload"], cores, reps, dt, ", ".join("%.2f" % t for t in ts)))
 
 
-def e2e_from_host(paths_range, eng, th0, base, upd, device, reps=2):
+def host_threads():
+    from mjrl_amd.engine import _host_threads
+    return _host_threads()
+
+
+def e2e_from_host(paths_range, eng, th0, base, upd, device, cfg, reps=3):
     """End-to-end update from numpy sampler paths (what train_agent sees):
-    pinned staging + H2D + device LinearBaseline predict + update + readback.
+    f64 paths -> threaded f32 conversion into reused pinned slabs, chunked H2D
+    overlapping it -> device LinearBaseline predict -> update -> readback.
     Reported beside `value` (never as it): SURVEY.md §8 d1."""
     from mjrl_amd.engine import DeviceBatch
     p0, p1 = paths_range
-    obs, act, rew = make_paths(p0, p1)
+    obs, act, rew = make_paths(p0, p1, cfg=cfg)
     paths = [dict(observations=o.astype(np.float64), actions=a.astype(np.float64), rewards=r, terminated=False)
              for o, a, r in zip(obs, act, rew)]
     del obs, act
     T = sum(len(p["rewards"]) for p in paths)
     th = th0.clone()
+    stage_ms = []
 
     def one():
         nonlocal th
-        b = DeviceBatch.from_paths(paths, device, baseline=base)
+        t0 = time.perf_counter()
+        b = DeviceBatch.from_paths(paths, device, baseline=base, reuse=True)
+        torch.cuda.synchronize()
+        stage_ms.append((time.perf_counter() - t0) * 1e3)
         eng.update(b, th, **upd)
         th = eng.vec["theta_new"].clone()
         torch.cuda.synchronize()
 
     one()
+    one()
+    stage_ms.clear()
     ts = []
     for _ in range(reps):
         t0 = time.perf_counter()
@@ -202,8 +288,28 @@ def e2e_from_host(paths_range, eng, th0, base, upd, device, reps=2):
         ts.append(time.perf_counter() - t0)
     dt = float(np.median(ts))
     return dict(value=round(T / dt, 1), unit="timesteps/s", ms_per_step=round(dt * 1e3, 2),
-                note="numpy f64 paths -> pinned staging (reused) -> H2D -> device LinearBaseline.predict -> "
-                     "update -> readback; median of %d" % reps)
+                staging_ms=round(float(np.median(stage_ms)), 2),
+                note="numpy f64 paths -> f32 into reused pinned slabs on %d host threads, chunked H2D "
+                     "overlapping the conversion -> device LinearBaseline.predict -> update -> readback; "
+                     "median of %d (staging_ms: the staging alone, synchronised)" % (host_threads(), reps))
+
+
+def kernel_names(eng, cfg):
+    """(name, rocprof key, flops/row) of the FVP accumulate step and of the gather."""
+    fl = flops_per_row(cfg["n"], cfg["m"], *cfg["hidden"])
+    path = eng.accumulate_path()
+    np_, mp = eng.shape.np, eng.shape.mp
+    h0, h1 = cfg["hidden"]
+    if path == 0:   # row-chain kernel then split-K weight-gradient kernel, both inside the accumulate step
+        return ("k_rows<%d,%d,%d,FVP>+k_wgrad" % (h0, h1, mp), "k_rows<", fl["rows_fvp"] + fl["weight_grads"],
+                "k_gather", "k_gather", 0)
+    if path == 2 and eng.split:
+        acc = ("k_kx<%d,%d,FVP>" % (mp, np_ // 32), "k_kx<%d, %d, 1>" % (mp, np_ // 32))
+    elif path == 2:
+        acc = ("k_ks<%d,%d,FVP>" % (mp, np_ // 32), "k_ks<%d, %d, 1, false>" % (mp, np_ // 32))
+    else:
+        acc = ("k_fused<%d,%d,%d,FVP>" % (h0, h1, mp), "k_fused<")
+    return acc + (fl["rows_fvp"] + fl["weight_grads"], "k_gather", "k_gather", 0)
 
 
 def main():
@@ -211,10 +317,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--paths", type=int, default=N_PATHS)
-    ap.add_argument("--cpu-rows", type=int, default=200000)
+    ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
+    ap.add_argument("--paths", type=int, default=None, help="paths per update (default: the config's)")
+    ap.add_argument("--cpu-rows", type=int, default=200000,
+                    help="timesteps of the bounded CPU-baseline sample (c4; the other configs use their full batch)")
+    ap.add_argument("--cpu-full", action="store_true", help="CPU baseline on the full batch of the config")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end-from-host-paths measurement")
+    ap.add_argument("--no-f32", action="store_true", help="skip the exact-f32 companion timing")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only to rehearse the N > 1 "
                          "path with several ranks on one GPU)")
@@ -223,6 +333,10 @@ def main():
     ap.add_argument("--precision", default=None, choices=["auto", "split", "f32"],
                     help="first-layer MFMA form (UpdateEngine precision; default: split where supported)")
     args = ap.parse_args()
+    cfg = dict(CONFIGS[args.config])
+    if args.paths:
+        cfg["paths"] = args.paths
+    n, m, hidden, H = cfg["n"], cfg["m"], cfg["hidden"], cfg["horizon"]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -243,23 +357,22 @@ def main():
     from mjrl_amd.comm import partition_paths
     from mjrl_amd.engine import UpdateEngine
 
-    base = baseline_coeffs()
-    p0, p1 = partition_paths(np.full(args.paths, HORIZON), world)[rank]
-    batch = stage_shard(p0, p1, device, base)
-    T_total = args.paths * HORIZON
+    base = baseline_coeffs(cfg)
+    p0, p1 = partition_paths(np.full(cfg["paths"], H), world)[rank]
+    batch = stage_shard(p0, p1, device, base, cfg, demo_share(cfg, rank, world))
+    T_total = cfg["paths"] * H
 
-    eng = UpdateEngine(N_OBS, N_ACT, HIDDEN, device=device, comm=comm, precision=args.precision)
-    th = torch.from_numpy(initial_theta()).to(device)
-    upd = dict(algo="npg", gamma=GAMMA, gae_lambda=LAM, n_step_size=DELTA, cg_iters=CG_ITERS, damping=DAMPING,
-               T_global=float(T_total))
-
+    eng = UpdateEngine(n, m, hidden, device=device, comm=comm, precision=args.precision)
+    th0 = torch.from_numpy(initial_theta(cfg)).to(device)
+    th = th0.clone()
+    upd = update_args(cfg, T_total)
     eng.graphs = args.graph and world == 1
     eng.kernel_timing = []   # per-FVP (start, accumulate done, gather done) events
 
-    def step(graph=None):
+    def step(graph=None, e=eng):
         nonlocal th
-        eng.update(batch, th, graph=graph, **upd)
-        th = eng.vec["theta_new"].clone()
+        e.update(batch, th, graph=graph, **upd)
+        th = e.vec["theta_new"].clone()
 
     for _ in range(args.warmup):
         step()
@@ -291,10 +404,9 @@ def main():
             step()
             torch.cuda.synchronize()
             samples += [(a.elapsed_time(b), b.elapsed_time(c)) for a, b, c in eng.graph_kernel_timing()]
-        # the same update without the graph, for reference
         torch.cuda.synchronize()
         te = time.perf_counter()
-        for _ in range(2):
+        for _ in range(2):   # the same update without the graph, for reference
             step(graph=False)
         torch.cuda.synchronize()
         eager_ms = (time.perf_counter() - te) / 2 * 1e3
@@ -305,30 +417,17 @@ def main():
         samples = [(a.elapsed_time(b), b.elapsed_time(c)) for a, b, c in eng.kernel_timing]
     t_acc = np.mean([a for a, _ in samples]) / 1e3
     t_gat = np.mean([b for _, b in samples]) / 1e3
-    ev = samples
-    fl = flops_per_row(N_OBS, N_ACT, *HIDDEN)
+    acc_name, acc_key, acc_fl, gat_name, gat_key, gat_fl = kernel_names(eng, cfg)
     rows_rank = batch.T
-    path = eng.accumulate_path()
-    np_, mp = eng.shape.np, eng.shape.mp
+    np_ = eng.shape.np
+    h0, h1 = hidden
     # algorithmic HBM bytes per row of one FVP launch: the observation row (f32, or the
     # split-f16 hi / lo pair + row scale) and the cached a0 / a1 activations
-    fvp_bytes = 4 * np_ + (4 if eng.split else 0) + 4 * (HIDDEN[0] + HIDDEN[1])
-    if path == 0:   # rows kernel then split-K weight-gradient kernel: time each
-        acc_name, acc_key, acc_fl = "k_rows<64,64,32,FVP>", "k_rows<64, 64, 32, 1>", fl["rows_fvp"]
-        gat_name, gat_key, gat_fl = "k_wgrad", "k_wgrad", fl["weight_grads"]
-    else:           # one persistent kernel does both; the gather is a pure slab reduction
-        if path == 2 and eng.split:
-            acc_name, acc_key = "k_kx<%d,%d,FVP>" % (mp, np_ // 32), "k_kx<%d, %d, 1>" % (mp, np_ // 32)
-        elif path == 2:
-            acc_name, acc_key = "k_ks<%d,%d,FVP>" % (mp, np_ // 32), "k_ks<%d, %d, 1, false>" % (mp, np_ // 32)
-        else:
-            acc_name, acc_key = "k_fused<64,64,%d,FVP>" % mp, "k_fused<"
-        acc_fl = fl["rows_fvp"] + fl["weight_grads"]
-        gat_name, gat_key, gat_fl = "k_gather", "k_gather", 0
+    fvp_bytes = 4 * np_ + (4 if eng.split else 0) + 4 * (h0 + h1)
     kern = {acc_name: dict(avg_ms=t_acc * 1e3, tflops=acc_fl * rows_rank / t_acc / 1e12),
             gat_name: dict(avg_ms=t_gat * 1e3, tflops=gat_fl * rows_rank / t_gat / 1e12)}
     dom = max(kern, key=lambda k: kern[k]["avg_ms"])
-    traffic, tsrc = pmc_traffic(acc_key if dom == acc_name else gat_key)
+    traffic, tsrc = pmc_traffic(acc_key if dom == acc_name else gat_key) if args.config == "c4" else (None, None)
     if traffic is not None and rows_rank != N_PATHS * HORIZON:
         # the committed PMC pass is the default 1-GPU launch (1M rows); scale per row
         traffic = traffic * rows_rank / (N_PATHS * HORIZON)
@@ -355,31 +454,53 @@ def main():
                           % PEAK_SPLIT if eng.split else "f32 (v_mfma_f32_16x16x4_f32)",
                 ideal_ms=dict(mfma=round(t_mm * 1e3, 4), hbm=round(t_hbm * 1e3, 4)),
                 achieved_tflops=round(flops_dom / t_dom / 1e12, 3),
-                launches=len(ev), kernels={k: {kk: round(vv, 4) for kk, vv in v.items()} for k, v in kern.items()})
+                launches=len(samples), kernels={k: {kk: round(vv, 4) for kk, vv in v.items()}
+                                                for k, v in kern.items()})
     # whole-update algorithmic FLOP rate, all kernels and gaps included
-    ufl = update_flops_per_row(N_OBS, N_ACT, HIDDEN[0], HIDDEN[1], CG_ITERS)
+    ufl = update_flops_per_row(n, m, h0, h1, CG_ITERS)
     ut = ufl * T_total / (elapsed / args.steps) / 1e12
     roof["update"] = dict(flops_per_timestep=ufl, achieved=round(ut, 3), unit="TFLOP/s",
                           frac_f32_peak=round(ut / (PEAK_F32_MFMA * world), 4),
                           note="algorithmic FLOPs of a whole update / wall time per update, vs n_gpus x the "
                                "f32 matrix peak")
 
+    # the same update on the exact-f32 MFMA kernels (precision='f32'), for reference
+    f32_ms = None
+    if world == 1 and eng.split and not args.no_f32:
+        e32 = UpdateEngine(n, m, hidden, device=device, precision="f32")
+        e32.graphs = args.graph
+        th = th0.clone()
+        for _ in range(2):
+            step(e=e32)
+        torch.cuda.synchronize()
+        tf = time.perf_counter()
+        for _ in range(3):
+            step(e=e32)
+        torch.cuda.synchronize()
+        f32_ms = (time.perf_counter() - tf) / 3 * 1e3
+        del e32
+        torch.cuda.empty_cache()
+
     if rank == 0:
         ms = elapsed / args.steps * 1e3
-        out = dict(metric=METRIC, value=round(T_total * args.steps / elapsed, 1), unit="timesteps/s",
+        out = dict(metric=cfg["metric"], value=round(T_total * args.steps / elapsed, 1), unit="timesteps/s",
                    n_gpus=world, steps=args.steps, warmup=args.warmup, ms_per_step=round(ms, 3),
                    higher_is_better=True, scaling="strong", vs_baseline=None,
                    dtype="f32" if not eng.split else "f32 (split-f16 MFMA, f32 accumulate)",
                    data="synthetic (seeded N(0,1) obs/act/rewards, LinearBaseline fitted on 20 paths)",
-                   config=dict(workload="humanoid_npg_1M", obs_dim=N_OBS, act_dim=N_ACT, hidden=list(HIDDEN),
-                               timesteps=T_total, paths=args.paths, horizon=HORIZON, cg_iters=CG_ITERS,
+                   config=dict(workload=cfg["workload"], obs_dim=n, act_dim=m, hidden=list(hidden),
+                               algo=cfg["algo"], timesteps=T_total, paths=cfg["paths"], horizon=H,
+                               demo_timesteps=cfg.get("demos", 0) * H, cg_iters=CG_ITERS,
                                parallelism="dp%d" % world),
                    hipgraph=bool(graphed), eager_ms_per_step=None if eager_ms is None else round(eager_ms, 3),
+                   f32_ms_per_step=None if f32_ms is None else round(f32_ms, 3),
                    roofline=roof)
-        if world == 1 and not args.no_e2e:
-            out["e2e_from_host"] = e2e_from_host((p0, p1), eng, th, base, upd, device)
+        if world == 1 and not args.no_e2e and cfg["algo"] != "dapg":
+            th = th0.clone()
+            out["e2e_from_host"] = e2e_from_host((p0, p1), eng, th, base, upd, device, cfg)
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_rows, base)
+            rows = T_total if (args.cpu_full or args.config != "c4") else args.cpu_rows
+            out["cpu_baseline"] = cpu_baseline(rows, base, cfg=cfg)
         print(json.dumps(out))
     if world > 1:
         torch.distributed.destroy_process_group()

@@ -99,6 +99,15 @@ int mjrl_pack_batch(const double* obs, const double* act, int64_t T, const mjrl_
 int mjrl_pack_batch_split(const double* obs, const double* act, int64_t T, const mjrl_shape* s,
                           const float* in_shift, const float* in_scale, void* xs, float* xu,
                           float* act32, void* stream);
+/* The same two with observations / actions staged as f32 by the host (the
+ * policy's own input precision: gaussian_mlp.py:103 casts every observation to
+ * f32, so the policy passes see identical values). */
+int mjrl_pack_batch_f32(const float* obs, const float* act, int64_t T, const mjrl_shape* s,
+                        const float* in_shift, const float* in_scale, float* xhat, float* act32,
+                        void* stream);
+int mjrl_pack_batch_split_f32(const float* obs, const float* act, int64_t T, const mjrl_shape* s,
+                              const float* in_shift, const float* in_scale, void* xs, float* xu,
+                              float* act32, void* stream);
 /* 1 if the policy passes for this shape accept split-f16 rows (mjrl_rows.xs): the
  * K = np first layer then runs as three f16 MFMAs per product (hi*hi + hi*lo +
  * lo*hi, f32 accumulate), the rest of the network in exact f32. */
@@ -118,6 +127,10 @@ int mjrl_gae(const double* rew, const double* base, const int64_t* path_off,
 int mjrl_linear_baseline(const double* obs, int64_t T, int32_t n, const int64_t* path_off,
                          int64_t P, const double* coeffs, double* out, void* stream);
 
+/* The same from f32-staged observations (features computed in fp64 from them). */
+int mjrl_linear_baseline_f32(const float* obs, int64_t T, int32_t n, const int64_t* path_off,
+                             int64_t P, const double* coeffs, double* out, void* stream);
+
 /* ---- LinearBaseline.fit normal equations on device (baselines/linear_baseline.py:20-44) ----
  * Gram matrix of the augmented rows [f_t, y_t], f_t = [clip(obs_t, +-10), a, a^2, a^3, 1]
  * (a = (t - path start)/1000, as _features), y_t = returns: out[K][K] row-major fp64 with
@@ -129,11 +142,17 @@ int mjrl_linear_baseline_gram_scratch(int32_t n, int64_t T, int64_t* doubles);
 int mjrl_linear_baseline_gram(const double* obs, const double* returns, int64_t T, int32_t n,
                               const int64_t* path_off, int64_t P, double* scratch, double* out,
                               void* stream);
+int mjrl_linear_baseline_gram_f32(const float* obs, const double* returns, int64_t T, int32_t n,
+                                  const int64_t* path_off, int64_t P, double* scratch, double* out,
+                                  void* stream);
 /* out[t] = returns[t] - f_t . coeffs (fit(return_errors=True)'s residuals);
  * scratch as for mjrl_linear_baseline_gram. */
 int mjrl_linear_baseline_residual(const double* obs, const double* returns, int64_t T, int32_t n,
                                   const int64_t* path_off, int64_t P, const double* coeffs,
                                   double* scratch, double* out, void* stream);
+int mjrl_linear_baseline_residual_f32(const float* obs, const double* returns, int64_t T, int32_t n,
+                                      const int64_t* path_off, int64_t P, const double* coeffs,
+                                      double* scratch, double* out, void* stream);
 
 /* ---- subsampled Fisher rows (npg_cg.py:58-62: obs[rand_idx], act[rand_idx]) ----
  * dst row i = src row idx[i] for i < n, rows of row_bytes bytes (a multiple of 4);

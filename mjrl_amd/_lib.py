@@ -51,9 +51,12 @@ SIGNATURES = {
     "mjrl_scratch_size": [SP, I64, C.POINTER(I64), C.POINTER(I64), C.POINTER(I32)],
     "mjrl_pack_batch": [P, P, I64, SP, P, P, P, P, P],
     "mjrl_pack_batch_split": [P, P, I64, SP, P, P, P, P, P, P],
+    "mjrl_pack_batch_f32": [P, P, I64, SP, P, P, P, P, P],
+    "mjrl_pack_batch_split_f32": [P, P, I64, SP, P, P, P, P, P, P],
     "mjrl_split_supported": [SP],
     "mjrl_gae": [P, P, P, P, I64, F64, F64, I32, P, P, P, P],
     "mjrl_linear_baseline": [P, I64, I32, P, I64, P, P, P],
+    "mjrl_linear_baseline_f32": [P, I64, I32, P, I64, P, P, P],
     "mjrl_moments": [P, I64, P, P, P, P],
     "mjrl_moments_f32": [P, I64, P, P, P, P],
     "mjrl_moments2": [P, I64, P, P, I64, P, P, P, P, P],
@@ -79,6 +82,8 @@ SIGNATURES = {
     "mjrl_linear_baseline_gram_scratch": [I32, I64, C.POINTER(I64)],
     "mjrl_linear_baseline_gram": [P, P, I64, I32, P, I64, P, P, P],
     "mjrl_linear_baseline_residual": [P, P, I64, I32, P, I64, P, P, P, P],
+    "mjrl_linear_baseline_gram_f32": [P, P, I64, I32, P, I64, P, P, P],
+    "mjrl_linear_baseline_residual_f32": [P, P, I64, I32, P, I64, P, P, P, P],
     "mjrl_npg_step": [SP, P, P, P, I32, F32, F32, I32, F32, P, P, P, P],
 }
 

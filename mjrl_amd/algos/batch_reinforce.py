@@ -43,6 +43,10 @@ def _samplers():
 
 class BatchREINFORCE:
     algo = "vpg"
+    # dtype the sampled observations / actions are staged to HBM in: float32 (the
+    # policy's own input precision, half the PCIe bytes) or float64 (the device
+    # LinearBaseline then predicts / fits from the sampler's exact values)
+    staging_dtype = np.float32
 
     def __init__(self, env, policy, baseline, learn_rate=0.01, seed=None, save_logs=False, device=None,
                  comm=None):
@@ -199,7 +203,8 @@ class BatchREINFORCE:
         train_from_paths, fused on the device.  Writes returns / baseline /
         advantages into the path dicts like the reference does."""
         eng = self.engine()
-        batch = DeviceBatch.from_paths(paths, eng.device, baseline=self.baseline, demo_paths=self._demo_paths())
+        batch = DeviceBatch.from_paths(paths, eng.device, baseline=self.baseline, demo_paths=self._demo_paths(),
+                                       obs_dtype=self.staging_dtype, reuse=True)
         ret, adv = eng.returns_advantages(batch, gamma, gae_lambda)
         ret, adv = ret.cpu().numpy(), adv.cpu().numpy()
         base = batch.baseline.cpu().numpy()
@@ -214,7 +219,8 @@ class BatchREINFORCE:
 
     def train_from_paths(self, paths):
         eng = self.engine()
-        batch = DeviceBatch.from_paths(paths, eng.device, use_advantages=True, demo_paths=self._demo_paths())
+        batch = DeviceBatch.from_paths(paths, eng.device, use_advantages=True, demo_paths=self._demo_paths(),
+                                       obs_dtype=self.staging_dtype, reuse=True)
         return self._update(batch, paths)
 
     # ---- hooks for subclasses ---------------------------------------------------

@@ -44,10 +44,11 @@ __global__ void __launch_bounds__(256) k_path_time(const int64_t* __restrict__ o
 }
 
 // feature g of row `row` (linear_baseline.py:10-18), the return as feature n + 4, zero pad
-__device__ __forceinline__ double feat(const double* __restrict__ obs, const double* __restrict__ y,
+template <typename TO>
+__device__ __forceinline__ double feat(const TO* __restrict__ obs, const double* __restrict__ y,
                                        const double* __restrict__ al, int64_t row, int g, int n) {
     if (g < n) {
-        const double o = obs[row * n + g];
+        const double o = (double)obs[row * n + g];
         return o < -10.0 ? -10.0 : (o > 10.0 ? 10.0 : o);
     }
     const double a = al[row];
@@ -61,8 +62,9 @@ __device__ __forceinline__ double feat(const double* __restrict__ obs, const dou
     }
 }
 
+template <typename TO>
 struct GramArgs {
-    const double* obs;
+    const TO* obs;
     const double* y;
     const double* al;
     int64_t T;
@@ -70,7 +72,8 @@ struct GramArgs {
     double* slab;   // [GSLICES][npair][GT][GT]
 };
 
-__global__ void __launch_bounds__(GTHREADS, 2) k_gram(GramArgs a) {
+template <typename TO>
+__global__ void __launch_bounds__(GTHREADS, 2) k_gram(GramArgs<TO> a) {
     __shared__ __attribute__((aligned(16))) double PI[2][GRC][GLD];
     __shared__ __attribute__((aligned(16))) double PJ[2][GRC][GLD];
     // block -> (slice, pair): the npair blocks of a slice sit on one XCD (b % 8)
@@ -175,7 +178,8 @@ __global__ void __launch_bounds__(256) k_gram_reduce(const double* __restrict__ 
 }
 
 // r_t = y_t - [clip(o_t), a, a^2, a^3, 1] . c  (fit(return_errors=True)'s residuals)
-__global__ void __launch_bounds__(256) k_linear_residual(const double* __restrict__ obs, const double* __restrict__ y,
+template <typename TO>
+__global__ void __launch_bounds__(256) k_linear_residual(const TO* __restrict__ obs, const double* __restrict__ y,
                                                          const double* __restrict__ al, int64_t T, int n,
                                                          const double* __restrict__ coef, double* __restrict__ out) {
     const int lane = threadIdx.x & 63;
@@ -183,7 +187,7 @@ __global__ void __launch_bounds__(256) k_linear_residual(const double* __restric
     for (int64_t row = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; row < T; row += nw) {
         double acc = 0.0;
         for (int j = lane; j < n; j += 64) {
-            double o = obs[row * n + j];
+            double o = (double)obs[row * n + j];
             o = o < -10.0 ? -10.0 : (o > 10.0 ? 10.0 : o);
             acc += o * coef[j];
         }
@@ -216,8 +220,10 @@ int mjrl_linear_baseline_gram_scratch(int32_t n, int64_t T, int64_t* doubles) {
     return MJRL_OK;
 }
 
-int mjrl_linear_baseline_gram(const double* obs, const double* returns, int64_t T, int32_t n,
-                              const int64_t* path_off, int64_t P, double* scratch, double* out, void* stream) {
+extern "C++" {
+template <typename TO>
+static int linear_baseline_gram(const TO* obs, const double* returns, int64_t T, int32_t n, const int64_t* path_off,
+                                int64_t P, double* scratch, double* out, void* stream) {
     if (n <= 0 || T < 0 || P < 0 || !out || !scratch || (T > 0 && (!obs || !returns || !path_off)))
         return MJRL_EINVAL;
     hipStream_t st = (hipStream_t)stream;
@@ -229,18 +235,21 @@ int mjrl_linear_baseline_gram(const double* obs, const double* returns, int64_t 
         const int64_t g = (P + 3) / 4;
         hipLaunchKernelGGL(k_path_time, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, st, path_off, P, al);
     }
-    GramArgs ga{obs, returns, al, T, n, ntile, npair, slab};
+    GramArgs<TO> ga{obs, returns, al, T, n, ntile, npair, slab};
     const int groups = (GSLICES + 7) / 8;   // slices per XCD
-    hipLaunchKernelGGL(k_gram, dim3(8 * groups * npair), dim3(GTHREADS), 0, st, ga);
+    hipLaunchKernelGGL(k_gram<TO>, dim3(8 * groups * npair), dim3(GTHREADS), 0, st, ga);
     const int64_t ne = (int64_t)npair * GT * GT;
     hipLaunchKernelGGL(k_gram_reduce, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st, slab, ntile, npair, K,
                        out);
     return err(hipGetLastError());
 }
+}  // extern "C++"
 
-int mjrl_linear_baseline_residual(const double* obs, const double* returns, int64_t T, int32_t n,
-                                  const int64_t* path_off, int64_t P, const double* coeffs, double* scratch,
-                                  double* out, void* stream) {
+extern "C++" {
+template <typename TO>
+static int linear_baseline_residual(const TO* obs, const double* returns, int64_t T, int32_t n,
+                                    const int64_t* path_off, int64_t P, const double* coeffs, double* scratch,
+                                    double* out, void* stream) {
     if (n <= 0 || T < 0 || P < 0 || (T > 0 && (!obs || !returns || !path_off || !coeffs || !scratch || !out)))
         return MJRL_EINVAL;
     if (T == 0) return MJRL_OK;
@@ -253,9 +262,32 @@ int mjrl_linear_baseline_residual(const double* obs, const double* returns, int6
         hipLaunchKernelGGL(k_path_time, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, st, path_off, P, al);
     }
     const int64_t g = (T + 3) / 4;
-    hipLaunchKernelGGL(k_linear_residual, dim3((unsigned)(g < 16384 ? g : 16384)), dim3(256), 0, st, obs, returns,
-                       al, T, n, coeffs, out);
+    hipLaunchKernelGGL(k_linear_residual<TO>, dim3((unsigned)(g < 16384 ? g : 16384)), dim3(256), 0, st, obs,
+                       returns, al, T, n, coeffs, out);
     return err(hipGetLastError());
+}
+}  // extern "C++"
+
+int mjrl_linear_baseline_gram(const double* obs, const double* returns, int64_t T, int32_t n,
+                              const int64_t* path_off, int64_t P, double* scratch, double* out, void* stream) {
+    return linear_baseline_gram(obs, returns, T, n, path_off, P, scratch, out, stream);
+}
+
+int mjrl_linear_baseline_gram_f32(const float* obs, const double* returns, int64_t T, int32_t n,
+                                  const int64_t* path_off, int64_t P, double* scratch, double* out, void* stream) {
+    return linear_baseline_gram(obs, returns, T, n, path_off, P, scratch, out, stream);
+}
+
+int mjrl_linear_baseline_residual(const double* obs, const double* returns, int64_t T, int32_t n,
+                                  const int64_t* path_off, int64_t P, const double* coeffs, double* scratch,
+                                  double* out, void* stream) {
+    return linear_baseline_residual(obs, returns, T, n, path_off, P, coeffs, scratch, out, stream);
+}
+
+int mjrl_linear_baseline_residual_f32(const float* obs, const double* returns, int64_t T, int32_t n,
+                                      const int64_t* path_off, int64_t P, const double* coeffs, double* scratch,
+                                      double* out, void* stream) {
+    return linear_baseline_residual(obs, returns, T, n, path_off, P, coeffs, scratch, out, stream);
 }
 
 }  // extern "C"

@@ -12,9 +12,10 @@ namespace {
 constexpr int MOM_BLOCKS = 256;
 constexpr int MOM_THREADS = 256;
 
-// obs f64 [T][n] -> xhat f32 [T][np]; act f64 [T][m] -> f32.  One thread per 4
-// output columns so the xhat stores are 16 B per lane.
-__global__ void __launch_bounds__(256) k_pack_batch(const double* __restrict__ obs, const double* __restrict__ act,
+// obs f64 (or f32: staged by the host) [T][n] -> xhat f32 [T][np]; act -> f32.
+// One thread per 4 output columns so the xhat stores are 16 B per lane.
+template <typename TO>
+__global__ void __launch_bounds__(256) k_pack_batch(const TO* __restrict__ obs, const TO* __restrict__ act,
                                                     int64_t T, int n, int m, int np,
                                                     const float* __restrict__ in_shift,
                                                     const float* __restrict__ in_scale, float* __restrict__ xhat,
@@ -50,7 +51,8 @@ __global__ void __launch_bounds__(256) k_pack_batch(const double* __restrict__ o
 // hi = f16(y), lo = f16(y - hi) (split8, common.h).  The xhat values are those of
 // k_pack_batch.
 constexpr int PS_MAXP = 4;   // column pairs per lane (np <= 512)
-__global__ void __launch_bounds__(256) k_pack_split(const double* __restrict__ obs, const double* __restrict__ act,
+template <typename TO>
+__global__ void __launch_bounds__(256) k_pack_split(const TO* __restrict__ obs, const TO* __restrict__ act,
                                                     int64_t T, int n, int m, int np,
                                                     const float* __restrict__ in_shift,
                                                     const float* __restrict__ in_scale, _Float16* __restrict__ xs,
@@ -61,20 +63,26 @@ __global__ void __launch_bounds__(256) k_pack_split(const double* __restrict__ o
     const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
     const int npair = (np + 127) / 128;
-    const bool even = (n & 1) == 0 && (reinterpret_cast<uintptr_t>(obs) & 15) == 0;   // 16-byte pair loads
+    const bool even = (n & 1) == 0 && (reinterpret_cast<uintptr_t>(obs) & (2 * sizeof(TO) - 1)) == 0;   // pair loads
     for (int64_t row = wid; row < T; row += nw) {
-        const double* src = obs + row * n;
+        const TO* src = obs + row * n;
         float v[PS_MAXP][2];
         float mx = 0.f;
 #pragma unroll
         for (int j = 0; j < PS_MAXP; ++j) {
             const int c = 2 * lane + 128 * j;
-            double d0 = 0.0, d1 = 0.0;
+            TO d0 = 0, d1 = 0;
             if (j < npair) {
                 if (even && c + 1 < n) {
-                    const double2 d = *reinterpret_cast<const double2*>(src + c);
-                    d0 = d.x;
-                    d1 = d.y;
+                    if constexpr (sizeof(TO) == 8) {
+                        const double2 d = *reinterpret_cast<const double2*>(src + c);
+                        d0 = d.x;
+                        d1 = d.y;
+                    } else {
+                        const float2 d = *reinterpret_cast<const float2*>(src + c);
+                        d0 = d.x;
+                        d1 = d.y;
+                    }
                 } else {
                     if (c < n) d0 = src[c];
                     if (c + 1 < n) d1 = src[c + 1];
@@ -525,7 +533,8 @@ __global__ void __launch_bounds__(256) k_dapg_adv(const double* __restrict__ w64
 //       + (t/1000)^3 c[n+2] + c[n+3], t = index within the path.
 // One wave per row (lanes across the observation, coalesced f64 loads), a
 // grid-stride over rows; the row's path comes from a binary search of path_off.
-__global__ void __launch_bounds__(256) k_linear_baseline(const double* __restrict__ obs, int64_t T, int n,
+template <typename TO>
+__global__ void __launch_bounds__(256) k_linear_baseline(const TO* __restrict__ obs, int64_t T, int n,
                                                          const int64_t* __restrict__ off, int64_t P,
                                                          const double* __restrict__ coef, double* __restrict__ out) {
     const int lane = threadIdx.x & 63;
@@ -585,28 +594,55 @@ inline int err(hipError_t e) { return e == hipSuccess ? MJRL_OK : (int)e; }
 
 extern "C" {
 
-int mjrl_pack_batch(const double* obs, const double* act, int64_t T, const mjrl_shape* s, const float* in_shift,
-                    const float* in_scale, float* xhat, float* act32, void* stream) {
+extern "C++" {
+template <typename TO>
+static int pack_batch(const TO* obs, const TO* act, int64_t T, const mjrl_shape* s, const float* in_shift,
+                      const float* in_scale, float* xhat, float* act32, void* stream) {
     if (!s || T < 0 || (T > 0 && (!obs || !act || !xhat || !act32))) return MJRL_EINVAL;
     if ((in_shift == nullptr) != (in_scale == nullptr)) return MJRL_EINVAL;
     if (T == 0) return MJRL_OK;
     const int g = grid_for(T * (s->np / 4), 256, 2048);
-    hipLaunchKernelGGL(k_pack_batch, dim3(g), dim3(256), 0, (hipStream_t)stream, obs, act, T, s->n, s->m, s->np,
+    hipLaunchKernelGGL(k_pack_batch<TO>, dim3(g), dim3(256), 0, (hipStream_t)stream, obs, act, T, s->n, s->m, s->np,
                        in_shift, in_scale, xhat, act32);
     return err(hipGetLastError());
 }
+}  // extern "C++"
 
-int mjrl_pack_batch_split(const double* obs, const double* act, int64_t T, const mjrl_shape* s,
-                          const float* in_shift, const float* in_scale, void* xs, float* xu, float* act32,
-                          void* stream) {
+extern "C++" {
+template <typename TO>
+static int pack_batch_split(const TO* obs, const TO* act, int64_t T, const mjrl_shape* s, const float* in_shift,
+                            const float* in_scale, void* xs, float* xu, float* act32, void* stream) {
     if (!s || T < 0 || (T > 0 && (!obs || !act || !xs || !xu || !act32))) return MJRL_EINVAL;
     if ((in_shift == nullptr) != (in_scale == nullptr)) return MJRL_EINVAL;
     if (s->np > 128 * PS_MAXP) return MJRL_ESHAPE;
     if (T == 0) return MJRL_OK;
     const int g = grid_for(T, 4, 8192);
-    hipLaunchKernelGGL(k_pack_split, dim3(g), dim3(256), 0, (hipStream_t)stream, obs, act, T, s->n, s->m, s->np,
+    hipLaunchKernelGGL(k_pack_split<TO>, dim3(g), dim3(256), 0, (hipStream_t)stream, obs, act, T, s->n, s->m, s->np,
                        in_shift, in_scale, (_Float16*)xs, xu, act32);
     return err(hipGetLastError());
+}
+}  // extern "C++"
+
+int mjrl_pack_batch(const double* obs, const double* act, int64_t T, const mjrl_shape* s, const float* in_shift,
+                    const float* in_scale, float* xhat, float* act32, void* stream) {
+    return pack_batch(obs, act, T, s, in_shift, in_scale, xhat, act32, stream);
+}
+
+int mjrl_pack_batch_f32(const float* obs, const float* act, int64_t T, const mjrl_shape* s, const float* in_shift,
+                        const float* in_scale, float* xhat, float* act32, void* stream) {
+    return pack_batch(obs, act, T, s, in_shift, in_scale, xhat, act32, stream);
+}
+
+int mjrl_pack_batch_split(const double* obs, const double* act, int64_t T, const mjrl_shape* s,
+                          const float* in_shift, const float* in_scale, void* xs, float* xu, float* act32,
+                          void* stream) {
+    return pack_batch_split(obs, act, T, s, in_shift, in_scale, xs, xu, act32, stream);
+}
+
+int mjrl_pack_batch_split_f32(const float* obs, const float* act, int64_t T, const mjrl_shape* s,
+                              const float* in_shift, const float* in_scale, void* xs, float* xu, float* act32,
+                              void* stream) {
+    return pack_batch_split(obs, act, T, s, in_shift, in_scale, xs, xu, act32, stream);
 }
 
 int mjrl_gae(const double* rew, const double* base, const int64_t* path_off, const uint8_t* terminated, int64_t P,
@@ -681,14 +717,27 @@ int mjrl_dapg_adv(const double* w64, int64_t T, const double* mw1, const double*
     return err(hipGetLastError());
 }
 
-int mjrl_linear_baseline(const double* obs, int64_t T, int32_t n, const int64_t* path_off, int64_t P,
-                         const double* coeffs, double* out, void* stream) {
+extern "C++" {
+template <typename TO>
+static int linear_baseline(const TO* obs, int64_t T, int32_t n, const int64_t* path_off, int64_t P,
+                           const double* coeffs, double* out, void* stream) {
     if (T < 0 || n <= 0 || P < 0 || (T > 0 && (!obs || !path_off || !coeffs || !out))) return MJRL_EINVAL;
     if (T == 0) return MJRL_OK;
     const int g = grid_for(T * 64, 256, 4096);
-    hipLaunchKernelGGL(k_linear_baseline, dim3(g), dim3(256), 0, (hipStream_t)stream, obs, T, n, path_off, P,
+    hipLaunchKernelGGL(k_linear_baseline<TO>, dim3(g), dim3(256), 0, (hipStream_t)stream, obs, T, n, path_off, P,
                        coeffs, out);
     return err(hipGetLastError());
+}
+}  // extern "C++"
+
+int mjrl_linear_baseline(const double* obs, int64_t T, int32_t n, const int64_t* path_off, int64_t P,
+                         const double* coeffs, double* out, void* stream) {
+    return linear_baseline(obs, T, n, path_off, P, coeffs, out, stream);
+}
+
+int mjrl_linear_baseline_f32(const float* obs, int64_t T, int32_t n, const int64_t* path_off, int64_t P,
+                             const double* coeffs, double* out, void* stream) {
+    return linear_baseline(obs, T, n, path_off, P, coeffs, out, stream);
 }
 
 int mjrl_gather_rows(const void* src, int64_t row_bytes, const int64_t* idx, int64_t n, void* dst, void* stream) {

@@ -27,6 +27,11 @@ S_M1, S_M2, S_PM1, S_PM2, S_MS, S_MW1, S_MW2, S_EVAL = 0, 8, 16, 24, 32, 40, 48,
 N_STATS = 64
 
 
+def _thread_safe_predict(baseline):
+    """numpy baselines predict in parallel threads; torch-module baselines do not."""
+    return type(baseline).__name__ in ("QuadraticBaseline", "ZeroBaseline", "LinearBaseline")
+
+
 def _linear_coeffs(baseline, n):
     """Coefficients when `baseline` is a LinearBaseline (mjrl's or ours: same
     features, baselines/linear_baseline.py:10-18) — None before its first fit —
@@ -39,33 +44,125 @@ def _linear_coeffs(baseline, n):
     return c if len(c) == n + 4 else False
 
 
+def _host_threads():
+    """Host threads for staging: this process's CPU share (affinity), at most 16."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
 class _PinnedStaging:
-    """Grow-only pinned host buffers reused across batches (one per slot), so a
-    training loop does not pay a multi-GB cudaHostAlloc per train_step.  A slot
-    is reused only after the H2D copy that last read it has completed."""
+    """Host -> HBM staging of sampler paths.
+
+    Per slot (obs, act, rewards, ...) a grow-only pinned host buffer and, for
+    reuse=True callers, a grow-only device buffer, reused across batches so a
+    training loop pays no multi-GB allocation per train_step.  The rows are cut
+    into chunks of paths; a thread pool converts / concatenates each chunk
+    straight into the pinned buffer (np.copyto releases the GIL; f64 -> f32 for
+    the policy inputs), and each chunk's H2D copy is issued on a copy stream as
+    soon as that chunk is done, so the conversion of later chunks overlaps the
+    PCIe transfer of earlier ones.  The caller's current stream waits on the copy
+    stream.  A pinned slot is rewritten only after its previous copies completed;
+    a reused device slot only after the work already queued on the current
+    stream (which may still read the previous batch) completed."""
+
+    CHUNK_BYTES = 64 << 20
 
     def __init__(self):
-        self._buf = {}
+        self._host = {}
+        self._dev = {}
         self._ev = {}
+        self._pool = None
+        self._copy = {}
 
-    def stage(self, slot, arrs, shape, dtype, device):
-        nbytes = int(np.prod(shape)) * np.dtype(dtype).itemsize
+    def pool(self):
+        if self._pool is None:
+            import concurrent.futures as cf
+            self._pool = cf.ThreadPoolExecutor(_host_threads(), thread_name_prefix="mjrl_stage")
+        return self._pool
+
+    def _copy_stream(self, device):
+        st = self._copy.get(device)
+        if st is None:
+            st = self._copy[device] = torch.cuda.Stream(device=device)
+        return st
+
+    def device_slot(self, slot, numel, dtype, device):
+        """A reused device buffer of `numel` elements (no host data)."""
+        tdt = torch.float64 if dtype == np.float64 else torch.float32
+        nbytes = numel * np.dtype(dtype).itemsize
+        d = self._dev.get(slot)
+        if d is None or d.numel() < max(nbytes, 1) or d.device != torch.device(device):
+            d = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
+            self._dev[slot] = d
+        return d[:nbytes].view(tdt)
+
+    def stage(self, slot, arrs, ncols, dtype, device, reuse=False):
+        """Concatenation of `arrs` (each [rows] or [rows, ncols]) as a device
+        tensor [R] / [R, ncols] of `dtype` (np.float32 / np.float64 / np.int64 /
+        np.uint8)."""
+        dtype = np.dtype(dtype)
+        rows = [int(a.shape[0]) for a in arrs]
+        R = sum(rows)
+        width = max(ncols, 1)
+        nbytes = R * width * dtype.itemsize
         ev = self._ev.get(slot)
         if ev is not None:
             ev.synchronize()
-        h = self._buf.get(slot)
+        h = self._host.get(slot)
         if h is None or h.numel() < nbytes:
             h = torch.empty(max(nbytes, 1), dtype=torch.uint8, pin_memory=True)
-            self._buf[slot] = h
+            self._host[slot] = h
+        tdt = {np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64,
+               np.dtype(np.int64): torch.int64, np.dtype(np.uint8): torch.uint8}[dtype]
+        shape = (R, ncols) if ncols else (R,)
+        if reuse:
+            d = self._dev.get(slot)
+            if d is None or d.numel() < max(nbytes, 1) or d.device != torch.device(device):
+                d = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
+                self._dev[slot] = d
+            out = d[:nbytes].view(tdt).view(shape)
+        else:
+            out = torch.empty(shape, dtype=tdt, device=device)
         view = h[:nbytes].numpy().view(dtype).reshape(shape)
-        if len(arrs):
-            np.concatenate(arrs, axis=0, out=view)
-        out = torch.empty(shape, dtype=torch.float64 if dtype == np.float64 else torch.int64, device=device)
-        if nbytes:
-            out.view(-1).view(torch.uint8).copy_(h[:nbytes], non_blocking=True)
+        if R == 0:
+            return out
+        cur = torch.cuda.current_stream(device)
+        cs = self._copy_stream(device)
+        cs.wait_stream(cur)   # a reused device slot may still be read by queued work
+        # chunks of whole arrays of about CHUNK_BYTES each
+        bounds, acc, r0 = [0], 0, 0
+        for i, r in enumerate(rows):
+            acc += r * width * dtype.itemsize
+            if acc >= self.CHUNK_BYTES:
+                bounds.append(i + 1)
+                acc = 0
+        if bounds[-1] != len(rows):
+            bounds.append(len(rows))
+        offs = np.concatenate([[0], np.cumsum(rows)])
+
+        def fill(a0, a1):
+            for i in range(a0, a1):
+                np.copyto(view[offs[i]:offs[i + 1]], np.asarray(arrs[i]).reshape(view[offs[i]:offs[i + 1]].shape),
+                          casting="unsafe")
+
+        ex = self.pool()
+        futs = [ex.submit(fill, bounds[k], bounds[k + 1]) for k in range(len(bounds) - 1)]
+        hflat = h[:nbytes]
+        oflat = out.view(-1).view(torch.uint8)
+        row_bytes = width * dtype.itemsize
+        with torch.cuda.stream(cs):
+            for k, f in enumerate(futs):
+                f.result()
+                b0, b1 = offs[bounds[k]] * row_bytes, offs[bounds[k + 1]] * row_bytes
+                if b1 > b0:
+                    oflat[b0:b1].copy_(hflat[b0:b1], non_blocking=True)
         ev = torch.cuda.Event()
-        ev.record()
+        ev.record(cs)
         self._ev[slot] = ev
+        cur.wait_stream(cs)
         return out
 
 
@@ -111,18 +208,26 @@ class DeviceBatch:
         self.lengths = None   # host copy, set by from_paths
 
     @classmethod
-    def from_paths(cls, paths, device, baseline=None, use_advantages=False, demo_paths=None):
+    def from_paths(cls, paths, device, baseline=None, use_advantages=False, demo_paths=None, obs_dtype=np.float32,
+                   reuse=False):
         """Stages sampler-format paths (mjrl/samplers/base_sampler.py:76-83) into HBM.
 
-        The concatenation goes straight into pinned host buffers and one H2D
-        copy per array (np.concatenate of npg_cg.py:87-89 without the extra
-        temporary).  Baseline predictions come from the caller's baseline object,
-        per path, as compute_advantages does (process_samples.py:23)."""
+        The concatenation (npg_cg.py:87-89) goes straight into pinned host
+        buffers, chunk by chunk on a thread pool, each chunk's H2D copy overlapping
+        the conversion of the next (_PinnedStaging).  obs_dtype: the staged
+        observations / actions — np.float32 (default: the policy's own input
+        precision, gaussian_mlp.py:103, half the PCIe bytes) or np.float64 (the
+        sampler's values unchanged, as the value baseline sees them on the host).
+        A device LinearBaseline predict / fit reads the staged observations.
+        reuse: stage into the engine-wide grow-only device buffers (one batch
+        alive at a time; stable addresses, so hipGraph replay applies).
+        Baseline predictions of other baselines come from the caller's baseline
+        object, per path, as compute_advantages does (process_samples.py:23)."""
         with torch.cuda.device(device):
-            return cls._from_paths(paths, device, baseline, use_advantages, demo_paths)
+            return cls._from_paths(paths, device, baseline, use_advantages, demo_paths, np.dtype(obs_dtype), reuse)
 
     @classmethod
-    def _from_paths(cls, paths, device, baseline, use_advantages, demo_paths):
+    def _from_paths(cls, paths, device, baseline, use_advantages, demo_paths, obs_dtype, reuse):
         lengths = np.array([len(p["rewards"]) for p in paths], dtype=np.int64)
         T = int(lengths.sum())
         n = paths[0]["observations"].shape[1]
@@ -130,32 +235,39 @@ class DeviceBatch:
         dlen = [len(p["observations"]) for p in (demo_paths or [])]
         T_demo = int(sum(dlen))
 
-        def stage(slot, arrs, shape, dtype=np.float64):
-            return _STAGING.stage(slot, arrs, shape, dtype, device)
+        def stage(slot, arrs, ncols, dtype=np.float64):
+            return _STAGING.stage(slot, arrs, ncols, dtype, device, reuse)
 
-        obs = stage("obs", [p["observations"] for p in paths] + [p["observations"] for p in demo_paths or []],
-                    (T + T_demo, n))
-        act = stage("act", [p["actions"] for p in paths] + [p["actions"] for p in demo_paths or []],
-                    (T + T_demo, m))
-        rew = stage("rew", [p["rewards"] for p in paths], (T,))
-        off = torch.from_numpy(np.concatenate([[0], np.cumsum(lengths)]).astype(np.int64)).to(device)
+        obs = stage("obs", [p["observations"] for p in paths] + [p["observations"] for p in demo_paths or []], n,
+                    obs_dtype)
+        act = stage("act", [p["actions"] for p in paths] + [p["actions"] for p in demo_paths or []], m, obs_dtype)
+        rew = stage("rew", [p["rewards"] for p in paths], 0)
+        off = stage("off", [np.concatenate([[0], np.cumsum(lengths)]).astype(np.int64)], 0, np.int64)
+        term = stage("term", [np.array([bool(p.get("terminated", False)) for p in paths], dtype=np.uint8)], 0,
+                     np.uint8)
         if use_advantages:
             base = None
-            adv = stage("adv", [p["advantages"] for p in paths], (T,))
+            adv = stage("adv", [p["advantages"] for p in paths], 0)
         elif _linear_coeffs(baseline, n) is not False:
             # LinearBaseline.predict on the device (a4), reading the staged obs
             coeffs = _linear_coeffs(baseline, n)
-            base = torch.zeros(T, dtype=torch.float64, device=device)
+            base = _STAGING.device_slot("base", T, np.float64, device) if reuse else \
+                torch.empty(T, dtype=torch.float64, device=device)
+            base.zero_()
             if coeffs is not None and T > 0:
                 c = torch.from_numpy(np.ascontiguousarray(coeffs, dtype=np.float64)).to(device)
-                _lib.check(_lib.lib().mjrl_linear_baseline(_lib.ptr(obs), T, n, _lib.ptr(off), len(paths), _lib.ptr(c),
-                                                           _lib.ptr(base), _lib.stream_ptr()), "mjrl_linear_baseline")
+                fn = _lib.lib().mjrl_linear_baseline_f32 if obs.dtype == torch.float32 else \
+                    _lib.lib().mjrl_linear_baseline
+                _lib.check(fn(_lib.ptr(obs), T, n, _lib.ptr(off), len(paths), _lib.ptr(c), _lib.ptr(base),
+                              _lib.stream_ptr()), "mjrl_linear_baseline")
             adv = None
         else:
-            base = stage("base", [baseline.predict(p) if baseline is not None else np.zeros(len(p["rewards"]))
-                                  for p in paths], (T,))
+            preds = list(_STAGING.pool().map(
+                lambda p: baseline.predict(p) if baseline is not None else np.zeros(len(p["rewards"])), paths)) \
+                if baseline is not None and _thread_safe_predict(baseline) else \
+                [baseline.predict(p) if baseline is not None else np.zeros(len(p["rewards"])) for p in paths]
+            base = stage("base", preds, 0)
             adv = None
-        term = torch.tensor([bool(p.get("terminated", False)) for p in paths], dtype=torch.uint8).to(device)
         b = cls(obs, act, rew, base, off, term, advantages=adv, T_demo=T_demo)
         b.lengths = lengths
         return b
@@ -309,13 +421,17 @@ class UpdateEngine:
         w = self.ws
         ins, isc, _, _ = self.transforms
         sp = C.byref(self.shape)
+        f32 = obs.dtype == torch.float32
+        if f32 != (act.dtype == torch.float32):
+            raise ValueError("observations and actions must be staged in the same dtype")
         if self.split:
-            _lib.check(self.lib.mjrl_pack_batch_split(_lib.ptr(obs), _lib.ptr(act), T, sp, _lib.ptr(ins),
-                                                      _lib.ptr(isc), _lib.ptr(w["xs"]), _lib.ptr(w["xu"]),
-                                                      _lib.ptr(w["act32"]), st), "mjrl_pack_batch_split")
+            fn = self.lib.mjrl_pack_batch_split_f32 if f32 else self.lib.mjrl_pack_batch_split
+            _lib.check(fn(_lib.ptr(obs), _lib.ptr(act), T, sp, _lib.ptr(ins), _lib.ptr(isc), _lib.ptr(w["xs"]),
+                          _lib.ptr(w["xu"]), _lib.ptr(w["act32"]), st), "mjrl_pack_batch_split")
         else:
-            _lib.check(self.lib.mjrl_pack_batch(_lib.ptr(obs), _lib.ptr(act), T, sp, _lib.ptr(ins), _lib.ptr(isc),
-                                                _lib.ptr(w["xhat"]), _lib.ptr(w["act32"]), st), "mjrl_pack_batch")
+            fn = self.lib.mjrl_pack_batch_f32 if f32 else self.lib.mjrl_pack_batch
+            _lib.check(fn(_lib.ptr(obs), _lib.ptr(act), T, sp, _lib.ptr(ins), _lib.ptr(isc), _lib.ptr(w["xhat"]),
+                          _lib.ptr(w["act32"]), st), "mjrl_pack_batch")
 
     # ------------------------------------------------------------------
     def _side_stream(self):
@@ -378,8 +494,8 @@ class UpdateEngine:
         (npg_cg.py:58-62); rank 0 draws, the draw is broadcast, and after the update
         the RNG is left where the reference's early-exiting CG would leave it.
         graph (default self.graphs): replay a captured hipGraph of the update when
-        the batch, shape and arguments repeat (npg / vpg, one process, no
-        subsampled Fisher; see _maybe_capture).
+        the batch, shape and arguments repeat (npg / vpg / dapg, one process, no
+        subsampled Fisher, no line search; see _maybe_capture).
         Returns host scalars plus the new device theta (self.vec['theta_new'])."""
         L = self.lib
         s = self.shape
@@ -404,10 +520,10 @@ class UpdateEngine:
         sp = C.byref(s)
         ins, isc, osh, osc = self.transforms
         use_graph = ((self.graphs if graph is None else graph) and self.comm.world_size == 1 and sub is None
-                     and algo in ("npg", "vpg"))
+                     and algo in ("npg", "vpg", "dapg"))
         if use_graph:
             key = self._graph_key(batch, T_global, (algo, gamma, gae_lambda, n_step_size, const_lr, kl_dist, cg_iters,
-                                                    damping, residual_tol, learn_rate, skip_gae))
+                                                    damping, residual_tol, learn_rate, skip_gae, demo_coef))
             gs = self._gstate
             if gs.get("graph") is not None and gs["key"] == key:
                 # replay: the whole update is one graph launch; theta enters through
@@ -723,16 +839,18 @@ class UpdateEngine:
         f64 = dict(dtype=torch.float64, device=self.device)
         scratch = torch.empty(max(nd.value, 1), **f64)
         gram = torch.zeros((k + 1, k + 1), **f64)
-        _lib.check(L.mjrl_linear_baseline_gram(_lib.ptr(batch.obs), _lib.ptr(y), T, n, _lib.ptr(batch.path_off), P,
-                                               _lib.ptr(scratch), _lib.ptr(gram), st), "mjrl_linear_baseline_gram")
+        f32 = batch.obs.dtype == torch.float32
+        gram_fn = L.mjrl_linear_baseline_gram_f32 if f32 else L.mjrl_linear_baseline_gram
+        res_fn = L.mjrl_linear_baseline_residual_f32 if f32 else L.mjrl_linear_baseline_residual
+        _lib.check(gram_fn(_lib.ptr(batch.obs), _lib.ptr(y), T, n, _lib.ptr(batch.path_off), P,
+                           _lib.ptr(scratch), _lib.ptr(gram), st), "mjrl_linear_baseline_gram")
         self.comm.allreduce_sum(gram)
 
         def sse(coeffs):
             r = torch.empty(max(T, 1), **f64)
             c = torch.from_numpy(np.ascontiguousarray(coeffs, dtype=np.float64)).to(self.device)
-            _lib.check(L.mjrl_linear_baseline_residual(_lib.ptr(batch.obs), _lib.ptr(y), T, n,
-                                                       _lib.ptr(batch.path_off), P, _lib.ptr(c), _lib.ptr(scratch),
-                                                       _lib.ptr(r), st), "mjrl_linear_baseline_residual")
+            _lib.check(res_fn(_lib.ptr(batch.obs), _lib.ptr(y), T, n, _lib.ptr(batch.path_off), P, _lib.ptr(c),
+                              _lib.ptr(scratch), _lib.ptr(r), st), "mjrl_linear_baseline_residual")
             out = torch.zeros(8, **f64)
             part = torch.empty(4 * 256, **f64)
             _lib.check(L.mjrl_moments(_lib.ptr(r), T, None, _lib.ptr(part), _lib.ptr(out), st), "mjrl_moments")

@@ -85,7 +85,8 @@ def test_train_step_one_gpu_matches_oracle(linear):
         # the device LinearBaseline fit (all-reduced Gram + the reference's lstsq loop)
         host = LinearBaseline(EnvSpec(N_OBS, N_ACT, 100, 1))
         host.fit([dict(p) for p in paths])
-        np.testing.assert_allclose(r["coeffs"], host._coeffs, rtol=1e-6, atol=1e-9)
+        # the device fit reads the f32-staged observations (BatchREINFORCE.staging_dtype)
+        np.testing.assert_allclose(r["coeffs"], host._coeffs, rtol=1e-5, atol=1e-8)
     for k in ("time_sampling", "time_VF", "VF_error_before", "VF_error_after", "alpha", "kl_dist",
               "stoc_pol_mean", "running_score"):
         assert len(res[-1]["log"][k]) == 2, k

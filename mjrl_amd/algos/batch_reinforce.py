@@ -29,6 +29,17 @@ from ..utils.logger import DataLog
 logging.disable(logging.CRITICAL)   # as the reference's algos do at import
 
 
+def _check_policy(policy):
+    """Rejects, at agent construction, a policy shape no device kernel covers
+    (engine.kernel_hidden: two hidden layers of width <= 256, act_dim <= 64);
+    other hidden sizes run zero-padded to the next supported width."""
+    from ..engine import kernel_hidden
+    try:
+        kernel_hidden(int(policy.n), int(policy.m), policy.hidden)
+    except ValueError as e:
+        raise ValueError("policy shape not supported by the mjrl_amd update engine: %s" % e) from None
+
+
 def _samplers():
     """The reference's host-CPU samplers (MuJoCo stays on the CPU)."""
     try:
@@ -52,6 +63,7 @@ class BatchREINFORCE:
                  comm=None):
         self.env = env
         self.policy = policy
+        _check_policy(policy)
         self.baseline = baseline
         self.alpha = learn_rate
         self.seed = seed

@@ -3,6 +3,7 @@ with all_adv = 1e-2 [w / (std(w) + 1e-8); lam_0 lam_1^k], scaled by T_all / T_rl
 the Fisher metric on the RL rows only, delta = 2 kl_dist, no line search.  The
 demonstration rows are staged behind the RL rows of the same device batch."""
 from .npg_cg import NPG
+from .batch_reinforce import _check_policy
 from ..utils.logger import DataLog
 
 
@@ -14,6 +15,7 @@ class DAPG(NPG):
                  kl_dist=None, lam_0=1.0, lam_1=0.95, device=None, comm=None):
         self.env = env
         self.policy = policy
+        _check_policy(policy)
         self.baseline = baseline
         self.kl_dist = kl_dist if kl_dist is not None else 0.5 * normalized_step_size
         self.seed = seed

@@ -4,7 +4,7 @@ normalised step and the post-step surrogate / KL, one host readback."""
 import numpy as np
 import torch
 
-from .batch_reinforce import BatchREINFORCE
+from .batch_reinforce import BatchREINFORCE, _check_policy
 from ..utils.logger import DataLog
 
 
@@ -16,6 +16,7 @@ class NPG(BatchREINFORCE):
                  save_logs=False, kl_dist=None, device=None, comm=None):
         self.env = env
         self.policy = policy
+        _check_policy(policy)
         self.baseline = baseline
         self.alpha = const_learn_rate
         self.n_step_size = normalized_step_size if kl_dist is None else 2.0 * kl_dist

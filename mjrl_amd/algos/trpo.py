@@ -3,6 +3,7 @@
 KL < kl_dist, alpha = 0 after 100 trials).  Each trial is one device forward
 over the batch and one 2-double readback."""
 from .npg_cg import NPG
+from .batch_reinforce import _check_policy
 from ..utils.logger import DataLog
 
 
@@ -14,6 +15,7 @@ class TRPO(NPG):
                  comm=None):
         self.env = env
         self.policy = policy
+        _check_policy(policy)
         self.baseline = baseline
         self.kl_dist = kl_dist if kl_dist is not None else 0.5 * normalized_step_size
         self.seed = seed

@@ -1,0 +1,320 @@
+"""MLP value baseline with the API of mjrl/baselines/mlp_baseline.py:15-115, fitted
+and evaluated on the GPU.
+
+Same model as the reference: Linear(n+4, 128) - ReLU - Linear(128, 128) - ReLU -
+Linear(128, 1) on [clip(obs, +-10) / 10, (t/1000)^1..4] features (f32), created in
+the reference's module order (so a torch.manual_seed gives the same initial
+weights), trained by minibatch Adam (lr, weight_decay = reg_coef) on MSE for
+`epochs` passes, minibatches drawn from numpy's global RNG exactly as
+mlp_baseline.py:83-96 does (one np.random.permutation per epoch,
+int(N / batch_size) - 1 minibatches).
+
+Unlike the reference module, importing this one changes no environment variable
+(mlp_baseline.py:1-5 sets CUDA_VISIBLE_DEVICES = '0', which would hide GPUs 1-7
+of a multi-GPU run).
+
+Device work: the features are built on the GPU, every minibatch step (gather,
+forward, MSE, backward, Adam) is one replay of a captured hipGraph that reads
+the minibatch rows through a device index buffer (hipBLAS GEMMs inside), and
+predict is one forward.  The CPU model stays the source of truth for pickling and
+CPU sampling: its parameters and Adam state are copied to the device before a
+fit and back after it.  Sharded (fit_sharded, one process per GPU): rank 0's
+permutation is broadcast, every rank computes the minibatch gradient over its
+own rows of each minibatch, the gradients are all-reduced (a sum: the MSE is a
+mean over the global minibatch), and every rank takes the same Adam step.
+"""
+import numpy as np
+import torch
+import torch.nn as nn
+
+
+def _features_np(paths, n):
+    """mlp_baseline.py:37-56 on the host (f64, as the reference builds it)."""
+    o = np.concatenate([p["observations"] for p in paths])
+    o = np.clip(o, -10, 10) / 10.0
+    if o.ndim > 2:
+        o = o.reshape(o.shape[0], -1)
+    N = o.shape[0]
+    feat = np.ones((N, n + 4))
+    feat[:, :n] = o
+    k = 0
+    for p in paths:
+        H = len(p["rewards"])
+        al = np.arange(H) / 1000.0
+        for j in range(4):
+            feat[k:k + H, -4 + j] = al ** (j + 1)
+        k += H
+    return feat
+
+
+class MLPBaseline:
+    def __init__(self, env_spec, obs_dim=None, learn_rate=1e-3, reg_coef=0.0, batch_size=64, epochs=1,
+                 use_gpu=False, device=None):
+        self.n = obs_dim if obs_dim is not None else env_spec.observation_dim
+        self.batch_size = batch_size
+        self.epochs = epochs
+        self.reg_coef = reg_coef
+        self.use_gpu = use_gpu   # kept for API parity: fit / predict run on the GPU whenever one is visible
+        self.learn_rate = learn_rate
+        self.model = nn.Sequential()
+        self.model.add_module("fc_0", nn.Linear(self.n + 4, 128))
+        self.model.add_module("relu_0", nn.ReLU())
+        self.model.add_module("fc_1", nn.Linear(128, 128))
+        self.model.add_module("relu_1", nn.ReLU())
+        self.model.add_module("fc_2", nn.Linear(128, 1))
+        self.optimizer = torch.optim.Adam(self.model.parameters(), lr=learn_rate, weight_decay=reg_coef)
+        self.loss_function = torch.nn.MSELoss()
+        self._device = device
+        self._dev = None   # device mirror (never pickled)
+
+    def __getstate__(self):
+        d = dict(self.__dict__)
+        d["_dev"] = None
+        return d
+
+    def _features(self, paths):
+        return _features_np(paths, self.n)
+
+    # ---- device mirror -----------------------------------------------------
+    def _device_of(self):
+        if self._device is not None:
+            return torch.device(self._device)
+        return torch.device("cuda", torch.cuda.current_device())
+
+    def _to_device(self):
+        """Device copies of the model and of the Adam state (the CPU objects stay
+        the source of truth between fits)."""
+        dev = self._device_of()
+        st = self._dev
+        if st is None or st["device"] != dev:
+            model = nn.Sequential(
+                nn.Linear(self.n + 4, 128), nn.ReLU(), nn.Linear(128, 128), nn.ReLU(), nn.Linear(128, 1)).to(dev)
+            opt = torch.optim.Adam(model.parameters(), lr=self.learn_rate, weight_decay=self.reg_coef,
+                                   capturable=True)
+            st = self._dev = dict(device=dev, model=model, opt=opt, graph=None)
+        model, opt = st["model"], st["opt"]
+        with torch.no_grad():
+            for pd, pc in zip(model.parameters(), self.model.parameters()):
+                pd.copy_(pc.data)
+        # Adam state: CPU optimizer -> device optimizer (same parameter order)
+        for pd, pc in zip(model.parameters(), self.model.parameters()):
+            sc = self.optimizer.state.get(pc)
+            sd = opt.state[pd]
+            if not sc:
+                if sd:
+                    sd["step"].zero_()
+                    sd["exp_avg"].zero_()
+                    sd["exp_avg_sq"].zero_()
+                continue
+            if not sd:
+                sd["step"] = torch.zeros((), dtype=torch.float32, device=dev)
+                sd["exp_avg"] = torch.zeros_like(pd)
+                sd["exp_avg_sq"] = torch.zeros_like(pd)
+            sd["step"].copy_(torch.as_tensor(float(sc["step"])))
+            sd["exp_avg"].copy_(sc["exp_avg"])
+            sd["exp_avg_sq"].copy_(sc["exp_avg_sq"])
+        return st
+
+    def _from_device(self, st):
+        model, opt = st["model"], st["opt"]
+        with torch.no_grad():
+            for pd, pc in zip(model.parameters(), self.model.parameters()):
+                pc.data.copy_(pd.detach().cpu())
+        for pd, pc in zip(model.parameters(), self.model.parameters()):
+            sd = opt.state.get(pd)
+            if not sd:
+                continue
+            sc = self.optimizer.state[pc]
+            sc["step"] = torch.tensor(float(sd["step"].item()))
+            sc["exp_avg"] = sd["exp_avg"].detach().cpu().clone()
+            sc["exp_avg_sq"] = sd["exp_avg_sq"].detach().cpu().clone()
+
+    def _step_graph(self, st, X, Y):
+        """One minibatch Adam step as a captured hipGraph over static buffers:
+        idx (the minibatch row indices) -> gather -> forward -> MSE -> backward
+        -> Adam.  Captured once per (X, Y) buffers."""
+        key = (X.data_ptr(), Y.data_ptr(), X.shape[0], self.batch_size)
+        if st["graph"] is not None and st["gkey"] == key:
+            return st
+        model, opt = st["model"], st["opt"]
+        dev = st["device"]
+        idx = torch.zeros(self.batch_size, dtype=torch.int64, device=dev)
+        loss_fn = torch.nn.MSELoss()
+
+        def body():
+            opt.zero_grad(set_to_none=False)
+            loss = loss_fn(model(X.index_select(0, idx)), Y.index_select(0, idx))
+            loss.backward()
+            opt.step()
+
+        # the optimizer state must exist before capture; one warm-up step on a side
+        # stream, then restore the parameters / state it changed
+        saved = [p.detach().clone() for p in model.parameters()]
+        saved_state = {p: {k: v.clone() for k, v in opt.state[p].items()} for p in model.parameters()
+                       if opt.state.get(p)}
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            body()
+        torch.cuda.current_stream(dev).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            body()
+        with torch.no_grad():
+            for p, v in zip(model.parameters(), saved):
+                p.copy_(v)
+            for p in model.parameters():
+                if p in saved_state:
+                    for k, v in saved_state[p].items():
+                        opt.state[p][k].copy_(v)
+                else:
+                    for k, v in opt.state[p].items():
+                        v.zero_()
+        st.update(graph=g, gkey=key, idx=idx)
+        return st
+
+    # ---- the reference API ------------------------------------------------------
+    def _device_data(self, paths):
+        dev = self._device_of()
+        X = torch.from_numpy(self._features(paths).astype(np.float32)).to(dev)
+        Y = torch.from_numpy(np.concatenate([p["returns"] for p in paths]).reshape(-1, 1).astype(np.float32)).to(dev)
+        return X, Y
+
+    def _sq_err(self, st, X, Y):
+        with torch.no_grad():
+            e = Y - st["model"](X)
+            return e.pow(2).sum(), Y.pow(2).sum()
+
+    def fit(self, paths, return_errors=False):
+        """mlp_baseline.py:59-105 on the device."""
+        if not torch.cuda.is_available():
+            raise RuntimeError("mjrl_amd MLPBaseline fits on the GPU; no GPU is visible")
+        st = self._to_device()
+        X, Y = self._device_data(paths)
+        return self._fit_device(st, X, Y, return_errors, comm=None)
+
+    def fit_sharded(self, paths, comm, return_errors=False):
+        """fit on the union of every rank's paths (one process per GPU)."""
+        st = self._to_device()
+        X, Y = self._device_data(paths)
+        return self._fit_device(st, X, Y, return_errors, comm=comm)
+
+    def _fit_device(self, st, X, Y, return_errors, comm):
+        N_local = X.shape[0]
+        dev = st["device"]
+        if comm is not None and comm.world_size > 1:
+            counts = torch.zeros(comm.world_size, dtype=torch.float64, device=_comm_dev(comm, dev))
+            counts[comm.rank] = float(N_local)
+            comm.allreduce_sum(counts)
+            counts = counts.cpu().numpy().astype(np.int64)
+            N = int(counts.sum())
+            lo = int(counts[:comm.rank].sum())
+        else:
+            N, lo = N_local, 0
+        if return_errors:
+            e, y2 = self._sq_err(st, X, Y)
+            error_before = self._ratio(e, y2, comm, dev)
+        bs = self.batch_size
+        for _ in range(self.epochs):
+            # numpy's global RNG, as mlp_baseline.py:84 (rank 0 draws when sharded)
+            if comm is not None and comm.world_size > 1:
+                perm = torch.from_numpy(np.random.permutation(N) if comm.rank == 0 else np.zeros(N, np.int64))
+                perm = perm.to(_comm_dev(comm, dev))
+                comm.broadcast(perm)
+                self._epoch_sharded(st, X, Y, perm.to(dev), lo, N_local, comm)
+            else:
+                rand_idx = torch.from_numpy(np.random.permutation(N)).to(dev)
+                self._epoch(st, X, Y, rand_idx)
+        if return_errors:
+            e, y2 = self._sq_err(st, X, Y)
+            error_after = self._ratio(e, y2, comm, dev)
+        self._from_device(st)
+        if return_errors:
+            return error_before, error_after
+
+    @staticmethod
+    def _ratio(e, y2, comm, dev):
+        if comm is not None and comm.world_size > 1:
+            t = torch.stack([e, y2]).double().to(_comm_dev(comm, dev))
+            comm.allreduce_sum(t)
+            e, y2 = t[0], t[1]
+        return float(e.item() / (y2.item() + 1e-8))
+
+    def _epoch(self, st, X, Y, rand_idx):
+        bs = self.batch_size
+        nmb = int(X.shape[0] / bs) - 1
+        if nmb <= 0:
+            return
+        try:
+            st = self._step_graph(st, X, Y)
+        except Exception:   # no graph capture available: eager steps, same math
+            st["graph"] = None
+        model, opt = st["model"], st["opt"]
+        for mb in range(nmb):
+            sel = rand_idx[mb * bs:(mb + 1) * bs]
+            if st.get("graph") is not None:
+                st["idx"].copy_(sel)
+                st["graph"].replay()
+            else:
+                opt.zero_grad()
+                loss = self.loss_function(model(X[sel]), Y[sel])
+                loss.backward()
+                opt.step()
+
+    def _epoch_sharded(self, st, X, Y, perm, lo, N_local, comm):
+        """Data-parallel minibatches: this rank's members of each global minibatch
+        contribute sum((yhat - y)^2) / bs to the gradient; the sum over ranks is
+        the minibatch MSE gradient, then the same Adam step everywhere."""
+        bs = self.batch_size
+        model, opt = st["model"], st["opt"]
+        params = list(model.parameters())
+        nmb = int(perm.numel() / bs) - 1
+        for mb in range(nmb):
+            sel = perm[mb * bs:(mb + 1) * bs]
+            mine = (sel >= lo) & (sel < lo + N_local)
+            rows = (sel[mine] - lo)
+            opt.zero_grad(set_to_none=False)
+            if rows.numel():
+                loss = ((model(X[rows]) - Y[rows]) ** 2).sum() / bs
+                loss.backward()
+            flat = torch.cat([p.grad.reshape(-1) for p in params])
+            comm.allreduce_sum(flat)
+            o = 0
+            for p in params:
+                k = p.numel()
+                p.grad.copy_(flat[o:o + k].view_as(p))
+                o += k
+            opt.step()
+
+    def predict_device(self, obs, path_off, lengths):
+        """predict for every row of a staged batch at once: obs (device, [T][n]
+        RL rows first), path_off (device i64 [P+1]), lengths (host [P]) -> f64
+        device [T].  Features as _features (f64, then f32), one forward."""
+        st = self._dev if self._dev is not None else self._to_device()
+        dev = st["device"]
+        T = int(np.sum(lengths))
+        o = obs[:T].to(torch.float64).clamp(-10.0, 10.0) / 10.0
+        start = torch.repeat_interleave(path_off[:-1], torch.from_numpy(np.asarray(lengths, np.int64)).to(dev))
+        al = (torch.arange(T, device=dev, dtype=torch.int64) - start).to(torch.float64) / 1000.0
+        feat = torch.cat([o, al[:, None], (al ** 2)[:, None], (al ** 3)[:, None], (al ** 4)[:, None]], 1)
+        with torch.no_grad():
+            return st["model"](feat.to(torch.float32)).to(torch.float64).reshape(-1)
+
+    def predict(self, path):
+        """mlp_baseline.py:107-115: one forward of the f32 features (on the GPU
+        when one is visible, else on the CPU model)."""
+        feat = self._features([path]).astype("float32")
+        if torch.cuda.is_available():
+            st = self._dev if self._dev is not None else self._to_device()
+            with torch.no_grad():
+                return st["model"](torch.from_numpy(feat).to(st["device"])).cpu().numpy().ravel()
+        with torch.no_grad():
+            return self.model(torch.from_numpy(feat)).numpy().ravel()
+
+
+def _comm_dev(comm, dev):
+    try:
+        backend = comm.dist.get_backend(comm.group)
+    except Exception:
+        backend = "gloo"
+    return dev if backend == "nccl" else torch.device("cpu")

@@ -261,6 +261,10 @@ class DeviceBatch:
                 _lib.check(fn(_lib.ptr(obs), T, n, _lib.ptr(off), len(paths), _lib.ptr(c), _lib.ptr(base),
                               _lib.stream_ptr()), "mjrl_linear_baseline")
             adv = None
+        elif hasattr(baseline, "predict_device"):
+            # MLPBaseline: one device forward over every staged row
+            base = baseline.predict_device(obs, off, lengths)
+            adv = None
         else:
             preds = list(_STAGING.pool().map(
                 lambda p: baseline.predict(p) if baseline is not None else np.zeros(len(p["rewards"])), paths)) \
@@ -273,6 +277,55 @@ class DeviceBatch:
         return b
 
 
+HIDDEN_WIDTHS = (32, 64, 128, 256)   # hidden widths the row kernels are built for
+
+
+def kernel_hidden(n, m, hidden):
+    """The (h0, h1) the device kernels run a policy of this shape on.
+
+    MuNet(n, m, (h0, h1)) (mjrl/policies/gaussian_mlp.py:143-158) takes any two
+    hidden sizes; the kernels are built for square layers of width 32, 64, 128
+    or 256, so a policy is zero-padded to the smallest such square that holds
+    both layers: padded units have zero weights and biases, so tanh(0) = 0 flows
+    nowhere, their gradients and Fisher rows are exactly zero, and the update of
+    the real parameters is unchanged.  Raises ValueError for shapes no kernel
+    covers (more than two hidden layers, a layer wider than 256, act_dim > 64)."""
+    if m < 1 or m > 64:
+        raise ValueError("mjrl_amd kernels support act_dim 1..64, got %d" % m)
+    if n < 1:
+        raise ValueError("obs_dim must be positive")
+    if hidden is None or tuple(hidden) == (0, 0):
+        return (0, 0)
+    hidden = tuple(int(h) for h in hidden)
+    if len(hidden) != 2 or min(hidden) < 1:
+        raise ValueError("the Gaussian MLP has two hidden layers (gaussian_mlp.py:143-158), got %r" % (hidden,))
+    for w in HIDDEN_WIDTHS:
+        if max(hidden) <= w:
+            return (w, w)
+    raise ValueError("mjrl_amd kernels support hidden sizes up to %d, got %r" % (HIDDEN_WIDTHS[-1], hidden))
+
+
+def padded_positions(n, m, hidden, kh):
+    """Index in the flat parameter vector of the padded (kh) policy of every
+    entry of the real flat vector (trainable_params order, gaussian_mlp.py:61-64)."""
+    h0, h1 = hidden
+    p0, p1 = kh
+    o_b0 = p0 * n
+    o_w1 = o_b0 + p0
+    o_b1 = o_w1 + p1 * p0
+    o_w2 = o_b1 + p1
+    o_b2 = o_w2 + m * p1
+    o_ls = o_b2 + m
+    parts = [(np.arange(h0)[:, None] * n + np.arange(n)[None, :]).ravel(),
+             o_b0 + np.arange(h0),
+             (o_w1 + np.arange(h1)[:, None] * p0 + np.arange(h0)[None, :]).ravel(),
+             o_b1 + np.arange(h1),
+             (o_w2 + np.arange(m)[:, None] * p1 + np.arange(h1)[None, :]).ravel(),
+             o_b2 + np.arange(m),
+             o_ls + np.arange(m)]
+    return np.concatenate(parts).astype(np.int64)
+
+
 class UpdateEngine:
     """Owns the HBM workspace for one policy shape and runs updates on it."""
 
@@ -282,9 +335,15 @@ class UpdateEngine:
         on exact-f32 MFMA; default (None / 'auto', or $MJRL_AMD_PRECISION): split
         wherever the kernels support it (mjrl_split_supported), f32 elsewhere."""
         self.lib = _lib.lib()
-        h0, h1 = (0, 0) if hidden is None else (int(hidden[0]), int(hidden[1]))
-        self.shape = _lib.make_shape(int(n), int(m), h0, h1)
+        real = (0, 0) if hidden is None else (int(hidden[0]), int(hidden[1]))
+        kh = kernel_hidden(int(n), int(m), hidden)
+        self.shape = _lib.make_shape(int(n), int(m), *kh)
         self.device = torch.device(device if device is not None else "cuda")
+        self.hidden = real
+        self.pad_idx = None   # real flat index -> padded flat index (None: the kernels run the real shape)
+        if kh != real:
+            self.pad_idx = torch.from_numpy(padded_positions(int(n), int(m), real, kh)).to(self.device)
+            self._pad_bufs = {}
         self.comm = comm or LocalComm()
         self.min_log_std = float(min_log_std)
         self.cap_T = -1
@@ -295,7 +354,7 @@ class UpdateEngine:
         self.packed_theta = torch.zeros(s.packed, **f32)
         self.packed_new = torch.zeros(s.packed, **f32)
         self.packed_p = torch.zeros(s.packed, **f32)
-        self.vec = {k: torch.zeros(s.d, **f32) for k in ("g", "gsum", "x", "r", "p", "z", "theta_new")}
+        self.pvec = {k: torch.zeros(s.d, **f32) for k in ("g", "gsum", "x", "r", "p", "z", "theta_new")}
         self.cg = torch.zeros(_lib.CG_STATE, **f32)   # MJRL_CG_STATE
         self.done = torch.zeros(1, dtype=torch.int32, device=dev)
         self.out = torch.zeros(_lib.STEP_OUT, **f32)     # MJRL_STEP_OUT (results + step scratch)
@@ -314,6 +373,32 @@ class UpdateEngine:
         if prec == "split" and not can_split:
             raise ValueError("split precision is not available for this policy shape")
         self.split = can_split and prec != "f32"
+
+    # ------------------------------------------------------------------
+    @property
+    def vec(self):
+        """The update's flat vectors (g, x, theta_new, ...) in the policy's own
+        (real) parameter order; copies when the kernels run a padded shape."""
+        if self.pad_idx is None:
+            return self.pvec
+        return {k: t[self.pad_idx] for k, t in self.pvec.items()}
+
+    @property
+    def d(self):
+        return self.shape.d if self.pad_idx is None else int(self.pad_idx.numel())
+
+    def _pad(self, t, slot):
+        """A real flat vector scattered into a persistent zero-padded buffer."""
+        if self.pad_idx is None:
+            return t
+        b = self._pad_bufs.get(slot)
+        if b is None:
+            b = self._pad_bufs[slot] = torch.zeros(self.shape.d, dtype=torch.float32, device=self.device)
+        b.index_copy_(0, self.pad_idx, t.to(torch.float32))
+        return b
+
+    def _unpad(self, t):
+        return t if self.pad_idx is None else t[self.pad_idx]
 
     # ------------------------------------------------------------------
     def set_transformations(self, in_shift=None, in_scale=None, out_shift=None, out_scale=None):
@@ -500,6 +585,7 @@ class UpdateEngine:
         L = self.lib
         s = self.shape
         self.st = st = _lib.stream_ptr()
+        theta = self._pad(theta, "theta")
         T, T_demo, P = batch.T, batch.T_demo, batch.P
         T_all = T + T_demo
         # global row count (all ranks): scales every mean
@@ -516,7 +602,7 @@ class UpdateEngine:
         # workspace keeps its size and the GAE outputs already in it
         self._ensure(T_all, P)
         w = self.ws
-        v = self.vec
+        v = self.pvec
         sp = C.byref(s)
         ins, isc, osh, osc = self.transforms
         use_graph = ((self.graphs if graph is None else graph) and self.comm.world_size == 1 and sub is None
@@ -953,7 +1039,7 @@ class UpdateEngine:
         sp = C.byref(s)
         self.st = st = _lib.stream_ptr()
         T = self.last_T if T is None else T
-        vv = self.vec
+        vv = self.pvec
         T_global = self.last_T_global
         if idx is not None:
             n = int(idx.numel())
@@ -963,6 +1049,7 @@ class UpdateEngine:
         else:
             scratch = self._scratch(T)
             rows = self._rows(T, self.ws["adv32"])
+        v = self._pad(v, "v")
         _lib.check(L.mjrl_cg_init(sp, _lib.ptr(v), _lib.ptr(vv["x"]), _lib.ptr(vv["r"]), _lib.ptr(vv["p"]),
                                   _lib.ptr(self.packed_p), _lib.ptr(self.cg), _lib.ptr(self.done), st), "mjrl_cg_init")
         _lib.check(L.mjrl_policy_fvp(sp, C.byref(rows), T, _lib.ptr(self.packed_theta), _lib.ptr(self.packed_p),
@@ -973,7 +1060,7 @@ class UpdateEngine:
                                   _lib.ptr(self.packed_theta), _lib.ptr(vv["x"]), _lib.ptr(vv["r"]), _lib.ptr(vv["p"]),
                                   _lib.ptr(vv["z"]), _lib.ptr(self.packed_p), _lib.ptr(self.cg), _lib.ptr(self.done),
                                   0.0, st), "mjrl_cg_step")
-        return vv["z"].clone()
+        return self._unpad(vv["z"]).clone()
 
     # ------------------------------------------------------------------
     # standalone passes on explicit arrays (the reference's CPI_surrogate /
@@ -1003,6 +1090,7 @@ class UpdateEngine:
         """Forward + VPG sums at theta over the loaded rows; fills the caches.
         Returns the flat VPG mean (device) = sum / T."""
         L, s = self.lib, self.shape
+        theta = self._pad(theta, "theta")
         sp = C.byref(s)
         self.st = st = _lib.stream_ptr()
         _lib.check(L.mjrl_pack_params(sp, _lib.ptr(theta), _lib.ptr(self.packed_theta), 1, self.min_log_std, st),
@@ -1011,17 +1099,18 @@ class UpdateEngine:
         sc = self._scratch(T)
         _, _, osh, osc = self.transforms
         _lib.check(L.mjrl_policy_vpg(sp, C.byref(rows), _lib.ptr(self.packed_theta), _lib.ptr(osh), _lib.ptr(osc),
-                                     C.byref(sc), _lib.ptr(self.vec["gsum"]), st), "mjrl_policy_vpg")
+                                     C.byref(sc), _lib.ptr(self.pvec["gsum"]), st), "mjrl_policy_vpg")
         tg = float(T)
         self.last_T, self.last_T_global = T, tg
-        _lib.check(L.mjrl_scale_vec(_lib.ptr(self.vec["gsum"]), s.d, 1.0 / tg, _lib.ptr(self.vec["g"]), st),
+        _lib.check(L.mjrl_scale_vec(_lib.ptr(self.pvec["gsum"]), s.d, 1.0 / tg, _lib.ptr(self.pvec["g"]), st),
                    "mjrl_scale_vec")
-        return self.vec["g"]
+        return self._unpad(self.pvec["g"])
 
     @_on_device
     def eval_pass(self, theta_new, T):
         """(surrogate, KL) at theta_new against the caches of the last forward_pass."""
         L, s = self.lib, self.shape
+        theta_new = self._pad(theta_new, "theta_new")
         sp = C.byref(s)
         self.st = st = _lib.stream_ptr()
         _lib.check(L.mjrl_pack_params(sp, _lib.ptr(theta_new), _lib.ptr(self.packed_new), 1, self.min_log_std, st),

@@ -387,6 +387,10 @@ def main():
              terminated=[False] * 20, algo="npg",
              algo_kwargs=dict(normalized_step_size=0.1, hvp_sample_frac=0.5), seed=31, np_seed=2024,
              reverse_alt=False)
+    # C2h: non-square hidden sizes MLP(48, 32) (MuNet takes any pair, gaussian_mlp.py:143-158)
+    run_case("c2_h48x32", n=8, m=2, hidden=(48, 32), lengths=[200] * 10,
+             terminated=[False] * 10, algo="npg", algo_kwargs=dict(normalized_step_size=0.05), seed=43,
+             log_std=np.array([-0.5, 0.2]))
     # C2v: BatchREINFORCE (vanilla policy gradient, batch_reinforce.py:106-164)
     run_case("c2_vpg", n=8, m=2, hidden=(64, 64), lengths=[200] * 10,
              terminated=[False] * 10, algo="vpg", algo_kwargs=dict(learn_rate=0.05), seed=41)
@@ -437,7 +441,47 @@ def baselines_case():
                         quad_pred=np.concatenate([quad.predict(p) for p in paths]), quad_err=np.array(qerr))
 
 
+def mlp_baseline_case():
+    """Reference MLPBaseline (mlp_baseline.py:15-115, CPU) fit + predict: initial
+    weights under torch.manual_seed(7), two fits (the Adam state carries over)
+    with np.random.seed(11) / (12) before each, errors and predictions."""
+    saved = {k: os.environ.get(k) for k in ("CUDA_VISIBLE_DEVICES", "CUDA_DEVICE_ORDER", "MKL_THREADING_LAYER")}
+    from mjrl.baselines.mlp_baseline import MLPBaseline as RefMLP   # sets CUDA_VISIBLE_DEVICES at import
+    for k, v in saved.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
+    rs = np.random.RandomState(53)
+    n = 5
+    lengths = [300, 200, 250]
+    paths = make_paths(rs, n, 2, lengths, [False] * 3)
+    for p in paths:
+        p["observations"] = p["observations"] * 4.0   # exercise the +-10 clip
+    process_samples.compute_returns(paths, 0.99)
+    spec = EnvSpec(n, 2, 300, 1)
+    torch.manual_seed(7)
+    ref = RefMLP(spec, batch_size=64, epochs=2, learn_rate=3e-3)
+    init = {k: v.detach().numpy().copy() for k, v in ref.model.state_dict().items()}
+    out = dict(obs=concat(paths, "observations"), rewards=concat(paths, "rewards"),
+               returns=concat(paths, "returns"), lengths=np.array(lengths))
+    for k, v in init.items():
+        out["init_" + k.replace(".", "_")] = v
+    for it, seed in enumerate((11, 12)):
+        np.random.seed(seed)
+        err = ref.fit(paths, return_errors=True)
+        out["err%d" % it] = np.array(err, dtype=np.float64)
+        out["pred%d" % it] = np.concatenate([ref.predict(p) for p in paths])
+        out["np_seed%d" % it] = np.int64(seed)
+    for k, v in ref.model.state_dict().items():
+        out["final_" + k.replace(".", "_")] = v.detach().numpy().copy()
+    np.savez_compressed(os.path.join(OUT, "mlp_baseline.npz"), **out)
+    print("mlp_baseline errors", out["err0"], out["err1"])
+
+
 if __name__ == "__main__":
     main()
     if not ONLY or "baselines" in ONLY:
         baselines_case()
+    if not ONLY or "mlp_baseline" in ONLY:
+        mlp_baseline_case()

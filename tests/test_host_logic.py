@@ -167,3 +167,51 @@ def test_engine_methods_run_on_their_device():
                  "load_rows", "forward_pass", "eval_pass"):
         fn = getattr(UpdateEngine, name)
         assert getattr(fn, "__wrapped__", None) is not None, name
+
+
+def test_unsupported_policy_shape_rejected_at_construction():
+    """Hidden sizes the kernels cannot run are rejected when the agent is built,
+    not deep inside the first update; others run zero-padded."""
+    import pytest
+    from mjrl_amd.algos.npg_cg import NPG
+    from mjrl_amd.engine import kernel_hidden, padded_positions
+    from mjrl_amd.policies.gaussian_mlp import MLP
+    from mjrl_amd.utils.gym_env import EnvSpec
+    assert kernel_hidden(8, 2, (48, 32)) == (64, 64)
+    assert kernel_hidden(8, 2, (100, 50)) == (128, 128)
+    assert kernel_hidden(8, 2, None) == (0, 0)
+    NPG(None, MLP(EnvSpec(8, 2, 10, 1), hidden_sizes=(100, 50), seed=0), None)   # fine: padded
+    with pytest.raises(ValueError, match="hidden sizes up to 256"):
+        NPG(None, MLP(EnvSpec(8, 2, 10, 1), hidden_sizes=(300, 64), seed=0), None)
+    with pytest.raises(ValueError, match="act_dim"):
+        NPG(None, MLP(EnvSpec(8, 70, 10, 1), hidden_sizes=(64, 64), seed=0), None)
+    idx = padded_positions(8, 2, (48, 32), (64, 64))
+    assert len(idx) == 48 * 8 + 48 + 32 * 48 + 32 + 2 * 32 + 2 + 2 and len(set(idx.tolist())) == len(idx)
+
+
+def test_mlp_baseline_mirror_matches_reference_init_and_leaves_env_alone():
+    """MLPBaseline (mlp_baseline.py:15-35): same modules in the same order, so
+    torch.manual_seed gives the reference's initial weights bit for bit; importing
+    it changes no environment variable (the reference sets CUDA_VISIBLE_DEVICES)."""
+    import importlib
+    import os
+    import sys
+    before = dict(os.environ)
+    sys.modules.pop("mjrl_amd.baselines.mlp_baseline", None)
+    mod = importlib.import_module("mjrl_amd.baselines.mlp_baseline")
+    assert dict(os.environ) == before
+    from mjrl_amd.utils.gym_env import EnvSpec
+    z = np.load(os.path.join(GOLDEN, "mlp_baseline.npz"))
+    torch.manual_seed(7)
+    b = mod.MLPBaseline(EnvSpec(5, 2, 300, 1), batch_size=64, epochs=2, learn_rate=3e-3)
+    for k, v in b.model.state_dict().items():
+        assert np.array_equal(v.numpy(), z["init_" + k.replace(".", "_")]), k
+    offs = np.concatenate([[0], np.cumsum(z["lengths"])])
+    paths = [dict(observations=z["obs"][offs[i]:offs[i + 1]], rewards=z["rewards"][offs[i]:offs[i + 1]])
+             for i in range(len(z["lengths"]))]
+    f = b._features(paths)
+    t = np.concatenate([np.arange(L) / 1000.0 for L in z["lengths"]])
+    np.testing.assert_array_equal(f[:, :5], np.clip(z["obs"], -10, 10) / 10.0)
+    np.testing.assert_array_equal(f[:, 5:], np.stack([t, t ** 2, t ** 3, t ** 4], 1))
+    clone = pickle.loads(pickle.dumps(b))
+    assert all(torch.equal(a, c) for a, c in zip(clone.model.parameters(), b.model.parameters()))

@@ -479,9 +479,71 @@ def mlp_baseline_case():
     print("mlp_baseline errors", out["err0"], out["err1"])
 
 
+def bc_case():
+    """Reference BC (behavior_cloning.py:11-68): MLE of expert actions by minibatch
+    Adam, minibatches from np.random.choice after np.random.seed(17); the
+    transformations it sets, the per-epoch full-data losses, the final params."""
+    from mjrl.algos.behavior_cloning import BC as RefBC
+    rs = np.random.RandomState(61)
+    n, m = 6, 3
+    lengths = [100, 80, 120]
+    paths = make_paths(rs, n, m, lengths, [False] * 3)
+    for p in paths:
+        p["observations"] = p["observations"] * 3.0 + 1.0
+        p["actions"] = np.tanh(p["observations"][:, :m]) + 0.1 * p["actions"]
+    spec = EnvSpec(n, m, 120, 1)
+    policy = MLP(spec, hidden_sizes=(32, 32), seed=5)
+    init = policy.get_param_values()
+    bc = RefBC(paths, policy, epochs=2, batch_size=32, lr=1e-3)
+    np.random.seed(17)
+    bc.train()
+    t = policy.model.transformations
+    np.savez_compressed(os.path.join(OUT, "bc.npz"), obs=concat(paths, "observations"),
+                        act=concat(paths, "actions"), lengths=np.array(lengths), init=init,
+                        final=policy.get_param_values(), loss=np.array(bc.logger.log["loss"], dtype=np.float64),
+                        in_shift=t["in_shift"], in_scale=t["in_scale"], out_shift=t["out_shift"],
+                        out_scale=t["out_scale"], np_seed=np.int64(17))
+    print("bc losses", bc.logger.log["loss"])
+
+
+def ppo_case():
+    """Reference PPO (ppo_clip.py:23-120) train_from_paths, two iterations (the
+    Adam state carries over) after np.random.seed(23) / (24): base_stats, the
+    logged kl / surrogate improvement and the params after each."""
+    from mjrl.algos.ppo_clip import PPO as RefPPO
+    rs = np.random.RandomState(71)
+    n, m = 6, 2
+    lengths = [150, 90, 200, 160]
+    spec = EnvSpec(n, m, 200, 1)
+    policy = MLP(spec, hidden_sizes=(32, 32), seed=3, init_log_std=-0.5)
+    ppo = RefPPO(None, policy, None, clip_coef=0.2, epochs=2, mb_size=64, learn_rate=3e-3, save_logs=True)
+    out = dict(init=policy.get_param_values(), lengths=np.array(lengths))
+    for it, seed in enumerate((23, 24)):
+        paths = make_paths(rs, n, m, lengths, [False] * 4)
+        for p in paths:
+            p["advantages"] = rs.randn(len(p["rewards"])) * 2.0 + 0.3
+        np.random.seed(seed)
+        stats = ppo.train_from_paths(paths)
+        out["obs%d" % it] = concat(paths, "observations")
+        out["act%d" % it] = concat(paths, "actions")
+        out["rew%d" % it] = concat(paths, "rewards")
+        out["adv%d" % it] = concat(paths, "advantages")
+        out["np_seed%d" % it] = np.int64(seed)
+        out["base_stats%d" % it] = np.array(stats, dtype=np.float64)
+        out["params%d" % it] = policy.get_param_values()
+        for k in ("kl_dist", "surr_improvement", "running_score"):
+            out["%s%d" % (k, it)] = np.float64(ppo.logger.log[k][-1])
+    np.savez_compressed(os.path.join(OUT, "ppo.npz"), **out)
+    print("ppo kl", out["kl_dist0"], out["kl_dist1"], "surr", out["surr_improvement0"], out["surr_improvement1"])
+
+
 if __name__ == "__main__":
     main()
     if not ONLY or "baselines" in ONLY:
         baselines_case()
     if not ONLY or "mlp_baseline" in ONLY:
         mlp_baseline_case()
+    if not ONLY or "bc" in ONLY:
+        bc_case()
+    if not ONLY or "ppo" in ONLY:
+        ppo_case()

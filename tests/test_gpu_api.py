@@ -493,3 +493,46 @@ def test_mlp_baseline_device_batch_predict():
     batch = DeviceBatch.from_paths(paths, torch.device("cuda:0"), baseline=b, obs_dtype=np.float64)
     ref = np.concatenate([b.predict(p) for p in paths])
     np.testing.assert_allclose(batch.baseline.cpu().numpy(), ref, rtol=1e-6, atol=1e-7)
+
+
+def test_bc_on_gpu_matches_reference():
+    """BC (behavior_cloning.py:11-68) with its minibatch steps replayed as a
+    captured graph on the GPU, against the reference's CPU run: Adam's
+    normalised steps carry the GEMM summation-order differences into the
+    weights, so the final parameters agree in norm to 1e-3, the logged losses
+    to 1e-4."""
+    from test_bc_ppo import run_bc
+    bc, policy, z = run_bc("cuda:0")
+    assert bc.trainer().graphable
+    np.testing.assert_allclose(np.array(bc.logger.log["loss"], dtype=np.float64), z["loss"], rtol=1e-4)
+    ref = z["final"]
+    assert np.linalg.norm(policy.get_param_values() - ref) <= 1e-3 * np.linalg.norm(ref)
+
+
+def test_ppo_on_gpu_matches_reference():
+    """PPO.train_from_paths (ppo_clip.py:57-120) twice (the Adam state carries
+    over), against the reference run: base_stats exact; parameters in norm to
+    1e-3; surrogate improvement and KL (HIP evaluation passes) to the same
+    relative level of the step they measure."""
+    from mjrl_amd.algos.ppo_clip import PPO
+    from mjrl_amd.policies.gaussian_mlp import MLP
+    from mjrl_amd.utils.gym_env import EnvSpec
+    z = np.load(os.path.join(GOLDEN, "ppo.npz"))
+    policy = MLP(EnvSpec(6, 2, 200, 1), hidden_sizes=(32, 32), seed=3, init_log_std=-0.5)
+    np.testing.assert_array_equal(policy.get_param_values(), z["init"])
+    ppo = PPO(None, policy, None, clip_coef=0.2, epochs=2, mb_size=64, learn_rate=3e-3, save_logs=True)
+    offs = np.concatenate([[0], np.cumsum(z["lengths"])])
+    for it in range(2):
+        sl = lambda k: [z["%s%d" % (k, it)][offs[i]:offs[i + 1]] for i in range(len(z["lengths"]))]
+        paths = [dict(observations=o, actions=a, rewards=r, advantages=v)
+                 for o, a, r, v in zip(sl("obs"), sl("act"), sl("rew"), sl("adv"))]
+        np.random.seed(int(z["np_seed%d" % it]))
+        stats = ppo.train_from_paths(paths)
+        np.testing.assert_allclose(stats, z["base_stats%d" % it], rtol=1e-12)
+        ref = z["params%d" % it]
+        assert np.linalg.norm(policy.get_param_values() - ref) <= 1e-3 * np.linalg.norm(ref), it
+        step = np.linalg.norm(ref - (z["init"] if it == 0 else z["params0"]))
+        assert abs(ppo.logger.log["kl_dist"][-1] - z["kl_dist%d" % it]) <= 0.05 * abs(z["kl_dist%d" % it]) + 1e-6
+        assert abs(ppo.logger.log["surr_improvement"][-1] - z["surr_improvement%d" % it]) <= \
+            0.05 * abs(z["surr_improvement%d" % it]) + 1e-5, (it, step)
+        np.testing.assert_allclose(ppo.logger.log["running_score"][-1], z["running_score%d" % it], rtol=1e-12)

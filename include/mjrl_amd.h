@@ -302,6 +302,17 @@ int mjrl_npg_step(const mjrl_shape* s, const float* g, const float* x, const flo
                   float min_log_std, float* theta_new, float* packed_new, float* out,
                   void* stream);
 
+/* ---- batched policy forward for vectorised sampling ----
+ * Replaces the per-observation MuNet forward inside policy.get_action
+ * (mjrl/policies/gaussian_mlp.py:92-98, gaussian_linear.py:90-96) for the N
+ * lock-stepped environments of one sampling step (mjrl/samplers/base_sampler.py:64-74):
+ * mean[N][m] (f32) = out_scale * MuNet((obs - in_shift) / (in_scale + 1e-8)) + out_shift
+ * from obs f32 [N][n] and the packed parameters of mjrl_pack_params.  The Gaussian
+ * noise stays on the host (each trajectory's own numpy stream). */
+int mjrl_policy_mean(const mjrl_shape* s, const float* obs, int64_t N, const float* packed_theta,
+                     const float* in_shift, const float* in_scale, const float* out_shift,
+                     const float* out_scale, float* mean, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -85,6 +85,7 @@ SIGNATURES = {
     "mjrl_linear_baseline_gram_f32": [P, P, I64, I32, P, I64, P, P, P],
     "mjrl_linear_baseline_residual_f32": [P, P, I64, I32, P, I64, P, P, P, P],
     "mjrl_npg_step": [SP, P, P, P, I32, F32, F32, I32, F32, P, P, P, P],
+    "mjrl_policy_mean": [SP, P, I64, P, P, P, P, P, P, P],
 }
 
 _LIB = None

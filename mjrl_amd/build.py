@@ -22,7 +22,7 @@ FLAGS = [
     "-ffp-contract=off",          # keep the reference's multiply-then-add order
     "-Wall", "-Wno-unused-function", "-Wno-unused-variable",
 ]
-SOURCES = ["batch.hip", "policy.hip", "cg.hip", "baseline.hip"]
+SOURCES = ["batch.hip", "policy.hip", "cg.hip", "baseline.hip", "rollout.hip"]
 
 
 def _deps():

@@ -148,7 +148,7 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
-constexpr int GAE_WAVES = 4;       // waves (paths in flight) per workgroup
+constexpr int GAE_WAVES = 2;       // waves (paths in flight) per workgroup (3 x 8 KB windows each)
 constexpr int GU = 8;              // serial steps per batch of LDS reads
 
 __global__ void __launch_bounds__(64 * GAE_WAVES) k_gae(const double* __restrict__ rew,
@@ -159,11 +159,85 @@ __global__ void __launch_bounds__(64 * GAE_WAVES) k_gae(const double* __restrict
                                                         double* __restrict__ adv, double* __restrict__ path_ret) {
     __shared__ double sr[GAE_WAVES][GW];
     __shared__ double sb[GAE_WAVES][GW];
+    __shared__ double stt[GAE_WAVES][GW];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     double* R = sr[w];
     double* B = sb[w];
+    double* TD = stt[w];
     for (int64_t p = (int64_t)blockIdx.x * GAE_WAVES + w; p < P; p += (int64_t)gridDim.x * GAE_WAVES) {
         const int64_t b = off[p], e = off[p + 1];
+        if (e - b <= GW) {
+            // One window: the three serial chains — the path-return sum (forward),
+            // the returns and the advantages (backward) — run side by side on lanes 0,
+            // 1 and 2 of ONE instruction stream, acc = x + c * acc with (x, c) =
+            // (reward, 1), (reward, gamma), (td, gamma * lambda): c = 1 makes the
+            // product exact, so lane 0 is Python's front-to-back sum bit for bit, and
+            // lanes 1 / 2 are discount_sum's recurrences (process_samples.py:37-44).
+            // The td terms are formed by the whole wave first.
+            const int cnt = (int)(e - b);
+            {
+                double x[GW / 64], y[GW / 64];
+#pragma unroll
+                for (int k = 0; k < GW / 64; ++k) {
+                    const bool in = lane + 64 * k < cnt;
+                    x[k] = in ? rew[b + lane + 64 * k] : 0.0;
+                    y[k] = in ? base[b + lane + 64 * k] : 0.0;
+                }
+#pragma unroll
+                for (int k = 0; k < GW / 64; ++k)
+                    if (lane + 64 * k < cnt) {
+                        R[lane + 64 * k] = x[k];
+                        B[lane + 64 * k] = y[k];
+                    }
+            }
+            wave_sync();
+            // GAE td = r + gamma * b1[t+1] - b[t] with b1 = append(b, 0 if terminated
+            // else b[-1]) (process_samples.py:23-27); plain advantages keep b here
+            const double blast = cnt > 0 ? (term[p] ? 0.0 : B[cnt - 1]) : 0.0;
+            for (int i = lane; i < cnt; i += 64) {
+                const double bb = B[i];
+                if (use_gae) {
+                    const double bn = i + 1 < cnt ? B[i + 1] : blast;
+                    TD[i] = __dsub_rn(__dadd_rn(R[i], __dmul_rn(gamma, bn)), bb);
+                } else {
+                    TD[i] = bb;
+                }
+            }
+            wave_sync();
+            if (lane < 3) {
+                const bool fwd = lane == 0;
+                const double c = lane == 0 ? 1.0 : (lane == 1 ? gamma : gl);
+                const double* src = lane == 2 ? TD : R;
+                double* dst = lane == 1 ? B : TD;             // returns over B (free now), advantages in place
+                const bool put = lane == 1 || (lane == 2 && use_gae);
+                double acc = 0.0;
+                int j = 0;
+                for (; j + GU <= cnt; j += GU) {
+                    double xv[GU];
+#pragma unroll
+                    for (int u = 0; u < GU; ++u) xv[u] = src[fwd ? j + u : cnt - 1 - j - u];
+#pragma unroll
+                    for (int u = 0; u < GU; ++u) {
+                        acc = __dadd_rn(xv[u], __dmul_rn(c, acc));
+                        if (put) dst[cnt - 1 - j - u] = acc;
+                    }
+                }
+                for (; j < cnt; ++j) {
+                    const int idx = fwd ? j : cnt - 1 - j;
+                    acc = __dadd_rn(src[idx], __dmul_rn(c, acc));
+                    if (put) dst[idx] = acc;
+                }
+                if (lane == 0) path_ret[p] = acc;
+            }
+            wave_sync();
+            for (int i = lane; i < cnt; i += 64) {
+                const double rr = B[i];
+                ret[b + i] = rr;
+                adv[b + i] = use_gae ? TD[i] : __dsub_rn(rr, TD[i]);   // plain: ret - baseline
+            }
+            wave_sync();
+            continue;
+        }
         // sum(p["rewards"]) — Python's builtin sum, front to back (npg_cg.py:97)
         double s = 0.0;
         for (int64_t w0 = b; w0 < e; w0 += GW) {

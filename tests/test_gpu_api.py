@@ -536,3 +536,50 @@ def test_ppo_on_gpu_matches_reference():
         assert abs(ppo.logger.log["surr_improvement"][-1] - z["surr_improvement%d" % it]) <= \
             0.05 * abs(z["surr_improvement%d" % it]) + 1e-5, (it, step)
         np.testing.assert_allclose(ppo.logger.log["running_score"][-1], z["running_score%d" % it], rtol=1e-12)
+
+
+def test_vectorized_sampler_matches_serial_rollout():
+    """sample_paths_vectorized (f3: one mjrl_policy_mean launch per lock-stepped
+    step) against base_sampler.do_rollout's serial loop with policy.get_action on
+    the CPU (tests/stub_env.py): same trajectory lengths and termination flags,
+    observations / actions / rewards to f32 rounding of the mean, and numpy's
+    global RNG left where the serial loop leaves it."""
+    from mjrl_amd.policies.gaussian_mlp import MLP
+    from mjrl_amd.samplers.vector_sampler import sample_paths_vectorized
+    from mjrl_amd.utils.gym_env import EnvSpec
+    from stub_env import StubEnv, serial_rollout
+    policy = MLP(EnvSpec(6, 2, 40, 1), hidden_sizes=(48, 32), seed=2, init_log_std=-1.0)
+    policy.model.set_transformations(np.full(6, 0.1), np.full(6, 1.5), np.zeros(2), np.full(2, 0.5))
+    ref = serial_rollout(13, policy, 1e6, StubEnv, 100)
+    after_ref = np.random.rand()
+    got = sample_paths_vectorized(13, policy, 1e6, env=StubEnv, pegasus_seed=100, num_envs=5)
+    assert np.random.rand() == after_ref
+    assert len(got) == 13
+    for r, g in zip(ref, got):
+        assert g["terminated"] == r["terminated"]
+        assert len(g["rewards"]) == len(r["rewards"])
+        np.testing.assert_allclose(g["agent_infos"]["mean"], r["mean"], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(g["observations"], r["observations"], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(g["actions"], r["actions"], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(g["rewards"], r["rewards"], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(g["env_infos"]["norm"], r["norm"], rtol=1e-5, atol=1e-6)
+    assert any(r["terminated"] for r in ref) and not all(r["terminated"] for r in ref)
+
+
+def test_policy_mean_kernel_matches_cpu_forward():
+    """mjrl_policy_mean against the CPU MuNet for MLP(64,64) at the Humanoid shape,
+    an MLP(128,128) and a linear policy, 1000 rows."""
+    from mjrl_amd.policies.gaussian_mlp import MLP
+    from mjrl_amd.policies.gaussian_linear import LinearPolicy
+    from mjrl_amd.samplers.vector_sampler import BatchedPolicy
+    from mjrl_amd.utils.gym_env import EnvSpec
+    rs = np.random.RandomState(4)
+    for pol in (MLP(EnvSpec(376, 17, 10, 1), seed=1), MLP(EnvSpec(17, 6, 10, 1), hidden_sizes=(128, 128), seed=2),
+                LinearPolicy(EnvSpec(6, 2, 10, 1), seed=3)):
+        th = pol.get_param_values()
+        pol.set_param_values(th + 0.1 * rs.randn(th.size).astype(np.float32))
+        obs = rs.randn(1000, pol.n) * 2
+        bp = BatchedPolicy(pol, "cuda:0")
+        with torch.no_grad():
+            ref = pol.model(torch.from_numpy(obs).float()).numpy()
+        np.testing.assert_allclose(bp.means(obs), ref, rtol=1e-4, atol=1e-5)

@@ -251,13 +251,14 @@ int mjrl_fused_path(const mjrl_shape* s);
 
 /* ---- conjugate gradient on device (cg_solve.py:3-22) ----
  * State cg[MJRL_CG_STATE] (f32, device): cg[0] rdotr, cg[1] iterations run,
- * cg[2] v, cg[3] mu, cg[4] p.z; cg[8..] scratch of the multi-workgroup step
- * (ticket and per-workgroup partials).
+ * cg[2] v, cg[3] mu, cg[4] p.z; cg[8..1023] scratch of the multi-workgroup step
+ * (ticket and per-workgroup partials), cg[1024..] the p.z partials of the fused
+ * gather (one double per 64 parameters).
  * init: x = 0, r = b, p = b, rdotr = b.b; packs p into packed_p.
  * step: z = gsum * inv_T + c(sigma) * p_logstd + damping * p, then the
  *       reference's update of x, r, p, rdotr and the residual_tol break
  *       (three multi-workgroup launches; fixed-order fp64 dot products). */
-#define MJRL_CG_STATE 1024
+#define MJRL_CG_STATE 4096
 int mjrl_cg_init(const mjrl_shape* s, const float* b, float* x, float* r, float* p,
                  float* packed_p, float* cg, int32_t* done, void* stream);
 int mjrl_cg_step(const mjrl_shape* s, const float* gsum, double inv_T, float damping,
@@ -269,10 +270,12 @@ int mjrl_cg_step(const mjrl_shape* s, const float* gsum, double inv_T, float dam
  * all-reduce between the gather and the step): mjrl_gather_cg_z folds the
  * accumulate slabs (as mjrl_gather_grads, with_log_std = 0, also writing gsum)
  * and, in the same launch, forms z = gsum * inv_T + c(sigma) * p_logstd +
- * damping * p and p.z -> cg[4], v -> cg[2]; mjrl_cg_step_xr_p then updates x, r,
- * rdotr, mu, done and p / packed_p.  Same arithmetic as mjrl_cg_step (the p.z
- * partials are folded per 64 parameters instead of per 1024).  Needs
- * d <= 64 * (MJRL_CG_STATE - 16) / 2 (else MJRL_EINVAL: use the unfused pair). */
+ * damping * p and one p.z partial per 64 parameters; mjrl_cg_step_xr_p folds
+ * those partials (every workgroup, the same fixed order: no grid-wide atomic in
+ * the gather), sets p.z -> cg[4], v -> cg[2], then updates x, r, rdotr, mu, done
+ * and p / packed_p.  Same arithmetic as mjrl_cg_step (the p.z partials are
+ * folded per 64 parameters instead of per 1024).  Needs
+ * d <= 64 * (MJRL_CG_STATE - 1024) / 2 (else MJRL_EINVAL: use the unfused pair). */
 int mjrl_gather_cg_z(const mjrl_shape* s, const mjrl_rows* rows, int64_t T, const mjrl_scratch* sc,
                      const int32_t* done, float* gsum, double inv_T, float damping,
                      const float* packed_theta, const float* p, float* z, float* cg, void* stream);

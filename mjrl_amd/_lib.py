@@ -19,7 +19,8 @@ LIB_PATH = os.path.join(HERE, "lib", "libmjrl_amd.so")
 MJRL_OK = 0
 MJRL_EINVAL = -1
 MJRL_ESHAPE = -2
-CG_STATE = 1024   # MJRL_CG_STATE: floats of the device CG state
+CG_STATE = 4096   # MJRL_CG_STATE: floats of the device CG state
+CG_PZ_PARTS = 1024   # float offset of the fused gather's p.z partials (csrc/common.h)
 STEP_OUT = 1024   # MJRL_STEP_OUT: floats of mjrl_npg_step's out buffer
 MOM_SCRATCH = 2056   # MJRL_MOM_SCRATCH: doubles of the one-launch moments scratch
 

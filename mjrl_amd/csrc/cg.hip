@@ -211,7 +211,8 @@ __global__ void __launch_bounds__(CG_THREADS) k_cg_step(mjrl_shape s, const floa
 constexpr int CGM_T = 256;                 // threads per workgroup
 constexpr int CGM_U = 4;                   // elements per thread
 constexpr int CGM_WG = CGM_T * CGM_U;      // elements per workgroup
-constexpr int CGM_MAXWG = (MJRL_CG_STATE - 16) / 2;
+constexpr int CGM_MAXWG = (CG_PZ_PARTS - 16) / 2;   // partials below the fused gather's region
+constexpr int CG_PZ_MAX = (MJRL_CG_STATE - CG_PZ_PARTS) / 2;   // fused gather workgroups (64 parameters each)
 
 // fixed-order fold of nwg per-workgroup partials by the last workgroup to finish
 __device__ __forceinline__ bool cgm_last(double part, float* cg, int nwg, double* red, double& total) {
@@ -281,6 +282,45 @@ __global__ void __launch_bounds__(CGM_T) k_cgm_xr(int d, const float* __restrict
     __shared__ double red[CGM_T / 64];
     if (*done) return;
     const float v = cg[2];
+    double acc = 0.0;
+#pragma unroll
+    for (int u = 0; u < CGM_U; ++u) {
+        const int f = blockIdx.x * CGM_WG + u * CGM_T + threadIdx.x;
+        if (f >= d) continue;
+        x[f] = __fadd_rn(x[f], __fmul_rn(v, p[f]));
+        const float rf = __fsub_rn(r[f], __fmul_rn(v, z[f]));
+        r[f] = rf;
+        acc += (double)rf * (double)rf;
+    }
+    double t;
+    if (cgm_last(acc, cg, gridDim.x, red, t) && threadIdx.x == 0) {
+        const float rr = (float)t;
+        const float rdotr = cg[0];
+        cg[3] = rr / rdotr;   // mu
+        cg[0] = rr;
+        cg[1] += 1.f;
+        if (rr < tol) *done = 1;   // cg_solve.py:19-20
+    }
+}
+
+// k_cgm_xr after the fused gather (mjrl_gather_cg_z): every workgroup first folds
+// the gather's ng p.z partials in the same fixed order (thread t: partials t, t +
+// CGM_T, ...; then the block tree), so all of them hold the same p.z and v =
+// rdotr / p.z without a grid-wide ticket in the gather; workgroup 0 records both.
+__global__ void __launch_bounds__(CGM_T) k_cgm_xr_f(int d, const float* __restrict__ p, const float* __restrict__ z,
+                                                    float* __restrict__ x, float* __restrict__ r, float* cg,
+                                                    int32_t* __restrict__ done, float tol, int ng) {
+    __shared__ double red[CGM_T / 64];
+    if (*done) return;
+    const double* pzp = reinterpret_cast<const double*>(cg + CG_PZ_PARTS);
+    double q = 0.0;
+    for (int i = threadIdx.x; i < ng; i += CGM_T) q += pzp[i];
+    const float pz = (float)block_sum<CGM_T>(q, red);
+    const float v = cg[0] / pz;   // v = rdotr / p.z
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        cg[4] = pz;
+        cg[2] = v;
+    }
     double acc = 0.0;
 #pragma unroll
     for (int u = 0; u < CGM_U; ++u) {
@@ -523,9 +563,10 @@ int mjrl_cg_step_xr_p(const mjrl_shape* s, float* x, float* r, float* p, const f
                       int32_t* done, float residual_tol, void* stream) {
     if (!s || !x || !r || !p || !z || !packed_p || !cg || !done) return MJRL_EINVAL;
     const int nwg = (s->d + CGM_WG - 1) / CGM_WG;
-    if (nwg > CGM_MAXWG) return MJRL_EINVAL;
+    const int ng = (s->d + 63) / 64;   // the fused gather's workgroups
+    if (nwg > CGM_MAXWG || ng > CG_PZ_MAX) return MJRL_EINVAL;
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_cgm_xr, dim3(nwg), dim3(CGM_T), 0, st, s->d, p, z, x, r, cg, done, residual_tol);
+    hipLaunchKernelGGL(k_cgm_xr_f, dim3(nwg), dim3(CGM_T), 0, st, s->d, p, z, x, r, cg, done, residual_tol, ng);
     hipLaunchKernelGGL(k_cgm_p, dim3(nwg), dim3(CGM_T), 0, st, *s, r, p, packed_p, cg, done);
     return err(hipGetLastError());
 }

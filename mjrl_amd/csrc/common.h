@@ -304,8 +304,9 @@ __device__ __forceinline__ float cg_logstd_curv(float log_std) {
 }
 
 // wave 0 of a gather workgroup: lane -> flat parameter f (< d), gs = the folded
-// (f32-rounded) gradient sum of f.  Writes z, folds p.z, and in the last workgroup
-// sets cg[4] = p.z and cg[2] = v = rdotr / p.z (cg_solve.py:12).
+// (f32-rounded) gradient sum of f.  Writes z and this workgroup's partial of p.z
+// (cg[CG_PZ_PARTS + 2 blockIdx.x], a double); mjrl_cg_step_xr_p folds them.
+constexpr int CG_PZ_PARTS = 1024;   // float offset of the fused gather's p.z partials in the CG state
 __device__ __forceinline__ void cgz_epilogue(const CgZ& c, int f, int d, float gs) {
     double pz = 0.0;
     if (f < d) {
@@ -324,13 +325,7 @@ __device__ __forceinline__ void cgz_epilogue(const CgZ& c, int f, int d, float g
         pz = (double)pf * (double)zf;
     }
     pz = wave_sum(pz);
-    double t;
-    if (last_wg_fold(pz, reinterpret_cast<double*>(c.cg + 16), reinterpret_cast<unsigned*>(c.cg + 8), gridDim.x, t) &&
-        (threadIdx.x & 63) == 0) {
-        const float pzf = (float)t;
-        c.cg[4] = pzf;
-        c.cg[2] = c.cg[0] / pzf;
-    }
+    if ((threadIdx.x & 63) == 0) reinterpret_cast<double*>(c.cg + CG_PZ_PARTS)[blockIdx.x] = pz;
 }
 
 // Offsets (in floats) of the packed parameter set — see pack_params.

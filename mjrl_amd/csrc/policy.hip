@@ -1189,7 +1189,7 @@ int mjrl_gather_cg_z(const mjrl_shape* s, const mjrl_rows* rows, int64_t T, cons
     if (!rows_ok(s, rows) || !sc || !gsum || !packed_theta || !p || !z || !cg || T < 0 || T > rows->T)
         return MJRL_EINVAL;
     if (!shape_supported(s->h0, s->h1, s->mp)) return MJRL_ESHAPE;
-    if ((s->d + 63) / 64 > (MJRL_CG_STATE - 16) / 2) return MJRL_EINVAL;   // partials beyond the CG state
+    if ((s->d + 63) / 64 > (MJRL_CG_STATE - CG_PZ_PARTS) / 2) return MJRL_EINVAL;   // partials beyond the CG state
     const Packed pk(s->h0, s->h1, s->np, s->mp);
     CgZ cz{p, z, cg, packed_theta + pk.ls, inv_T, damping, s->d - s->m};
     return run_gather(s, rows, T, sc, nullptr, done, gsum, (hipStream_t)stream, cz);

@@ -708,7 +708,7 @@ class UpdateEngine:
                 inv_T_fvp = inv_T if sub is None else 1.0 / max(sub["Ts"], 1)
                 # gather + CG z fused when no all-reduce sits between them and the CG
                 # state holds one p.z partial per 64 parameters
-                fuse_cg = self.comm.world_size == 1 and (s.d + 63) // 64 <= (_lib.CG_STATE - 16) // 2
+                fuse_cg = self.comm.world_size == 1 and (s.d + 63) // 64 <= (_lib.CG_STATE - _lib.CG_PZ_PARTS) // 2
                 for k in range(int(cg_iters)):
                     rows_k, sc_k, T_k = rows_fvp, sc_fvp, T
                     if sub is not None:

@@ -12,8 +12,10 @@ Synthetic data: obs / act / rewards ~ N(0,1) from a per-path seeded generator;
 LinearBaseline fitted once on 20 paths and frozen.  A step = one full update
 from the device-resident f64 paths: batch assembly, GAE, whitening, forward +
 VPG, 10 Fisher-vector products + CG, step, post-step surrogate / KL, host
-readback of the statistics.  On one GPU the update is replayed as one captured
-hipGraph (--no-graph: eager launches; both times are reported).
+readback of the statistics.  On one GPU an update of at most
+engine.GRAPH_AUTO_ROWS rows is replayed as one captured hipGraph (launch gaps
+dominate there; at 1M rows eager launches are faster), and the eager time is
+reported beside it (--graph on / off forces either).
 
 --config c2 / c3 / c5 runs the other BASELINE.json GPU shapes (Swimmer NPG,
 HalfCheetah TRPO with its line search, door DAPG with demonstrations) with their
@@ -328,8 +330,9 @@ def main():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only to rehearse the N > 1 "
                          "path with several ranks on one GPU)")
-    ap.add_argument("--graph", action=argparse.BooleanOptionalAction, default=True,
-                    help="replay each update as one captured hipGraph (one GPU; default on)")
+    ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
+                    help="replay each update as one captured hipGraph (one GPU): auto = the engine's "
+                         "default, graphs for batches up to engine.GRAPH_AUTO_ROWS rows")
     ap.add_argument("--precision", default=None, choices=["auto", "split", "f32"],
                     help="first-layer MFMA form (UpdateEngine precision; default: split where supported)")
     args = ap.parse_args()
@@ -366,8 +369,11 @@ def main():
     th0 = torch.from_numpy(initial_theta(cfg)).to(device)
     th = th0.clone()
     upd = update_args(cfg, T_total)
-    eng.graphs = args.graph and world == 1
-    eng.kernel_timing = []   # per-FVP (start, accumulate done, gather done) events
+    eng.graphs = {"auto": "auto", "on": True, "off": False}[args.graph] if world == 1 else False
+    # per-FVP (start, accumulate done, gather done) events on eager steps; a captured
+    # graph is kept free of them (30 event nodes per update measured +3 % on the
+    # replay) and the kernel timings come from eager steps after the timed region
+    eng.kernel_timing = None if eng.graphs else []
 
     def step(graph=None, e=eng):
         nonlocal th
@@ -376,7 +382,8 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    eng.kernel_timing.clear()
+    if eng.kernel_timing is not None:
+        eng.kernel_timing.clear()
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -392,25 +399,24 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # dominant-kernel roofline from live HIP events on the launch stream.  Eager
-    # steps record them around every FVP of the timed region; a replayed hipGraph
-    # holds them as captured event nodes (valid after each replay completes), read
-    # over three more replays
-    graphed = eng.graph_kernel_timing() is not None
-    samples = [(a.elapsed_time(b), b.elapsed_time(c)) for a, b, c in eng.kernel_timing]
+    # dominant-kernel roofline from live HIP events on the launch stream, recorded
+    # around every FVP of eager steps: the timed region's when it ran eager, else
+    # the same update run eagerly after it (which also gives eager_ms_per_step)
+    graphed = bool(eng.graphs) and eng._gstate.get("graph") is not None
+    samples = [] if eng.kernel_timing is None else \
+        [(a.elapsed_time(b), b.elapsed_time(c)) for a, b, c in eng.kernel_timing]
     eager_ms = None
     if graphed:
-        for _ in range(3):
-            step()
-            torch.cuda.synchronize()
-            samples += [(a.elapsed_time(b), b.elapsed_time(c)) for a, b, c in eng.graph_kernel_timing()]
+        eng.kernel_timing = []
+        step(graph=False)
         torch.cuda.synchronize()
+        eng.kernel_timing.clear()
         te = time.perf_counter()
-        for _ in range(2):   # the same update without the graph, for reference
+        for _ in range(3):   # the same update without the graph
             step(graph=False)
         torch.cuda.synchronize()
-        eager_ms = (time.perf_counter() - te) / 2 * 1e3
-        samples = [sm for sm in samples if np.isfinite(sm[0])]
+        eager_ms = (time.perf_counter() - te) / 3 * 1e3
+        samples = [(a.elapsed_time(b), b.elapsed_time(c)) for a, b, c in eng.kernel_timing]
     if not samples:   # no events available: time the accumulate / gather pair alone
         eng.kernel_timing = []
         step(graph=False)
@@ -468,7 +474,7 @@ def main():
     f32_ms = None
     if world == 1 and eng.split and not args.no_f32:
         e32 = UpdateEngine(n, m, hidden, device=device, precision="f32")
-        e32.graphs = args.graph
+        e32.graphs = eng.graphs
         th = th0.clone()
         for _ in range(2):
             step(e=e32)

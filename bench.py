@@ -90,11 +90,38 @@ def cpu_model():
 
 
 def host_cores():
-    """CPU cores this process may run on (affinity), as the CPU baseline uses them."""
+    """CPU cores this process may actually use, as the CPU baseline uses them: the
+    affinity set, capped by the cgroup CPU quota (a container's affinity can list
+    the whole machine while its quota is a fraction of it) and by
+    OMP_NUM_THREADS when the environment sets it."""
     try:
-        return len(os.sched_getaffinity(0))
+        n = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
-        return os.cpu_count() or 1
+        n = os.cpu_count() or 1
+    quota = None
+    try:   # cgroup v2
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:   # cgroup v1
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    if quota:
+        n = min(n, max(1, int(quota)))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def log(msg):
+    """Progress on stderr (the JSON line alone goes to stdout)."""
+    print("bench: " + msg, file=sys.stderr, flush=True)
 
 
 def pmc_traffic(kernel_key):
@@ -240,8 +267,13 @@ def cpu_baseline(rows, base, reps=3, cfg=None):
         O.update(pol, obs[:r], act[:r], adv, rew[:r], lengths[:Pr], **kw)
         return time.perf_counter() - t0
 
+    log("cpu baseline: %d timesteps on %d threads" % (P * H, cores))
     one(max(H, (P * H // 10) // H * H))
-    ts = sorted(one(P * H) for _ in range(reps))
+    ts = []
+    for i in range(reps):
+        ts.append(one(P * H))
+        log("cpu baseline update %d: %.2f s" % (i + 1, ts[-1]))
+    ts.sort()
     dt = ts[len(ts) // 2]
     return dict(value=round(P * H / dt, 1), unit="timesteps/s", cores=cores, kind="port", cpu=cpu_model(),
                 sample="%d paths x %d steps (%d timesteps) of the same %s workload, one update "
@@ -394,6 +426,7 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
+    log("timed region: %d steps, %.3f ms per step" % (args.steps, elapsed / args.steps * 1e3))
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -473,6 +506,7 @@ def main():
     # the same update on the exact-f32 MFMA kernels (precision='f32'), for reference
     f32_ms = None
     if world == 1 and eng.split and not args.no_f32:
+        log("exact-f32 companion timing")
         e32 = UpdateEngine(n, m, hidden, device=device, precision="f32")
         e32.graphs = eng.graphs
         th = th0.clone()
@@ -503,6 +537,7 @@ def main():
                    roofline=roof)
         if world == 1 and not args.no_e2e and cfg["algo"] != "dapg":
             th = th0.clone()
+            log("end-to-end from host paths")
             out["e2e_from_host"] = e2e_from_host((p0, p1), eng, th, base, upd, device, cfg)
         if world == 1 and not args.no_cpu_baseline:
             rows = T_total if (args.cpu_full or args.config != "c4") else args.cpu_rows

@@ -3,8 +3,13 @@
 API of mjrl/baselines/linear_baseline.py:4-49: `predict(path)` feeds
 compute_advantages; `fit(paths, return_errors)` solves the ridge normal
 equations on [clip(obs, +-10), t/1000, (t/1000)^2, (t/1000)^3, 1] features.
-Host numpy (fp64) — it is the caller's object; moving fit onto the GPU is the
-next row of the scope table (§8f, f1).
+This object is the host numpy (fp64) form, used when a caller calls it directly.
+Inside the agents both directions run on the GPU from the batch already in HBM:
+predict as k_linear_baseline while the paths are staged (engine.DeviceBatch,
+C-ABI mjrl_linear_baseline), and fit as the fp64 MFMA Gram of [features,
+returns] plus the residual pass (UpdateEngine.fit_linear_baseline, C-ABI
+mjrl_linear_baseline_gram / _residual) followed by this class's lstsq retry loop
+on the (n+5) x (n+5) system (§8f row f1).
 """
 import numpy as np
 

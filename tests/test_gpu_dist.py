@@ -41,15 +41,28 @@ def _worker(rank, world, port, name, q):
         r0, r1 = offs[p0], offs[p1]
         dev = torch.device("cuda:0")
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
-        b = DeviceBatch(t(c["obs64"][r0:r1]), t(c["act64"][r0:r1]), t(c["rewards"][r0:r1]),
+        obs, act, T_demo = c["obs64"][r0:r1], c["act64"][r0:r1], 0
+        if "demo_obs" in c:
+            # DAPG: the 200-row demo paths are split over the ranks (BatchREINFORCE._rank_share),
+            # so each demo row enters the all-reduced VPG sum once
+            nd = c["demo_obs"].shape[0] // 200
+            d0, d1 = partition_paths(np.full(nd, 200), world)[rank]
+            obs = np.concatenate([obs, c["demo_obs"][200 * d0:200 * d1].astype(np.float64)])
+            act = np.concatenate([act, c["demo_act"][200 * d0:200 * d1].astype(np.float64)])
+            T_demo = 200 * (d1 - d0)
+        b = DeviceBatch(t(obs), t(act), t(c["rewards"][r0:r1]),
                         t(c["baseline"][r0:r1]), t(offs[p0:p1 + 1] - offs[p0]),
-                        t(c["terminated"][p0:p1].astype(np.uint8)))
+                        t(c["terminated"][p0:p1].astype(np.uint8)), T_demo=T_demo)
         eng = UpdateEngine(int(c["n"]), int(c["m"]), c["hidden_t"], device=dev, comm=DistComm())
+        if c["transforms"] is not None:
+            eng.set_transformations(*c["transforms"])
         args = dict(algo=kw["algo"], gamma=float(c["gamma"]), gae_lambda=float(c["gae_lambda"]), trpo_verbose=False)
         if kw["algo"] == "npg":
             args["n_step_size"] = kw.get("n_step_size", 0.01)
         else:
             args["kl_dist"] = kw["kl_dist"]
+        if kw["algo"] == "dapg":
+            args["demo_coef"] = kw["demo_coef"]
         if "hvp_sample_frac" in kw:
             # rank 0 draws (and must match the reference's draws); rank 1's RNG is
             # deliberately different to show the broadcast is what it uses
@@ -61,7 +74,7 @@ def _worker(rank, world, port, name, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name", ["c2_ragged", "c3_halfcheetah_trpo", "c2_hvp_sub", "c4_humanoid"])
+@pytest.mark.parametrize("name", ["c2_ragged", "c3_halfcheetah_trpo", "c2_hvp_sub", "c4_humanoid", "c5_door_dapg"])
 def test_two_rank_update(name):
     from oracle import npg_cpu as O
     world = 2

@@ -270,17 +270,19 @@ int mjrl_cg_step(const mjrl_shape* s, const float* gsum, double inv_T, float dam
  * all-reduce between the gather and the step): mjrl_gather_cg_z folds the
  * accumulate slabs (as mjrl_gather_grads, with_log_std = 0, also writing gsum)
  * and, in the same launch, forms z = gsum * inv_T + c(sigma) * p_logstd +
- * damping * p and one p.z partial per 64 parameters; mjrl_cg_step_xr_p folds
- * those partials (every workgroup, the same fixed order: no grid-wide atomic in
- * the gather), sets p.z -> cg[4], v -> cg[2], then updates x, r, rdotr, mu, done
- * and p / packed_p.  Same arithmetic as mjrl_cg_step (the p.z partials are
+ * damping * p and one p.z partial per 64 parameters; mjrl_cg_step_xr_p (one
+ * launch) folds those partials and the new r.r in every workgroup (the same
+ * fixed order: no grid-wide atomic in the gather, no second launch), sets
+ * p.z -> cg[4], v -> cg[2], then updates x, r (into r_out != r: the caller
+ * alternates the two buffers), rdotr, mu, done and p / packed_p.  Same arithmetic as mjrl_cg_step (the p.z partials are
  * folded per 64 parameters instead of per 1024).  Needs
  * d <= 64 * (MJRL_CG_STATE - 1024) / 2 (else MJRL_EINVAL: use the unfused pair). */
 int mjrl_gather_cg_z(const mjrl_shape* s, const mjrl_rows* rows, int64_t T, const mjrl_scratch* sc,
                      const int32_t* done, float* gsum, double inv_T, float damping,
                      const float* packed_theta, const float* p, float* z, float* cg, void* stream);
-int mjrl_cg_step_xr_p(const mjrl_shape* s, float* x, float* r, float* p, const float* z,
-                      float* packed_p, float* cg, int32_t* done, float residual_tol, void* stream);
+int mjrl_cg_step_xr_p(const mjrl_shape* s, float* x, const float* r, float* r_out, float* p,
+                      const float* z, float* packed_p, float* cg, int32_t* done, float residual_tol,
+                      void* stream);
 
 /* Generic CG (cg_solve.py:3-22 with a caller-supplied operator): init from b,
  * then one update per z = A p the caller computed.  Same scalar arithmetic and

@@ -303,42 +303,61 @@ __global__ void __launch_bounds__(CGM_T) k_cgm_xr(int d, const float* __restrict
     }
 }
 
-// k_cgm_xr after the fused gather (mjrl_gather_cg_z): every workgroup first folds
-// the gather's ng p.z partials in the same fixed order (thread t: partials t, t +
-// CGM_T, ...; then the block tree), so all of them hold the same p.z and v =
-// rdotr / p.z without a grid-wide ticket in the gather; workgroup 0 records both.
-__global__ void __launch_bounds__(CGM_T) k_cgm_xr_f(int d, const float* __restrict__ p, const float* __restrict__ z,
-                                                    float* __restrict__ x, float* __restrict__ r, float* cg,
-                                                    int32_t* __restrict__ done, float tol, int ng) {
-    __shared__ double red[CGM_T / 64];
+// The rest of a fused-gather CG iteration in ONE launch (cg_solve.py:11-20):
+// every workgroup folds the gather's p.z partials, then computes the new
+// r.r = sum_f (r_f - v z_f)^2 over ALL of d itself (the same f32 r_f the update
+// stores, fp64 sums in the same fixed order in every workgroup), so it knows mu
+// without waiting for the others and updates x, r and p of its own 1024-element
+// chunk.  The new r goes to r_out (every workgroup reads all of r_in), the
+// caller alternating the two buffers.  The last workgroup to take the ticket (all
+// have read rdotr by then) records rdotr, mu, v, p.z, the iteration count and the
+// residual_tol break.
+constexpr int CGX_T = 1024;
+__global__ void __launch_bounds__(CGX_T) k_cgm_xrp_f(mjrl_shape s, float* __restrict__ p, const float* __restrict__ z,
+                                                     float* __restrict__ x, const float* __restrict__ r,
+                                                     float* __restrict__ r_out, float* __restrict__ packed_p, float* cg,
+                                                     int32_t* __restrict__ done, float tol, int ng) {
+    __shared__ double red[CGX_T / 64];
+    __shared__ unsigned ticket;
     if (*done) return;
+    const int d = s.d;
     const double* pzp = reinterpret_cast<const double*>(cg + CG_PZ_PARTS);
     double q = 0.0;
-    for (int i = threadIdx.x; i < ng; i += CGM_T) q += pzp[i];
-    const float pz = (float)block_sum<CGM_T>(q, red);
-    const float v = cg[0] / pz;   // v = rdotr / p.z
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        cg[4] = pz;
-        cg[2] = v;
-    }
+    for (int i = threadIdx.x; i < ng; i += CGX_T) q += pzp[i];
+    const float pz = (float)block_sum<CGX_T>(q, red);
+    const float rdotr = cg[0];
+    const float v = rdotr / pz;   // v = rdotr / p.z
     double acc = 0.0;
-#pragma unroll
-    for (int u = 0; u < CGM_U; ++u) {
-        const int f = blockIdx.x * CGM_WG + u * CGM_T + threadIdx.x;
-        if (f >= d) continue;
-        x[f] = __fadd_rn(x[f], __fmul_rn(v, p[f]));
+#pragma unroll 8
+    for (int f = threadIdx.x; f < d; f += CGX_T) {
         const float rf = __fsub_rn(r[f], __fmul_rn(v, z[f]));
-        r[f] = rf;
         acc += (double)rf * (double)rf;
     }
-    double t;
-    if (cgm_last(acc, cg, gridDim.x, red, t) && threadIdx.x == 0) {
-        const float rr = (float)t;
-        const float rdotr = cg[0];
-        cg[3] = rr / rdotr;   // mu
+    const float rr = (float)block_sum<CGX_T>(acc, red);
+    const float mu = rr / rdotr;
+    const int f = blockIdx.x * CGX_T + threadIdx.x;
+    if (f < d) {
+        const float pf = p[f];
+        x[f] = __fadd_rn(x[f], __fmul_rn(v, pf));
+        const float rf = __fsub_rn(r[f], __fmul_rn(v, z[f]));
+        r_out[f] = rf;
+        if (!(rr < tol)) {   // converged: p is not used again
+            const float pn = __fadd_rn(rf, __fmul_rn(mu, pf));
+            p[f] = pn;
+            pack_one(PackMap(s), f, pn, packed_p, false, 0.f);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) ticket = atomicAdd(reinterpret_cast<unsigned*>(cg + 8), 1u);
+    __syncthreads();
+    if (ticket == gridDim.x - 1 && threadIdx.x == 0) {
+        cg[4] = pz;
+        cg[2] = v;
+        cg[3] = mu;
         cg[0] = rr;
         cg[1] += 1.f;
         if (rr < tol) *done = 1;   // cg_solve.py:19-20
+        *reinterpret_cast<unsigned*>(cg + 8) = 0u;
     }
 }
 
@@ -559,15 +578,13 @@ int mjrl_cg_init(const mjrl_shape* s, const float* b, float* x, float* r, float*
     return err(hipGetLastError());
 }
 
-int mjrl_cg_step_xr_p(const mjrl_shape* s, float* x, float* r, float* p, const float* z, float* packed_p, float* cg,
-                      int32_t* done, float residual_tol, void* stream) {
-    if (!s || !x || !r || !p || !z || !packed_p || !cg || !done) return MJRL_EINVAL;
-    const int nwg = (s->d + CGM_WG - 1) / CGM_WG;
+int mjrl_cg_step_xr_p(const mjrl_shape* s, float* x, const float* r, float* r_out, float* p, const float* z,
+                      float* packed_p, float* cg, int32_t* done, float residual_tol, void* stream) {
+    if (!s || !x || !r || !r_out || r_out == r || !p || !z || !packed_p || !cg || !done) return MJRL_EINVAL;
     const int ng = (s->d + 63) / 64;   // the fused gather's workgroups
-    if (nwg > CGM_MAXWG || ng > CG_PZ_MAX) return MJRL_EINVAL;
-    hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_cgm_xr_f, dim3(nwg), dim3(CGM_T), 0, st, s->d, p, z, x, r, cg, done, residual_tol, ng);
-    hipLaunchKernelGGL(k_cgm_p, dim3(nwg), dim3(CGM_T), 0, st, *s, r, p, packed_p, cg, done);
+    if (ng > CG_PZ_MAX) return MJRL_EINVAL;
+    hipLaunchKernelGGL(k_cgm_xrp_f, dim3((s->d + CGX_T - 1) / CGX_T), dim3(CGX_T), 0, (hipStream_t)stream, *s, p, z,
+                       x, r, r_out, packed_p, cg, done, residual_tol, ng);
     return err(hipGetLastError());
 }
 

@@ -355,7 +355,7 @@ class UpdateEngine:
         self.packed_theta = torch.zeros(s.packed, **f32)
         self.packed_new = torch.zeros(s.packed, **f32)
         self.packed_p = torch.zeros(s.packed, **f32)
-        self.pvec = {k: torch.zeros(s.d, **f32) for k in ("g", "gsum", "x", "r", "p", "z", "theta_new")}
+        self.pvec = {k: torch.zeros(s.d, **f32) for k in ("g", "gsum", "x", "r", "r2", "p", "z", "theta_new")}
         self.cg = torch.zeros(_lib.CG_STATE, **f32)   # MJRL_CG_STATE
         self.done = torch.zeros(1, dtype=torch.int32, device=dev)
         self.out = torch.zeros(_lib.STEP_OUT, **f32)     # MJRL_STEP_OUT (results + step scratch)
@@ -742,9 +742,12 @@ class UpdateEngine:
                         e2.record()
                         prof.append((e0, e1, e2))
                     if fuse_cg:
-                        _lib.check(L.mjrl_cg_step_xr_p(sp, _lib.ptr(v["x"]), _lib.ptr(v["r"]), _lib.ptr(v["p"]),
-                                                       _lib.ptr(v["z"]), _lib.ptr(self.packed_p), _lib.ptr(self.cg),
-                                                       _lib.ptr(self.done), float(residual_tol), st), "mjrl_cg_step_xr_p")
+                        # the rest of the iteration in one launch; r alternates between two buffers
+                        r_in, r_out = (v["r"], v["r2"]) if k % 2 == 0 else (v["r2"], v["r"])
+                        _lib.check(L.mjrl_cg_step_xr_p(sp, _lib.ptr(v["x"]), _lib.ptr(r_in), _lib.ptr(r_out),
+                                                       _lib.ptr(v["p"]), _lib.ptr(v["z"]), _lib.ptr(self.packed_p),
+                                                       _lib.ptr(self.cg), _lib.ptr(self.done), float(residual_tol), st),
+                                   "mjrl_cg_step_xr_p")
                         continue
                     self.comm.allreduce_sum(v["gsum"])
                     _lib.check(L.mjrl_cg_step(sp, _lib.ptr(v["gsum"]), inv_T_fvp, float(damping),

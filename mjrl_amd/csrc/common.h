@@ -187,14 +187,17 @@ __device__ __forceinline__ short4v ds_read_tr16(const void* p) {
 // and loads one B (weight) fragment per col block per k-step, reused across its
 // row blocks.
 // ---------------------------------------------------------------------------
-template <int RB, int CB>
+template <int RB, int CB, int NW = 4>
 struct Split {
-    static constexpr int NCW = CB >= 4 ? CB / 4 : 1;
-    static constexpr int NRW = CB >= 4 ? RB : (CB == 2 ? (RB / 2 > 0 ? RB / 2 : 1) : (RB / 4 > 0 ? RB / 4 : 1));
-    static constexpr int CBS = CB >= 4 ? 4 : 1;        // col block stride
-    static constexpr int RBS = CB >= 4 ? 1 : (CB == 2 ? 2 : 4);
-    __device__ static int cb0(int w) { return CB >= 4 ? w : (CB == 2 ? (w & 1) : 0); }
-    __device__ static int rb0(int w) { return CB >= 4 ? 0 : (CB == 2 ? (w >> 1) : w); }
+    // CB >= NW: wave w owns col blocks w, w + NW, ... over every row block;
+    // CB < NW: NW / CB waves share a col block, each a strided set of row blocks
+    static constexpr int WPC = CB >= NW ? 1 : NW / CB;                 // waves per col block
+    static constexpr int NCW = CB >= NW ? CB / NW : 1;
+    static constexpr int NRW = CB >= NW ? RB : (RB + WPC - 1) / WPC;
+    static constexpr int CBS = CB >= NW ? NW : 1;                      // col block stride
+    static constexpr int RBS = CB >= NW ? 1 : WPC;
+    __device__ static int cb0(int w) { return CB >= NW ? w : w % CB; }
+    __device__ static int rb0(int w) { return CB >= NW ? 0 : w / CB; }
 };
 
 // acc[i][j] += A[rows of rb(i)][k] * W[cols of cb(j)][k], k in [kb, ke) (multiples of 16).

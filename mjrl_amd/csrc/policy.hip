@@ -54,6 +54,9 @@ struct RowArgs {
 // the HalfCheetah FVP 388 -> 298 us against 64 rows and one workgroup; 256-wide
 // layers: 32 rows (16 rows, two workgroups per CU, measured 1 % slower)
 __host__ __device__ constexpr int rows_bt(int hmax) { return hmax >= 128 ? 32 : 64; }
+// threads per k_rows workgroup: 256-wide layers keep one workgroup per CU (138 KB
+// of LDS), so they run 8 waves (two per SIMD) instead of 4
+__host__ __device__ constexpr int rows_nt(int hmax) { return hmax >= 256 ? 512 : NTHREADS; }
 
 template <int H0, int H1, int MP>
 struct Layout {
@@ -75,7 +78,8 @@ struct Layout {
     static constexpr bool XS_ALIAS = !LIN && 2 * BT * LD1 >= XS;
     static constexpr int oXS = XS_ALIAS ? oD1 : oGP + BT * LDP;
     static constexpr int end1 = XS_ALIAS ? oGP + BT * LDP : oXS + XS;
-    static constexpr int total = end1 > 2 * NTHREADS ? end1 : 2 * NTHREADS;   // >= row_pass_final's doubles
+    static constexpr int NT = rows_nt(HMAX);
+    static constexpr int total = end1 > 2 * NT ? end1 : 2 * NT;   // >= row_pass_final's doubles
     static constexpr int bytes = total * 4;
 };
 
@@ -204,11 +208,12 @@ __device__ __forceinline__ void row_pass_final(double acc0, double acc1, double*
 }
 
 template <int H0, int H1, int MP, int MODE>
-__global__ void __launch_bounds__(NTHREADS, (Layout<H0, H1, MP>::bytes > 81920 ? 1 : 2)) k_rows(RowArgs a) {
+__global__ void __launch_bounds__((Layout<H0, H1, MP>::NT), (Layout<H0, H1, MP>::bytes > 81920 ? 1 : 2))
+    k_rows(RowArgs a) {
     using L = Layout<H0, H1, MP>;
-    constexpr int BT = L::BT, RB = L::RB;
+    constexpr int BT = L::BT, RB = L::RB, NT = L::NT, NW = NT / 64;
     constexpr int N1 = L::LIN ? MP : H0;
-    using S1 = Split<RB, N1 / 16>;
+    using S1 = Split<RB, N1 / 16, NW>;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float* D0 = smem + L::oD0;
     float* A0s = smem + L::oA0;
@@ -239,13 +244,14 @@ __global__ void __launch_bounds__(NTHREADS, (Layout<H0, H1, MP>::bytes > 81920 ?
         zero_acc(acc1);
         {
             const float* W = (MODE == FVP ? a.V : P) + pk.W0;
-            constexpr int PER = BT * (L::KC / 4) / NTHREADS;
+            constexpr int PER = BT * (L::KC / 4) / NT;
+            static_assert(PER >= 1 && PER * NT == BT * (L::KC / 4), "phase-1 staging");
             float4 st[PER];
             const int nch = (np + L::KC - 1) / L::KC;
             auto gload = [&](int c) {
 #pragma unroll
                 for (int u = 0; u < PER; ++u) {
-                    const int idx = tid + u * NTHREADS;
+                    const int idx = tid + u * NT;
                     const int row = idx / (L::KC / 4), c4 = idx % (L::KC / 4);
                     const int col = c * L::KC + c4 * 4;
                     const int64_t gr = row_base + row;
@@ -258,7 +264,7 @@ __global__ void __launch_bounds__(NTHREADS, (Layout<H0, H1, MP>::bytes > 81920 ?
                 float* xs = XS + (c & 1) * BT * L::LDX;
 #pragma unroll
                 for (int u = 0; u < PER; ++u) {
-                    const int idx = tid + u * NTHREADS;
+                    const int idx = tid + u * NT;
                     const int row = idx / (L::KC / 4), c4 = idx % (L::KC / 4);
                     *reinterpret_cast<float4*>(xs + row * L::LDX + c4 * 4) = st[u];
                 }
@@ -328,7 +334,7 @@ __global__ void __launch_bounds__(NTHREADS, (Layout<H0, H1, MP>::bytes > 81920 ?
             __syncthreads();
 
             // ---------------- phase 2: [BT x H1], K = H0 ----------------
-            using S2 = Split<RB, H1 / 16>;
+            using S2 = Split<RB, H1 / 16, NW>;
             floatx4 acc2[S2::NRW][S2::NCW];
             zero_acc(acc2);
             if (MODE == FVP) {
@@ -369,7 +375,7 @@ __global__ void __launch_bounds__(NTHREADS, (Layout<H0, H1, MP>::bytes > 81920 ?
             __syncthreads();
 
             // ---------------- phase 3: [BT x MP], K = H1 ----------------
-            using S3 = Split<RB, MP / 16>;
+            using S3 = Split<RB, MP / 16, NW>;
             floatx4 acc3[S3::NRW][S3::NCW];
             zero_acc(acc3);
             if (MODE == FVP) {
@@ -416,14 +422,14 @@ __global__ void __launch_bounds__(NTHREADS, (Layout<H0, H1, MP>::bytes > 81920 ?
 
         // ---------------- per-row pass: log-likelihood, VPG upstream, LR, KL -------------
         if (MODE != FVP) {
-            row_pass<MODE, BT, MP, NTHREADS, true>(a, P + pk.ls, sls, row_base, GPs, L::LDP, racc0, racc1, tid);
+            row_pass<MODE, BT, MP, NT, true>(a, P + pk.ls, sls, row_base, GPs, L::LDP, racc0, racc1, tid);
             __syncthreads();
         }
 
         if constexpr (!L::LIN) {
             if (MODE != EVAL) {
                 // ---------------- phase 4: ga1 = g * W2, K = MP ----------------
-                using S2 = Split<RB, H1 / 16>;
+                using S2 = Split<RB, H1 / 16, NW>;
                 floatx4 acc4[S2::NRW][S2::NCW];
                 zero_acc(acc4);
                 gemm_tile(acc4, GPs, L::LDP, 0, S2::rb0(w), S2::RBS, RB, P + pk.W2T, MP, S2::cb0(w), S2::CBS, 0, MP,
@@ -474,9 +480,9 @@ __global__ void __launch_bounds__(NTHREADS, (Layout<H0, H1, MP>::bytes > 81920 ?
     }
 
     if (MODE != FVP) {
-        static_assert(L::total >= 2 * NTHREADS, "row_pass_final scratch");
+        static_assert(L::total >= 2 * NT, "row_pass_final scratch");
         __syncthreads();
-        row_pass_final<MODE, MP, NTHREADS>(racc0, racc1, reinterpret_cast<double*>(smem), a.rpart, blockIdx.x, tid);
+        row_pass_final<MODE, MP, NT>(racc0, racc1, reinterpret_cast<double*>(smem), a.rpart, blockIdx.x, tid);
     }
 }
 
@@ -810,7 +816,7 @@ int launch_rows_t(const RowArgs& ra, int grid, hipStream_t st) {
         if (e != hipSuccess) return (int)e;
         attr = true;
     }
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(NTHREADS), L::bytes, st, ra);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(L::NT), L::bytes, st, ra);
     return (int)hipGetLastError();
 }
 

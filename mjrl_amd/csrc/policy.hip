@@ -54,9 +54,11 @@ struct RowArgs {
 // the HalfCheetah FVP 388 -> 298 us against 64 rows and one workgroup; 256-wide
 // layers: 32 rows (16 rows, two workgroups per CU, measured 1 % slower)
 __host__ __device__ constexpr int rows_bt(int hmax) { return hmax >= 128 ? 32 : 64; }
-// threads per k_rows workgroup: 256-wide layers keep one workgroup per CU (138 KB
-// of LDS), so they run 8 waves (two per SIMD) instead of 4
-__host__ __device__ constexpr int rows_nt(int hmax) { return hmax >= 256 ? 512 : NTHREADS; }
+// threads per k_rows workgroup: 8 waves for 128- and 256-wide layers (the
+// 256-wide layout is one 138 KB workgroup per CU: two waves per SIMD; 128-wide
+// two 70 KB workgroups: four).  Measured against 4 waves: door DAPG FVP 415 ->
+// 369 us, HalfCheetah TRPO FVP 298 -> 251 us
+__host__ __device__ constexpr int rows_nt(int hmax) { return hmax >= 128 ? 512 : NTHREADS; }
 
 template <int H0, int H1, int MP>
 struct Layout {

@@ -54,11 +54,12 @@ struct RowArgs {
 // the HalfCheetah FVP 388 -> 298 us against 64 rows and one workgroup; 256-wide
 // layers: 32 rows (16 rows, two workgroups per CU, measured 1 % slower)
 __host__ __device__ constexpr int rows_bt(int hmax) { return hmax >= 128 ? 32 : 64; }
-// threads per k_rows workgroup: 8 waves for 128- and 256-wide layers (the
-// 256-wide layout is one 138 KB workgroup per CU: two waves per SIMD; 128-wide
-// two 70 KB workgroups: four).  Measured against 4 waves: door DAPG FVP 415 ->
-// 369 us, HalfCheetah TRPO FVP 298 -> 251 us
-__host__ __device__ constexpr int rows_nt(int hmax) { return hmax >= 128 ? 512 : NTHREADS; }
+// threads per k_rows workgroup.  256-wide layers: one 138 KB workgroup per CU of
+// 16 waves (four per SIMD, 128 VGPRs each); 128-wide: two 70 KB workgroups of 8
+// waves.  Measured against 4 waves: door DAPG FVP 415 -> 369 us (8 waves) -> 353
+// us (16); HalfCheetah TRPO FVP 298 -> 251 us (8).  The phase-1 staging and the
+// row pass leave threads beyond the tile's elements idle.
+__host__ __device__ constexpr int rows_nt(int hmax) { return hmax >= 256 ? 1024 : (hmax >= 128 ? 512 : NTHREADS); }
 
 template <int H0, int H1, int MP>
 struct Layout {
@@ -116,8 +117,9 @@ template <int MODE, int BT, int MP, int NT, bool STORE_GP>
 __device__ __forceinline__ void row_pass(const RowArgs& a, const float* __restrict__ P_ls, float sls,
                                          int64_t row_base, float* GPs, int ldp, double& acc0, double& acc1,
                                          int tid) {
-    constexpr int PER = BT * MP / NT;
-    static_assert(NT % MP == 0 && PER * NT == BT * MP && MP <= 64, "row lanes in one wave");
+    constexpr int NE = BT * MP;                        // (row, action) elements of the tile
+    constexpr int PER = NE >= NT ? NE / NT : 1;        // more threads than elements: the rest idle
+    static_assert(NT % MP == 0 && (NE >= NT ? PER * NT == NE : NT % NE == 0) && MP <= 64, "row lanes in one wave");
     const int m = a.m;
     const int64_t T = a.T;
     const int j = tid % MP;
@@ -133,11 +135,12 @@ __device__ __forceinline__ void row_pass(const RowArgs& a, const float* __restri
     }
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
-        const int row = (tid + u * NT) / MP;
-        const int64_t gr = row_base + row;
+        const bool in = NE >= NT || tid + u * NT < NE;
+        const int row = in ? (tid + u * NT) / MP : 0;
+        const int64_t gr = in ? row_base + row : T;        // an idle thread acts as a row past T
         const bool valid = gr < T && act_j;
         float* g = GPs + row * ldp + j;
-        const float mu = *g;
+        const float mu = in ? *g : 0.f;
         const float av = valid ? a.act[gr * m + j] : 0.f;
         float mo = 0.f, adv = 0.f;
         if (MODE == EVAL) mo = valid ? a.mu0[gr * m + j] : 0.f;
@@ -151,7 +154,7 @@ __device__ __forceinline__ void row_pass(const RowArgs& a, const float* __restri
                 acc0 += (double)(adv * (z2 - 1.f));
             }
             const float gv = valid ? adv * (zs / sn) * os : 0.f;
-            *g = gv;
+            if (in) *g = gv;
             if (STORE_GP && gr < T) a.gp[gr * MP + j] = gv;
         } else if (valid) {
             const float dm = mo - mu;
@@ -246,8 +249,9 @@ __global__ void __launch_bounds__((Layout<H0, H1, MP>::NT), (Layout<H0, H1, MP>:
         zero_acc(acc1);
         {
             const float* W = (MODE == FVP ? a.V : P) + pk.W0;
-            constexpr int PER = BT * (L::KC / 4) / NT;
-            static_assert(PER >= 1 && PER * NT == BT * (L::KC / 4), "phase-1 staging");
+            constexpr int NQ = BT * (L::KC / 4);              // float4 pieces of a staged chunk
+            constexpr int PER = NQ >= NT ? NQ / NT : 1;
+            static_assert(NQ < NT ? NT % NQ == 0 : PER * NT == NQ, "phase-1 staging");
             float4 st[PER];
             const int nch = (np + L::KC - 1) / L::KC;
             auto gload = [&](int c) {
@@ -257,7 +261,7 @@ __global__ void __launch_bounds__((Layout<H0, H1, MP>::NT), (Layout<H0, H1, MP>:
                     const int row = idx / (L::KC / 4), c4 = idx % (L::KC / 4);
                     const int col = c * L::KC + c4 * 4;
                     const int64_t gr = row_base + row;
-                    st[u] = (gr < T && col < np) ? *reinterpret_cast<const float4*>(a.xhat + gr * np + col)
+                    st[u] = (idx < NQ && gr < T && col < np) ? *reinterpret_cast<const float4*>(a.xhat + gr * np + col)
                                                  : make_float4(0.f, 0.f, 0.f, 0.f);
                 }
             };
@@ -268,7 +272,7 @@ __global__ void __launch_bounds__((Layout<H0, H1, MP>::NT), (Layout<H0, H1, MP>:
                 for (int u = 0; u < PER; ++u) {
                     const int idx = tid + u * NT;
                     const int row = idx / (L::KC / 4), c4 = idx % (L::KC / 4);
-                    *reinterpret_cast<float4*>(xs + row * L::LDX + c4 * 4) = st[u];
+                    if (idx < NQ) *reinterpret_cast<float4*>(xs + row * L::LDX + c4 * 4) = st[u];
                 }
                 __syncthreads();
                 if (c + 1 < nch) gload(c + 1);

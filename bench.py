@@ -10,7 +10,9 @@ gamma 0.995, lambda 0.97; 1000 paths x 1000 steps = 1,000,000 timesteps per
 update, split by paths over the N ranks (strong scaling: the batch is fixed).
 Synthetic data: obs / act / rewards ~ N(0,1) from a per-path seeded generator;
 LinearBaseline fitted once on 20 paths and frozen.  A step = one full update
-from the device-resident f64 paths: batch assembly, GAE, whitening, forward +
+from the device-resident batch in the layout train_step stages it (f32
+observations / actions, f64 rewards and baseline; --stage-dtype f64 keeps the
+sampler's f64): batch assembly, GAE, whitening, forward +
 VPG, 10 Fisher-vector products + CG, step, post-step surrogate / KL, host
 readback of the statistics.  On one GPU an update of at most
 engine.GRAPH_AUTO_ROWS rows is replayed as one captured hipGraph (launch gaps
@@ -200,7 +202,10 @@ def demo_share(cfg, rank, world):
     return o, a
 
 
-def stage_shard(p0, p1, device, base, cfg=None, demos=None):
+def stage_shard(p0, p1, device, base, cfg=None, demos=None, dtype=np.float32):
+    """This rank's paths as a device batch in the layout train_step stages them
+    (BatchREINFORCE.staging_dtype: float32 observations / actions by default,
+    f64 rewards and baseline predictions)."""
     from mjrl_amd.engine import DeviceBatch
     cfg = cfg or CONFIGS["c4"]
     H, n, m = cfg["horizon"], cfg["n"], cfg["m"]
@@ -211,10 +216,11 @@ def stage_shard(p0, p1, device, base, cfg=None, demos=None):
     if demos is not None:
         obs, act = obs + demos[0], act + demos[1]
         T_demo = sum(len(o) for o in demos[0])
-    ho = torch.empty((T + T_demo, n), dtype=torch.float64, pin_memory=True)
-    np.concatenate(obs, out=ho.numpy())
-    ha = torch.empty((T + T_demo, m), dtype=torch.float64, pin_memory=True)
-    np.concatenate(act, out=ha.numpy())
+    tdt = torch.float32 if np.dtype(dtype) == np.float32 else torch.float64
+    ho = torch.empty((T + T_demo, n), dtype=tdt, pin_memory=True)
+    np.concatenate(obs, out=ho.numpy(), casting="same_kind")
+    ha = torch.empty((T + T_demo, m), dtype=tdt, pin_memory=True)
+    np.concatenate(act, out=ha.numpy(), casting="same_kind")
     rw = np.concatenate(rew)
     bl = np.concatenate([base.predict(dict(observations=o.astype(np.float64), rewards=r))
                          for o, r in zip(obs[:P], rew)])
@@ -359,6 +365,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end-from-host-paths measurement")
     ap.add_argument("--no-f32", action="store_true", help="skip the exact-f32 companion timing")
+    ap.add_argument("--stage-dtype", choices=("f32", "f64"), default="f32",
+                    help="observations / actions of the device-resident batch: f32 as train_step stages them "
+                         "(BatchREINFORCE.staging_dtype), or the sampler's f64")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only to rehearse the N > 1 "
                          "path with several ranks on one GPU)")
@@ -394,7 +403,8 @@ def main():
 
     base = baseline_coeffs(cfg)
     p0, p1 = partition_paths(np.full(cfg["paths"], H), world)[rank]
-    batch = stage_shard(p0, p1, device, base, cfg, demo_share(cfg, rank, world))
+    batch = stage_shard(p0, p1, device, base, cfg, demo_share(cfg, rank, world),
+                        np.float32 if args.stage_dtype == "f32" else np.float64)
     T_total = cfg["paths"] * H
 
     eng = UpdateEngine(n, m, hidden, device=device, comm=comm, precision=args.precision)

@@ -284,6 +284,16 @@ int mjrl_cg_step_xr_p(const mjrl_shape* s, float* x, const float* r, float* r_ou
                       const float* z, float* packed_p, float* cg, int32_t* done, float residual_tol,
                       void* stream);
 
+/* The whole iteration of mjrl_cg_step in one launch (the sharded path: gsum is
+ * the all-reduced sum): every workgroup forms z for all of d on the fly and folds
+ * p.z and the new r.r itself, then updates x, r and p of its own chunk; r and p
+ * go to r_out / p_out (!= r / p: the caller alternates each pair).  Same
+ * arithmetic as mjrl_cg_step up to the order of the fp64 dot-product sums. */
+int mjrl_cg_step1(const mjrl_shape* s, const float* gsum, double inv_T, float damping,
+                  const float* packed_theta, float* x, const float* r, float* r_out, const float* p,
+                  float* p_out, float* packed_p, float* cg, int32_t* done, float residual_tol,
+                  void* stream);
+
 /* Generic CG (cg_solve.py:3-22 with a caller-supplied operator): init from b,
  * then one update per z = A p the caller computed.  Same scalar arithmetic and
  * residual_tol break as mjrl_cg_step. */

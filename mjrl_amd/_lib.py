@@ -76,6 +76,7 @@ SIGNATURES = {
     "mjrl_cg_step": [SP, P, F64, F32, P, P, P, P, P, P, P, P, F32, P],
     "mjrl_gather_cg_z": [SP, C.POINTER(Rows), I64, C.POINTER(Scratch), P, P, F64, F32, P, P, P, P, P],
     "mjrl_cg_step_xr_p": [SP, P, P, P, P, P, P, P, P, F32, P],
+    "mjrl_cg_step1": [SP, P, F64, F32, P, P, P, P, P, P, P, P, P, F32, P],
     "mjrl_cg_init_vec": [I32, P, P, P, P, P, P, P],
     "mjrl_cg_update": [I32, P, P, P, P, P, P, F32, P],
     "mjrl_scale_vec": [P, I32, F64, P, P],

@@ -361,6 +361,78 @@ __global__ void __launch_bounds__(CGX_T) k_cgm_xrp_f(mjrl_shape s, float* __rest
     }
 }
 
+// A whole CG iteration after an all-reduced gradient sum (the sharded path) in ONE
+// launch: every workgroup forms z = gsum inv_T + c(sigma) p_ls + damping p on the
+// fly for all of d, folds p.z and then the new r.r in the same fixed order as
+// every other workgroup, and updates x, r (into r_out) and p of its own chunk;
+// the last workgroup to take the ticket records the CG scalars.  z itself is
+// never stored (cg_solve.py keeps it local too).
+__device__ __forceinline__ float cg_z(const mjrl_shape& s, const float* __restrict__ gsum, double inv_T,
+                                      float damping, const float* __restrict__ P_ls, const float* __restrict__ p,
+                                      int f) {
+    const float pf = p[f];
+    float hv;
+    const int ls0 = s.d - s.m;
+    if (f >= ls0) {
+        const float sg = expf(P_ls[f - ls0]);
+        const double uu = (double)sg * (double)sg;
+        const double c = 4.0 * uu * (2.0 * uu - 1e-8) / ((2.0 * uu + 1e-8) * (2.0 * uu + 1e-8));
+        hv = (float)(c * (double)pf);
+    } else {
+        hv = (float)((double)gsum[f] * inv_T);
+    }
+    return __fadd_rn(hv, __fmul_rn(damping, pf));   // hvp_flat + regu_coef * vector
+}
+
+__global__ void __launch_bounds__(CGX_T) k_cgm_step1(mjrl_shape s, const float* __restrict__ gsum, double inv_T,
+                                                     float damping, const float* __restrict__ packed_theta,
+                                                     float* __restrict__ x, const float* __restrict__ r,
+                                                     float* __restrict__ r_out, const float* __restrict__ p,
+                                                     float* __restrict__ p_out, float* __restrict__ packed_p,
+                                                     float* cg, int32_t* __restrict__ done, float tol) {
+    __shared__ double red[CGX_T / 64];
+    __shared__ unsigned ticket;
+    if (*done) return;
+    const int d = s.d;
+    const float* P_ls = packed_theta + Packed(s.h0, s.h1, s.np, s.mp).ls;
+    double acc = 0.0;
+#pragma unroll 4
+    for (int f = threadIdx.x; f < d; f += CGX_T) acc += (double)p[f] * (double)cg_z(s, gsum, inv_T, damping, P_ls, p, f);
+    const float pz = (float)block_sum<CGX_T>(acc, red);
+    const float rdotr = cg[0];
+    const float v = rdotr / pz;   // v = rdotr / p.z
+    acc = 0.0;
+#pragma unroll 4
+    for (int f = threadIdx.x; f < d; f += CGX_T) {
+        const float rf = __fsub_rn(r[f], __fmul_rn(v, cg_z(s, gsum, inv_T, damping, P_ls, p, f)));
+        acc += (double)rf * (double)rf;
+    }
+    const float rr = (float)block_sum<CGX_T>(acc, red);
+    const float mu = rr / rdotr;
+    const int f = blockIdx.x * CGX_T + threadIdx.x;
+    if (f < d) {   // own chunk; r and p go to the other buffer of their pair (all workgroups read r / p)
+        const float pf = p[f];
+        const float rf = __fsub_rn(r[f], __fmul_rn(v, cg_z(s, gsum, inv_T, damping, P_ls, p, f)));
+        x[f] = __fadd_rn(x[f], __fmul_rn(v, pf));
+        r_out[f] = rf;
+        const float pn = __fadd_rn(rf, __fmul_rn(mu, pf));
+        p_out[f] = pn;
+        pack_one(PackMap(s), f, pn, packed_p, false, 0.f);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) ticket = atomicAdd(reinterpret_cast<unsigned*>(cg + 8), 1u);
+    __syncthreads();
+    if (ticket == gridDim.x - 1 && threadIdx.x == 0) {
+        cg[4] = pz;
+        cg[2] = v;
+        cg[3] = mu;
+        cg[0] = rr;
+        cg[1] += 1.f;
+        if (rr < tol) *done = 1;   // cg_solve.py:19-20
+        *reinterpret_cast<unsigned*>(cg + 8) = 0u;
+    }
+}
+
 __global__ void __launch_bounds__(CGM_T) k_cgm_p(mjrl_shape s, const float* __restrict__ r, float* __restrict__ p,
                                                  float* __restrict__ packed_p, const float* cg,
                                                  const int32_t* __restrict__ done) {
@@ -602,6 +674,16 @@ int mjrl_cg_step(const mjrl_shape* s, const float* gsum, double inv_T, float dam
     hipLaunchKernelGGL(k_cgm_z, dim3(nwg), dim3(CGM_T), 0, st, *s, gsum, inv_T, damping, packed_theta, p, z, cg, done);
     hipLaunchKernelGGL(k_cgm_xr, dim3(nwg), dim3(CGM_T), 0, st, s->d, p, z, x, r, cg, done, residual_tol);
     hipLaunchKernelGGL(k_cgm_p, dim3(nwg), dim3(CGM_T), 0, st, *s, r, p, packed_p, cg, done);
+    return err(hipGetLastError());
+}
+
+int mjrl_cg_step1(const mjrl_shape* s, const float* gsum, double inv_T, float damping, const float* packed_theta,
+                  float* x, const float* r, float* r_out, const float* p, float* p_out, float* packed_p, float* cg,
+                  int32_t* done, float residual_tol, void* stream) {
+    if (!s || !gsum || !packed_theta || !x || !r || !r_out || !p || !p_out || !packed_p || !cg || !done) return MJRL_EINVAL;
+    if (r_out == r || p_out == p) return MJRL_EINVAL;
+    hipLaunchKernelGGL(k_cgm_step1, dim3((s->d + CGX_T - 1) / CGX_T), dim3(CGX_T), 0, (hipStream_t)stream, *s, gsum,
+                       inv_T, damping, packed_theta, x, r, r_out, p, p_out, packed_p, cg, done, residual_tol);
     return err(hipGetLastError());
 }
 

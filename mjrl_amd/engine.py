@@ -355,7 +355,7 @@ class UpdateEngine:
         self.packed_theta = torch.zeros(s.packed, **f32)
         self.packed_new = torch.zeros(s.packed, **f32)
         self.packed_p = torch.zeros(s.packed, **f32)
-        self.pvec = {k: torch.zeros(s.d, **f32) for k in ("g", "gsum", "x", "r", "r2", "p", "z", "theta_new")}
+        self.pvec = {k: torch.zeros(s.d, **f32) for k in ("g", "gsum", "x", "r", "r2", "p", "p2", "z", "theta_new")}
         self.cg = torch.zeros(_lib.CG_STATE, **f32)   # MJRL_CG_STATE
         self.done = torch.zeros(1, dtype=torch.int32, device=dev)
         self.out = torch.zeros(_lib.STEP_OUT, **f32)     # MJRL_STEP_OUT (results + step scratch)
@@ -750,11 +750,14 @@ class UpdateEngine:
                                    "mjrl_cg_step_xr_p")
                         continue
                     self.comm.allreduce_sum(v["gsum"])
-                    _lib.check(L.mjrl_cg_step(sp, _lib.ptr(v["gsum"]), inv_T_fvp, float(damping),
-                                              _lib.ptr(self.packed_theta),
-                                              _lib.ptr(v["x"]), _lib.ptr(v["r"]), _lib.ptr(v["p"]), _lib.ptr(v["z"]),
-                                              _lib.ptr(self.packed_p), _lib.ptr(self.cg), _lib.ptr(self.done),
-                                              float(residual_tol), st), "mjrl_cg_step")
+                    # the rest of the iteration in one launch; r and p alternate between two buffers each
+                    (r_in, r_out), (p_in, p_out) = ((v["r"], v["r2"]), (v["p"], v["p2"])) if k % 2 == 0 else \
+                        ((v["r2"], v["r"]), (v["p2"], v["p"]))
+                    _lib.check(L.mjrl_cg_step1(sp, _lib.ptr(v["gsum"]), inv_T_fvp, float(damping),
+                                               _lib.ptr(self.packed_theta), _lib.ptr(v["x"]), _lib.ptr(r_in),
+                                               _lib.ptr(r_out), _lib.ptr(p_in), _lib.ptr(p_out),
+                                               _lib.ptr(self.packed_p), _lib.ptr(self.cg), _lib.ptr(self.done),
+                                               float(residual_tol), st), "mjrl_cg_step1")
                 x = v["x"]
                 cg_iters_run = None
             timing[2].record()

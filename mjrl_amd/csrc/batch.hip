@@ -132,6 +132,94 @@ __global__ void __launch_bounds__(256) k_pack_split(const TO* __restrict__ obs, 
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < na; i += stride) act32[i] = (float)act[i];
 }
 
+// The same for f32 observations with n % 4 == 0 (the default staging of
+// train_step): lane l owns the column quads 4l + 256j, so each row is read with
+// 16-byte loads and written with 8-byte hi / lo stores, and the lane's
+// normalisation constants are loaded once per launch.  Same values as
+// k_pack_split (the same f32 operations per element).
+constexpr int PQ_MAXQ = 2;   // column quads per lane (np <= 512)
+__global__ void __launch_bounds__(256) k_pack_split_q(const float* __restrict__ obs, const float* __restrict__ act,
+                                                      int64_t T, int n, int m, int np,
+                                                      const float* __restrict__ in_shift,
+                                                      const float* __restrict__ in_scale, _Float16* __restrict__ xs,
+                                                      float* __restrict__ xu, float* __restrict__ act32) {
+    typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+    const int lane = threadIdx.x & 63;
+    const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const int nq = (np + 255) / 256;
+    float sh[PQ_MAXQ][4], den[PQ_MAXQ][4];
+#pragma unroll
+    for (int j = 0; j < PQ_MAXQ; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int ce = 4 * lane + 256 * j + e;
+            sh[j][e] = in_shift && ce < n ? in_shift[ce] : 0.f;
+            den[j][e] = in_shift && ce < n ? in_scale[ce] + 1e-8f : 1.f;
+        }
+    for (int64_t row = wid; row < T; row += nw) {
+        const float* src = obs + row * n;
+        float v[PQ_MAXQ][4];
+        float mx = 0.f;
+#pragma unroll
+        for (int j = 0; j < PQ_MAXQ; ++j) {
+            const int c = 4 * lane + 256 * j;
+            float d[4] = {0.f, 0.f, 0.f, 0.f};
+            if (j < nq) {
+                if (c + 3 < n) {
+                    const float4 q = *reinterpret_cast<const float4*>(src + c);
+                    d[0] = q.x; d[1] = q.y; d[2] = q.z; d[3] = q.w;
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (c + e < n) d[e] = src[c + e];
+                }
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int ce = c + e;
+                float x = 0.f;
+                if (j < nq) {
+                    if (ce < n) {
+                        x = d[e];
+                        if (in_shift) x = (x - sh[j][e]) / den[j][e];   // MuNet.forward:177
+                    } else if (ce == n) {
+                        x = 1.0f;                                    // bias column (zero padding after)
+                    }
+                }
+                v[j][e] = x;
+                mx = fmaxf(mx, fabsf(x));
+            }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+        float inv;
+        const float sc = pow2_scale(mx, inv);
+        _Float16* dst = xs + row * (2 * (int64_t)np);
+#pragma unroll
+        for (int j = 0; j < PQ_MAXQ; ++j) {
+            const int c = 4 * lane + 256 * j;
+            if (j < nq && c < np) {
+                half4 h, l;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float y = v[j][e] * sc;
+                    h[e] = (_Float16)y;
+                    l[e] = (_Float16)(y - (float)h[e]);
+                }
+                *reinterpret_cast<half4*>(dst + c) = h;
+                *reinterpret_cast<half4*>(dst + np + c) = l;
+            }
+        }
+        if (lane == 0) xu[row] = inv;
+    }
+    if (act32 != act) {
+        const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+        const int64_t na = (int64_t)T * m;
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < na; i += stride) act32[i] = act[i];
+    }
+}
+
 // One wave per path.  The path's rewards and baselines come into LDS with
 // coalesced loads, in windows of GW steps; lane 0 runs the serial fp64 chains out
 // of LDS (separate multiply and add, __dmul_rn / __dadd_rn cannot be contracted:
@@ -700,6 +788,13 @@ static int pack_batch_split(const TO* obs, const TO* act, int64_t T, const mjrl_
     if (s->np > 128 * PS_MAXP) return MJRL_ESHAPE;
     if (T == 0) return MJRL_OK;
     const int g = grid_for(T, 4, 8192);
+    if constexpr (sizeof(TO) == 4) {
+        if (s->n % 4 == 0 && (reinterpret_cast<uintptr_t>(obs) & 15) == 0 && s->np % 4 == 0 && s->np <= 256 * PQ_MAXQ) {
+            hipLaunchKernelGGL(k_pack_split_q, dim3(g), dim3(256), 0, (hipStream_t)stream, obs, act, T, s->n, s->m,
+                               s->np, in_shift, in_scale, (_Float16*)xs, xu, act32);
+            return err(hipGetLastError());
+        }
+    }
     hipLaunchKernelGGL(k_pack_split<TO>, dim3(g), dim3(256), 0, (hipStream_t)stream, obs, act, T, s->n, s->m, s->np,
                        in_shift, in_scale, (_Float16*)xs, xu, act32);
     return err(hipGetLastError());

@@ -583,3 +583,37 @@ def test_policy_mean_kernel_matches_cpu_forward():
         with torch.no_grad():
             ref = pol.model(torch.from_numpy(obs).float()).numpy()
         np.testing.assert_allclose(bp.means(obs), ref, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("n", [376, 252, 255])
+def test_pack_split_f32_input_matches_f64(n):
+    """mjrl_pack_batch_split_f32 (train_step's f32 staging; the 16-byte quad
+    kernel when n % 4 == 0) writes the same split rows, row scales and actions
+    as the f64-input pack of the same (f32-representable) values."""
+    from mjrl_amd.engine import UpdateEngine
+    rs = np.random.RandomState(n)
+    T, m = 1000, 17
+    obs = (rs.randn(T, n) * np.exp(rs.randn(n) * 2)).astype(np.float32)
+    act = rs.randn(T, m).astype(np.float32)
+    dev = torch.device("cuda:0")
+    for tf in (None, (rs.randn(n) * 0.1, rs.rand(n) + 0.5, rs.randn(m), rs.rand(m) + 0.5)):
+        outs = []
+        for dt in (torch.float64, torch.float32):
+            eng = UpdateEngine(n, m, (64, 64), device=dev)
+            assert eng.split
+            if tf is not None:
+                eng.set_transformations(*tf)
+            eng._ensure(T, 1)
+            o = torch.from_numpy(obs).to(dev, dt)
+            a = torch.from_numpy(act).to(dev, dt)
+            eng._pack(o, a, T, _lib_stream())
+            torch.cuda.synchronize()
+            outs.append([eng.ws[k][:T].cpu().clone() for k in ("xs", "xu", "act32")])
+        for x64, x32 in zip(*outs):
+            assert torch.equal(x64.view(torch.int16) if x64.dtype == torch.float16 else x64,
+                               x32.view(torch.int16) if x32.dtype == torch.float16 else x32)
+
+
+def _lib_stream():
+    from mjrl_amd import _lib
+    return _lib.stream_ptr()

@@ -452,6 +452,10 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
         }
         __syncthreads();
         KX_STAMP(0);
+        // EVAL: this tile's row-pass inputs into registers now (L2 hits since the
+        // previous tile's touch below), consumed after P3
+        RowPre<BT, MP, KT> rpre;
+        if constexpr (MODE == EVAL) row_pre_load<MODE, BT, MP, KT>(a, row_base, ltid, rpre);
         // pull the next tile's other per-row inputs into L2: one dword per 128-byte
         // line (FVP the a0 / a1 caches; FWD / EVAL actions, advantages and the old
         // means / log-likelihoods), kept alive in 2 VGPRs until the next publish
@@ -665,8 +669,16 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
         __syncthreads();
         KX_STAMP(4);
 
+        if (MODE == EVAL) {
+            // per-row pass: LR and KL, its inputs loaded at the top of the tile
+            row_pass<MODE, BT, MP, KT, false, true>(a, P + pk.ls, sls, row_base, GPf, L::LDG, racc0, racc1, ltid,
+                                                    &rpre);
+            __syncthreads();
+            KX_STAMP(5);
+            continue;
+        }
         if (MODE != FVP) {
-            // per-row pass: FWD log-lik / caches / VPG upstream; EVAL LR and KL
+            // per-row pass: FWD log-lik / caches / VPG upstream
             row_pass<MODE, BT, MP, KT, false>(a, P + pk.ls, sls, row_base, GPf, L::LDG, racc0, racc1, ltid);
             __syncthreads();
         KX_STAMP(5);

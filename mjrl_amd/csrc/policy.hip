@@ -113,10 +113,40 @@ __device__ __forceinline__ float ls_sum(const float* __restrict__ P_ls, int m) {
 //         past T); ll0 <- log-likelihood; acc0 += adv (z^2 - 1) (log-std VPG, action j).
 //   EVAL: acc0 += exp(LL_new - LL_old) adv, acc1 += KL(old || new) (lanes j = 0).
 // The per-thread partials are folded once per launch by row_pass_final.
-template <int MODE, int BT, int MP, int NT, bool STORE_GP>
+// The per-row inputs of row_pass (actions, old means, old log-likelihoods,
+// advantages) for this thread's elements, loaded ahead of the pass by a caller
+// with registers to spare (the EVAL pass of k_kx loads them at the top of the
+// tile, so the row pass no longer waits on them).
+template <int BT, int MP, int NT>
+struct RowPre {
+    static constexpr int NE = BT * MP;
+    static constexpr int PER = NE >= NT ? NE / NT : 1;
+    float av[PER], mo[PER], l0[PER], ad[PER];
+};
+
+template <int MODE, int BT, int MP, int NT>
+__device__ __forceinline__ void row_pre_load(const RowArgs& a, int64_t row_base, int tid, RowPre<BT, MP, NT>& pre) {
+    using R = RowPre<BT, MP, NT>;
+    const int m = a.m;
+    const int64_t T = a.T;
+    const int j = tid % MP;
+#pragma unroll
+    for (int u = 0; u < R::PER; ++u) {
+        const bool in = R::NE >= NT || tid + u * NT < R::NE;
+        const int row = in ? (tid + u * NT) / MP : 0;
+        const int64_t gr = in ? row_base + row : T;
+        const bool valid = gr < T && j < m;
+        pre.av[u] = valid ? a.act[gr * m + j] : 0.f;
+        pre.mo[u] = MODE == EVAL && valid ? a.mu0[gr * m + j] : 0.f;
+        pre.l0[u] = MODE == EVAL && j == 0 && gr < T ? a.ll0[gr] : 0.f;
+        pre.ad[u] = gr < T ? (MODE == FWD ? a.adv_vpg[gr] : (j == 0 ? a.adv[gr] : 0.f)) : 0.f;
+    }
+}
+
+template <int MODE, int BT, int MP, int NT, bool STORE_GP, bool PRE = false>
 __device__ __forceinline__ void row_pass(const RowArgs& a, const float* __restrict__ P_ls, float sls,
                                          int64_t row_base, float* GPs, int ldp, double& acc0, double& acc1,
-                                         int tid) {
+                                         int tid, const RowPre<BT, MP, NT>* pre = nullptr) {
     constexpr int NE = BT * MP;                        // (row, action) elements of the tile
     constexpr int PER = NE >= NT ? NE / NT : 1;        // more threads than elements: the rest idle
     static_assert(NT % MP == 0 && (NE >= NT ? PER * NT == NE : NT % NE == 0) && MP <= 64, "row lanes in one wave");
@@ -141,10 +171,10 @@ __device__ __forceinline__ void row_pass(const RowArgs& a, const float* __restri
         const bool valid = gr < T && act_j;
         float* g = GPs + row * ldp + j;
         const float mu = in ? *g : 0.f;
-        const float av = valid ? a.act[gr * m + j] : 0.f;
+        const float av = PRE ? pre->av[u] : (valid ? a.act[gr * m + j] : 0.f);
         float mo = 0.f, adv = 0.f;
-        if (MODE == EVAL) mo = valid ? a.mu0[gr * m + j] : 0.f;
-        if (MODE == FWD) adv = gr < T ? a.adv_vpg[gr] : 0.f;
+        if (MODE == EVAL) mo = PRE ? pre->mo[u] : (valid ? a.mu0[gr * m + j] : 0.f);
+        if (MODE == FWD) adv = PRE ? pre->ad[u] : (gr < T ? a.adv_vpg[gr] : 0.f);
         const float zs = valid ? (av - mu) / sn : 0.f;
         float z2 = zs * zs;
         float kl = 0.f;
@@ -172,8 +202,8 @@ __device__ __forceinline__ void row_pass(const RowArgs& a, const float* __restri
             if (MODE == FWD) {
                 a.ll0[gr] = ll;
             } else {
-                const float lr = expf(ll - a.ll0[gr]);
-                acc0 += (double)(lr * a.adv[gr]);
+                const float lr = expf(ll - (PRE ? pre->l0[u] : a.ll0[gr]));
+                acc0 += (double)(lr * (PRE ? pre->ad[u] : a.adv[gr]));
                 acc1 += (double)kl;
             }
         }

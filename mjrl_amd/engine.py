@@ -414,7 +414,17 @@ class UpdateEngine:
         if (ins is None) != (isc is None):   # the kernel needs both; defaults are 0 / 1
             ins = ins if ins is not None else torch.zeros(self.shape.n, dtype=torch.float32, device=self.device)
             isc = isc if isc is not None else torch.ones(self.shape.n, dtype=torch.float32, device=self.device)
-        self.transforms = (ins, isc, dv(out_shift), dv(out_scale))
+        new = (ins, isc, dv(out_shift), dv(out_scale))
+        # the same device buffers when the set of given vectors is unchanged (the
+        # agents re-apply the policy's transformations before every update): stable
+        # addresses keep a captured update graph valid
+        old = self.transforms
+        if all((a is None) == (b is None) and (a is None or a.shape == b.shape) for a, b in zip(old, new)):
+            for a, b in zip(old, new):
+                if a is not None:
+                    a.copy_(b)
+            return
+        self.transforms = new
 
     def _ensure(self, T_all, P):
         if T_all <= self.cap_T and P <= self.cap_P:

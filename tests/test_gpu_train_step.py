@@ -138,3 +138,32 @@ def test_train_step_two_ranks_equals_one():
         assert nrel(g0, single[it]["g"]) < 1e-5
         assert nrel(th0, single[it]["theta"]) < 1e-5, nrel(th0, single[it]["theta"])
         np.testing.assert_allclose(c0, single[it]["coeffs"], rtol=1e-6, atol=1e-9)
+
+
+def test_train_from_paths_graph_replay_bitwise():
+    """Three train_from_paths iterations with the same path lengths: the engine
+    captures the update on the second (graphs = "auto", 6k rows) and replays it on
+    the third; the parameters stay bit-identical to an agent running every update
+    eagerly (staging buffers and transformation buffers keep their addresses)."""
+    import copy
+    from mjrl_amd.algos.npg_cg import NPG
+    from mjrl_amd.baselines.zero_baseline import ZeroBaseline
+    from mjrl_amd.policies.gaussian_mlp import MLP
+    from mjrl_amd.utils.gym_env import EnvSpec
+    spec = EnvSpec(N_OBS, N_ACT, 100, 1)
+    agents = []
+    for graphs in ("auto", False):
+        pol = MLP(spec, hidden_sizes=(64, 64), seed=1)
+        pol.model.set_transformations(np.full(N_OBS, 0.1), np.full(N_OBS, 2.0), np.zeros(N_ACT), np.ones(N_ACT))
+        ag = NPG(_Env(), pol, ZeroBaseline(spec), normalized_step_size=0.05, device="cuda:0")
+        ag.engine().graphs = graphs
+        agents.append(ag)
+    for it in range(3):
+        rs = np.random.RandomState(it)
+        paths = [dict(observations=rs.randn(100, N_OBS), actions=rs.randn(100, N_ACT), rewards=rs.randn(100),
+                      advantages=rs.randn(100), terminated=False) for _ in range(60)]
+        for ag in agents:
+            ag.train_from_paths(copy.deepcopy(paths))
+    assert agents[0].engine()._gstate.get("graph") is not None
+    assert agents[1].engine()._gstate.get("graph") is None
+    np.testing.assert_array_equal(agents[0].policy.get_param_values(), agents[1].policy.get_param_values())

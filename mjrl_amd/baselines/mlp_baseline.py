@@ -113,6 +113,23 @@ class MLPBaseline:
             sd["step"].copy_(torch.as_tensor(float(sc["step"])))
             sd["exp_avg"].copy_(sc["exp_avg"])
             sd["exp_avg_sq"].copy_(sc["exp_avg_sq"])
+        st["cpu_key"] = self._cpu_key()
+        return st
+
+    def _cpu_key(self):
+        """Identity of the CPU parameters' current contents: their storage (a
+        `param.data = ...` assignment changes it) and the parameters' version
+        counters (in-place updates through the parameter, e.g. an optimizer
+        step).  Edits through `param.data.<op>_()` bypass the counter and are not
+        seen."""
+        return tuple((p.data_ptr(), p._version) for p in self.model.parameters())
+
+    def _predict_state(self):
+        """The device mirror for a forward: re-copied when the CPU parameters
+        changed since the last copy (a caller may set them directly)."""
+        st = self._dev
+        if st is None or st.get("cpu_key") != self._cpu_key():
+            st = self._to_device()
         return st
 
     def _from_device(self, st):
@@ -120,6 +137,7 @@ class MLPBaseline:
         with torch.no_grad():
             for pd, pc in zip(model.parameters(), self.model.parameters()):
                 pc.data.copy_(pd.detach().cpu())
+        st["cpu_key"] = self._cpu_key()
         for pd, pc in zip(model.parameters(), self.model.parameters()):
             sd = opt.state.get(pd)
             if not sd:
@@ -290,7 +308,7 @@ class MLPBaseline:
         """predict for every row of a staged batch at once: obs (device, [T][n]
         RL rows first), path_off (device i64 [P+1]), lengths (host [P]) -> f64
         device [T].  Features as _features (f64, then f32), one forward."""
-        st = self._dev if self._dev is not None else self._to_device()
+        st = self._predict_state()
         dev = st["device"]
         T = int(np.sum(lengths))
         o = obs[:T].to(torch.float64).clamp(-10.0, 10.0) / 10.0
@@ -305,7 +323,7 @@ class MLPBaseline:
         when one is visible, else on the CPU model)."""
         feat = self._features([path]).astype("float32")
         if torch.cuda.is_available():
-            st = self._dev if self._dev is not None else self._to_device()
+            st = self._predict_state()
             with torch.no_grad():
                 return st["model"](torch.from_numpy(feat).to(st["device"])).cpu().numpy().ravel()
         with torch.no_grad():

@@ -215,3 +215,20 @@ def test_mlp_baseline_mirror_matches_reference_init_and_leaves_env_alone():
     np.testing.assert_array_equal(f[:, 5:], np.stack([t, t ** 2, t ** 3, t ** 4], 1))
     clone = pickle.loads(pickle.dumps(b))
     assert all(torch.equal(a, c) for a, c in zip(clone.model.parameters(), b.model.parameters()))
+
+
+def test_mlp_baseline_device_mirror_tracks_cpu_parameters():
+    """MLPBaseline's staleness key changes when the CPU parameters are replaced
+    or modified in place, so a forward re-copies them to the device."""
+    from mjrl_amd.baselines.mlp_baseline import MLPBaseline
+    from mjrl_amd.utils.gym_env import EnvSpec
+    b = MLPBaseline(EnvSpec(4, 1, 10, 1))
+    k0 = b._cpu_key()
+    with torch.no_grad():
+        next(b.model.parameters()).add_(1.0)
+    k1 = b._cpu_key()
+    assert k1 != k0
+    p = next(b.model.parameters())
+    p.data = p.data.clone()
+    assert b._cpu_key() != k1
+    assert b._cpu_key() == b._cpu_key()

@@ -398,6 +398,11 @@ def main():
     run_case("c3_halfcheetah_trpo", n=17, m=6, hidden=(128, 128),
              lengths=[1000] * 10, terminated=[False] * 10, algo="trpo",
              algo_kwargs=dict(kl_dist=0.01))
+    # C3f: the HalfCheetah TRPO config at its full bench size (100 x 1000 rows,
+    # BASELINE configs[2]); inputs regenerated from the seed, outputs only
+    run_case("c3_halfcheetah_full", n=17, m=6, hidden=(128, 128),
+             lengths=[1000] * 100, terminated=[False] * 100, algo="trpo",
+             algo_kwargs=dict(kl_dist=0.01), regen=True, seed=131)
     # C3b: TRPO with a step large enough that the line search backtracks
     run_case("c3_trpo_backtrack", n=17, m=6, hidden=(128, 128),
              lengths=[300] * 4, terminated=[False] * 4, algo="trpo",

@@ -422,6 +422,11 @@ def main():
              lengths=[200] * 10, terminated=[False] * 10, algo="dapg",
              algo_kwargs=dict(), demo=[200] * 5, transforms=transforms,
              log_std=np.linspace(-1.0, 0.0, m))
+    # C5f: the door DAPG config at its full bench size (200 x 200 rows + 25 demos)
+    run_case("c5_door_full", n=n, m=m, hidden=(256, 256),
+             lengths=[200] * 200, terminated=[False] * 200, algo="dapg",
+             algo_kwargs=dict(), demo=[200] * 25, transforms=transforms,
+             log_std=np.linspace(-1.0, 0.0, m), regen=True, seed=151)
 
 
 def baselines_case():

@@ -320,6 +320,8 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
         wq3 = os3 * os3 * (2.f / (2.f * sg * sg + 1e-8f));
     }
     const float sls = MODE == FVP ? 0.f : ls_sum(P + pk.ls, m);
+    RowConst rconst{};
+    if constexpr (MODE != FVP) rconst = row_const<MODE, MP>(a, P + pk.ls, tid);
     half8 wh[KS], wl[KS];
     float wsc;
     {
@@ -379,7 +381,15 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
     float4 xn[L::XPER];
     float un = 1.f;
     // pieces u0 .. u1 - 1 (callers split the loads over two phases so the vector
-    // memory issue of the 48 KB tile does not stall one phase)
+    // memory issue of the 48 KB tile does not stall one phase).  The vector-memory
+    // counter is in order, so a load under a branch makes the compiler's wait for
+    // any EARLIER load conservative (vmcnt(0)-like): the loads whose values are
+    // waited for inside a tile (the FVP's cached activations, EVAL's row-pass
+    // inputs, the L2 touch) are unconditional from clamped addresses, and the
+    // conditional xhat loads of the next tile come before them (EVAL) or after
+    // their last use (FWD / FVP: P4 / P5); a rejected variant with unconditional
+    // xhat loads made the compiler copy them between registers right after issue,
+    // waiting on HBM there.
     auto xload = [&](int64_t t_, int tid_, int u0 = 0, int u1 = L::XPER) {
         const int64_t rb_ = t_ * BT;
         const int row = tid_ >> 4, c16 = tid_ & 15;
@@ -389,7 +399,12 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
         for (int u = 0; u < L::XPER; ++u)
             if (u >= u0 && u < u1)
                 xn[u] = ok ? *reinterpret_cast<const float4*>(src + 16 * (c16 + 16 * u)) : make_float4(0.f, 0.f, 0.f, 0.f);
-        if (u0 == 0) un = (tid_ < BT && t_ < ntiles && rb_ + tid_ < T) ? a.xu[rb_ + tid_] : 1.f;
+        if (u0 == 0) {
+            // rows past T take row 0's scale (finite; their xhat and gradient rows are
+            // zero), without a select whose wait the compiler would hoist
+            const bool uok = tid_ < BT && t_ < ntiles && rb_ + tid_ < T;
+            un = a.xu[uok ? rb_ + tid_ : 0];
+        }
     };
     xload(blockIdx.x, tid);
     __syncthreads();   // images and scales ready
@@ -441,13 +456,20 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
             }
             if (ltid < BT) Us[ltid] = un;
         }
+        // EVAL has no weight-gradient phase: the next tile's xhat loads go right
+        // after the publish, before this tile's unconditional row-pass loads
+        if (MODE == EVAL) xload(tile + gridDim.x, ltid);
         float pa0[4], pa1[4];   // FVP: cached a0 / a1 at (rows kh*16 + 4q + rr, unit cb*16 + r)
         if (MODE == FVP) {
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr) {
                 const int row = kh * 16 + 4 * lq + rr;
-                pa0[rr] = row < nrow ? a.a0[(row_base + row) * H + cb * 16 + lr16] : 0.f;
-                pa1[rr] = row < nrow ? a.a1[(row_base + row) * H + cb * 16 + lr16] : 0.f;
+                // rows past T read row 0 of the tile instead of zero: finite values whose
+                // output-layer weights are masked to zero (gp), so they add nothing, and
+                // no select pulls the wait for these L2 loads to the top of P1
+                const int64_t gi = (row_base + (row < nrow ? row : 0)) * H + cb * 16 + lr16;
+                pa0[rr] = a.a0[gi];
+                pa1[rr] = a.a1[gi];
             }
         }
         __syncthreads();
@@ -482,7 +504,9 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
                         p = a.ll0 + nb;
                     }
                 }
-                if (p) touch[0] = *p;
+                touch[0] = *(p ? p : reinterpret_cast<const float*>(a.xs));   // unconditional (see xload)
+            } else {
+                touch[0] = *reinterpret_cast<const float*>(a.xs);
             }
         }
 
@@ -527,9 +551,6 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
                 D0[((1 - kh) * 16 + 4 * lq + rr) * L::LD + cb * 16 + lr16] = kh ? acc1[0][rr] : acc1[1][rr];
             __syncthreads();
             KX_STAMP(1);
-            // EVAL has no weight-gradient phase: the next tile's xhat loads go here,
-            // after the first layer's image reads
-            if (MODE == EVAL) xload(tile + gridDim.x, ltid);
             {
                 const int col = cb * 16 + lr16;
                 float av[4];
@@ -672,14 +693,15 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
         if (MODE == EVAL) {
             // per-row pass: LR and KL, its inputs loaded at the top of the tile
             row_pass<MODE, BT, MP, KT, false, true>(a, P + pk.ls, sls, row_base, GPf, L::LDG, racc0, racc1, ltid,
-                                                    &rpre);
+                                                    &rpre, &rconst);
             __syncthreads();
             KX_STAMP(5);
             continue;
         }
         if (MODE != FVP) {
             // per-row pass: FWD log-lik / caches / VPG upstream
-            row_pass<MODE, BT, MP, KT, false>(a, P + pk.ls, sls, row_base, GPf, L::LDG, racc0, racc1, ltid);
+            row_pass<MODE, BT, MP, KT, false>(a, P + pk.ls, sls, row_base, GPf, L::LDG, racc0, racc1, ltid,
+                                              nullptr, &rconst);
             __syncthreads();
         KX_STAMP(5);
             if (MODE == EVAL) continue;

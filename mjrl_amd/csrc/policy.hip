@@ -130,23 +130,56 @@ __device__ __forceinline__ void row_pre_load(const RowArgs& a, int64_t row_base,
     const int m = a.m;
     const int64_t T = a.T;
     const int j = tid % MP;
+    // unconditional loads from clamped indices, no selects: row_pass reads an element
+    // only where it is valid (gr < T, j < m; j == 0 for the per-row values), and a
+    // load under a branch would make every later vmcnt wait conservative (it waited
+    // for the next tile's xhat loads)
+    const int jc = j < m ? j : 0;
 #pragma unroll
     for (int u = 0; u < R::PER; ++u) {
         const bool in = R::NE >= NT || tid + u * NT < R::NE;
         const int row = in ? (tid + u * NT) / MP : 0;
         const int64_t gr = in ? row_base + row : T;
-        const bool valid = gr < T && j < m;
-        pre.av[u] = valid ? a.act[gr * m + j] : 0.f;
-        pre.mo[u] = MODE == EVAL && valid ? a.mu0[gr * m + j] : 0.f;
-        pre.l0[u] = MODE == EVAL && j == 0 && gr < T ? a.ll0[gr] : 0.f;
-        pre.ad[u] = gr < T ? (MODE == FWD ? a.adv_vpg[gr] : (j == 0 ? a.adv[gr] : 0.f)) : 0.f;
+        const int64_t gc = gr < T ? gr : T - 1;
+        pre.av[u] = a.act[gc * m + jc];
+        pre.mo[u] = MODE == EVAL ? a.mu0[gc * m + jc] : 0.f;
+        pre.l0[u] = MODE == EVAL ? a.ll0[gc] : 0.f;
+        pre.ad[u] = MODE == FWD ? a.adv_vpg[gc] : a.adv[gc];
     }
+}
+
+// The row pass's per-launch constants of this thread's action j (log-stds, out_scale),
+// loaded once before the tile loop by callers that keep them in registers: a
+// per-tile load would make the row pass wait (in-order vmcnt) on every global load
+// issued before it, the next tile's xhat prefetch included.
+struct RowConst {
+    float lsn, sn, os, lso, so;
+};
+
+template <int MODE, int MP>
+__device__ __forceinline__ RowConst row_const(const RowArgs& a, const float* __restrict__ P_ls, int tid) {
+    const int j = tid % MP;
+    const bool act_j = j < a.m;
+    RowConst c;
+    c.lsn = act_j ? P_ls[j] : 0.f;
+    c.sn = expf(c.lsn);
+    c.os = 1.f;
+    c.lso = 0.f;
+    c.so = 1.f;
+    if (MODE == FWD) {
+        if (a.out_scale && act_j) c.os = a.out_scale[j];
+    } else {
+        c.lso = act_j ? a.V[(P_ls - a.P) + j] : 0.f;
+        c.so = expf(c.lso);
+    }
+    return c;
 }
 
 template <int MODE, int BT, int MP, int NT, bool STORE_GP, bool PRE = false>
 __device__ __forceinline__ void row_pass(const RowArgs& a, const float* __restrict__ P_ls, float sls,
                                          int64_t row_base, float* GPs, int ldp, double& acc0, double& acc1,
-                                         int tid, const RowPre<BT, MP, NT>* pre = nullptr) {
+                                         int tid, const RowPre<BT, MP, NT>* pre = nullptr,
+                                         const RowConst* rc = nullptr) {
     constexpr int NE = BT * MP;                        // (row, action) elements of the tile
     constexpr int PER = NE >= NT ? NE / NT : 1;        // more threads than elements: the rest idle
     static_assert(NT % MP == 0 && (NE >= NT ? PER * NT == NE : NT % NE == 0) && MP <= 64, "row lanes in one wave");
@@ -154,15 +187,8 @@ __device__ __forceinline__ void row_pass(const RowArgs& a, const float* __restri
     const int64_t T = a.T;
     const int j = tid % MP;
     const bool act_j = j < m;
-    const float lsn = act_j ? P_ls[j] : 0.f;
-    const float sn = expf(lsn);
-    float os = 1.f, lso = 0.f, so = 1.f;
-    if (MODE == FWD) {
-        if (a.out_scale && act_j) os = a.out_scale[j];
-    } else {
-        lso = act_j ? a.V[(P_ls - a.P) + j] : 0.f;
-        so = expf(lso);
-    }
+    const RowConst c = rc ? *rc : row_const<MODE, MP>(a, P_ls, tid);
+    const float lsn = c.lsn, sn = c.sn, os = c.os, lso = c.lso, so = c.so;
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
         const bool in = NE >= NT || tid + u * NT < NE;

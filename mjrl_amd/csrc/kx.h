@@ -736,6 +736,30 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
             }
             *reinterpret_cast<float4*>(G1T + hcol * L::LDT + kh * 16 + 4 * lq) = make_float4(gv[0], gv[1], gv[2], gv[3]);
         }
+        // the gW2 sums (gW2[jb = w >> 2][kb = w & 3] += gp^T a1; gb2 = row sums of gp on
+        // waves kb = 0): FVP runs them beside P4, off P5's chain (GPT is complete since
+        // P3); FWD in P5 (its GPT is transposed right before P4, without a barrier)
+        auto gw2_sum = [&]() __attribute__((always_inline)) {
+            half8 gh, gl;
+            float s4[4];
+            if ((w >> 2) < MP / 16) {
+                const float8v v = load8(GPT + ((w >> 2) * 16 + lr16) * L::LDT + 8 * lq);
+                float inv;
+                const float sc = pow2_scale(max_over_groups(absmax8(v)), inv);
+                split8(v, sc, gh, gl);
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) s4[rr] = __shfl(inv, 4 * lq + rr, 64);
+                if ((w & 3) == 0) {
+                    b2acc += sum_over_groups(((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7])));
+                }
+                half8 bh, bl;
+                acol(A1i, (w & 3) * 16 + lr16, lq, bh, bl);
+                const floatx4 t = mfma_x3(gh, gl, bh, bl, zero4());
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) g2[rr] += t[rr] * s4[rr];
+            }
+        };
+        if (MODE == FVP) gw2_sum();
         __syncthreads();
         KX_STAMP(6);
         // ---- P5: gu0 = (1 - a0^2) (gu1 W1), times the xhat row scale; beside it the
@@ -790,28 +814,12 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) g1[jj][rr] += t[rr] * s4[rr];
             }
-            // gW2[jb = w >> 2][kb = w & 3] += gp^T a1;  gb2 = row sums of gp (waves kb = 0)
-            if ((w >> 2) < MP / 16) {
-                const float8v v = load8(GPT + ((w >> 2) * 16 + lr16) * L::LDT + 8 * lq);
-                float inv;
-                const float sc = pow2_scale(max_over_groups(absmax8(v)), inv);
-                split8(v, sc, gh, gl);
-#pragma unroll
-                for (int rr = 0; rr < 4; ++rr) s4[rr] = __shfl(inv, 4 * lq + rr, 64);
-                if ((w & 3) == 0) {
-                    b2acc += sum_over_groups(((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7])));
-                }
-                half8 bh, bl;
-                acol(A1i, (w & 3) * 16 + lr16, lq, bh, bl);
-                const floatx4 t = mfma_x3(gh, gl, bh, bl, zero4());
-#pragma unroll
-                for (int rr = 0; rr < 4; ++rr) g2[rr] += t[rr] * s4[rr];
-            }
         };
         // (running the two halves in opposite orders on the two waves of a SIMD,
         // kh = 0 / 1, measured 0.5 %: the phase is issue-bound, not latency-bound)
         p5_gu0();
         p5_gw();
+        if (MODE != FVP) gw2_sum();
         __syncthreads();
         KX_STAMP(7);
 

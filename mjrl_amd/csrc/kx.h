@@ -26,7 +26,7 @@
 // phase profile (debug builds): wave 0 of block 0 accumulates s_memtime cycles
 // between stamps in (wave-uniform, scalar) registers, written once at the end;
 // read with mjrl_debug_kx_prof
-constexpr int KX_NPROF = 18;   // 0-14 phases, 15 launch preamble, 16 tail (slab writes), 17 launches
+constexpr int KX_NPROF = 24;   // 0-14 phases, 15 launch preamble, 16 tail (slab writes), 17 launches, 18-23 preamble parts
 __device__ unsigned long long g_kx_prof[KX_NPROF];
 #define KX_STAMP(i)                                                     \
     do {                                                                \
@@ -34,7 +34,11 @@ __device__ unsigned long long g_kx_prof[KX_NPROF];
         kx_acc_[i] += now_ - kx_last_;                                  \
         kx_last_ = now_;                                                \
     } while (0)
+#define KX_PRE(i) kx_pre_[i] = __builtin_amdgcn_s_memtime()
 #else
+#define KX_PRE(i) \
+    do {          \
+    } while (0)
 #define KX_STAMP(i) \
     do {            \
     } while (0)
@@ -283,6 +287,7 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
     if (MODE == FVP && a.done && *a.done) return;
 #ifdef MJRL_KX_PROF
     const unsigned long long kx_t0_ = __builtin_amdgcn_s_memtime();
+    unsigned long long kx_pre_[6];
 #endif
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int r16 = lane & 15, q = lane >> 4;
@@ -322,6 +327,7 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
     const float sls = MODE == FVP ? 0.f : ls_sum(P + pk.ls, m);
     RowConst rconst{};
     if constexpr (MODE != FVP) rconst = row_const<MODE, MP>(a, P + pk.ls, tid);
+    KX_PRE(0);
     half8 wh[KS], wl[KS];
     float wsc;
     {
@@ -335,6 +341,7 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
 #pragma unroll
         for (int s = 0; s < KS; ++s) split8(v[s], sc, wh[s], wl[s]);
     }
+    KX_PRE(1);
     {
         float* red1 = D0;          // [8][64] column-max partials (D0 / D0B are free until P1)
         float* red3 = D0 + 512;
@@ -348,11 +355,13 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
             wscale<false>(w4v, sc4v, nullptr, tid);
         }
         __syncthreads();
+        KX_PRE(2);
         if (MODE != EVAL) {
             wscale_cols(sc1, red1, tid);
             wscale_cols(sc3, red3, tid);
             __syncthreads();
         }
+        KX_PRE(3);
         if (MODE == EVAL) {
             wstore<false>(w1v, S1, L::WIMG, sc1, tid);
             wstore<false>(w3v, S3, L::WIMG2, sc3, tid);
@@ -363,6 +372,7 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
             wstore<false>(w4v, S4, L::WIMG2, sc4v, tid);
         }
     }
+    KX_PRE(4);
 
     floatx4 g0[KG];
 #pragma unroll
@@ -413,6 +423,9 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
     unsigned long long kx_last_ = __builtin_amdgcn_s_memtime();
     kx_acc_[15] = kx_last_ - kx_t0_;
     kx_acc_[17] = 1;
+    kx_acc_[18] = kx_pre_[0] - kx_t0_;
+    for (int i = 1; i < 5; ++i) kx_acc_[18 + i] = kx_pre_[i] - kx_pre_[i - 1];
+    kx_acc_[23] = kx_last_ - kx_pre_[4];
 #endif
 
     // FVP: P1's partials carry the W1c column scale of their unit (both powers of two:

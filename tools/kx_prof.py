@@ -20,7 +20,7 @@ NAMES = ["publish", "P1 first layer", "P1 fold", "P2", "P3", "row pass", "P4", "
          "P6 xload", "P6 G0 split", "P6 gW0", "P6 gW1", "P6 gW2+bias"]
 
 
-NPROF = 18
+NPROF = 24
 
 
 def read(lib):
@@ -63,7 +63,8 @@ def main(T=1000000):
         print("%-16s" % n + "".join("%10.0f" % (r[i] / tiles) for r in res.values()))
     print("%-16s" % "total" + "".join("%10.0f" % (r[:15].sum() / tiles) for r in res.values()))
     print("per launch (cycles, workgroup 0):")
-    for i, n in ((15, "preamble"), (16, "tail")):
+    for i, n in ((15, "preamble"), (18, " loads issued"), (19, " W0 slice split"), (20, " row scales+bar"),
+                 (21, " col scales+bar"), (22, " image stores"), (23, " xhat load+bar"), (16, "tail")):
         print("%-16s" % n + "".join("%10.0f" % (r[i] / max(r[17], 1)) for r in res.values()))
     print("%-16s" % "tile loop" + "".join("%10.0f" % (r[:15].sum() / max(r[17], 1)) for r in res.values()))
 

@@ -289,7 +289,10 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
     const unsigned long long kx_t0_ = __builtin_amdgcn_s_memtime();
     unsigned long long kx_pre_[6];
 #endif
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    // the wave index in an SGPR (readfirstlane): cb / kh and every address term and
+    // branch condition derived from them are scalar, not per-lane VALU work and
+    // exec-mask branches
+    const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r16 = lane & 15, q = lane >> 4;
     const int cb = w & 3, kh = w >> 2;
     const int m = a.m;
@@ -451,9 +454,14 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
         KX_STAMP(9);   // loop top (the wait on the previous tile's last barrier)
         // per-lane indices through an opaque zero: recomputed per tile rather than
         // hoisted into live registers (see ks.h)
+        // (FVP keeps its lane indices r16 / q in registers at the cost of 8 spilled
+        // VGPRs: 220 fewer VALU per tile, FVP 896 -> 867 us in rocprofv3; FWD
+        // spills 19 that way and is 5 % slower, so it recomputes them; EVAL has the
+        // registers to keep all three; profiles/r02s/ab_lane_index.txt)
         int opq = 0;
-        asm volatile("" : "+v"(opq));
-        const int ltid = tid + opq, lr16 = r16 + opq, lq = q + opq;
+        if constexpr (MODE != EVAL) asm volatile("" : "+v"(opq));
+        constexpr int OPQ_LANE = MODE == FWD ? 1 : 0;
+        const int ltid = tid + opq, lr16 = r16 + OPQ_LANE * opq, lq = q + OPQ_LANE * opq;
         const int64_t row_base = tile * BT;
         const int nrow = (int)(T - row_base < BT ? T - row_base : BT);
 

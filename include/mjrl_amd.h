@@ -62,15 +62,20 @@ typedef struct mjrl_rows {
     float* gu1;               /* [T][h1] per-row upstream gradient at layer 1 */
     float* gp;                /* [T][mp] per-row upstream gradient at the output */
     /* Split-f16 observation rows (alternative to xhat, MLP(64,64) with np % 128 == 0,
-     * see mjrl_split_supported): row t = [hi np][lo np] f16 of y = xhat[t] / xu[t],
-     * hi = f16(y), lo = f16(y - hi); xu[t] a power of two with |y| < 1.
-     * When xs is non-null the policy passes read xs / xu and ignore xhat. */
+     * see mjrl_split_supported): row t = [hi np][lo np] f16 of
+     * y[t][k] = xhat[t][k] / (xc[k] xu[t]), hi = f16(y), lo = f16(y - hi);
+     * xc[k] a power of two per column (mjrl_obs_colscale), xu[t] a power of two per
+     * row with max_k |y[t][k]| in [2^14, 2^15).  Element bound:
+     * |xc xu (hi + lo) - xhat| <= 2^-23 |xhat| + 2^-38 colmax_k, colmax_k the
+     * column's max |xhat| over the batch.
+     * When xs is non-null the policy passes read xs / xu / xc and ignore xhat. */
     const void* xs;           /* [T][2][np] f16 */
     const float* xu;          /* [T] */
+    const float* xc;          /* [np] */
 } mjrl_rows;
 
 /* Scratch the caller allocates once per (shape, T) — sizes from
- * mjrl_scratch_floats(). */
+ * mjrl_scratch_size(). */
 typedef struct mjrl_scratch {
     float* wpart;             /* weight-gradient partial slabs */
     double* rpart;            /* per-workgroup scalar partials */
@@ -93,12 +98,20 @@ int mjrl_pack_batch(const double* obs, const double* act, int64_t T, const mjrl_
                     const float* in_shift, const float* in_scale, float* xhat, float* act32,
                     void* stream);
 
-/* Same batch assembly into the split-f16 form of mjrl_rows.xs / xu (one wave per
- * row: the row's max |xhat| picks xu[t] = 2^E, then hi / lo as described there).
- * Only for shapes with mjrl_split_supported(s). */
+/* Column scales of the split form: xc[k] = 2^E with max_t |xhat[t][k]| 2^-E in
+ * [1/2, 1) (1 for an all-zero column; the bias column's max is 1).  One pass over
+ * the observations (xhat computed as mjrl_pack_batch does); xc holds np floats. */
+int mjrl_obs_colscale(const double* obs, int64_t T, const mjrl_shape* s, const float* in_shift,
+                      const float* in_scale, float* xc, void* stream);
+int mjrl_obs_colscale_f32(const float* obs, int64_t T, const mjrl_shape* s, const float* in_shift,
+                          const float* in_scale, float* xc, void* stream);
+/* Same batch assembly into the split-f16 form of mjrl_rows.xs / xu, given the
+ * column scales xc of mjrl_obs_colscale (one wave per row: the row's max
+ * |xhat / xc| picks xu[t], then hi / lo as described at mjrl_rows).  Only for
+ * shapes with mjrl_split_supported(s). */
 int mjrl_pack_batch_split(const double* obs, const double* act, int64_t T, const mjrl_shape* s,
-                          const float* in_shift, const float* in_scale, void* xs, float* xu,
-                          float* act32, void* stream);
+                          const float* in_shift, const float* in_scale, const float* xc, void* xs,
+                          float* xu, float* act32, void* stream);
 /* The same two with observations / actions staged as f32 by the host (the
  * policy's own input precision: gaussian_mlp.py:103 casts every observation to
  * f32, so the policy passes see identical values). */
@@ -106,11 +119,11 @@ int mjrl_pack_batch_f32(const float* obs, const float* act, int64_t T, const mjr
                         const float* in_shift, const float* in_scale, float* xhat, float* act32,
                         void* stream);
 int mjrl_pack_batch_split_f32(const float* obs, const float* act, int64_t T, const mjrl_shape* s,
-                              const float* in_shift, const float* in_scale, void* xs, float* xu,
-                              float* act32, void* stream);
-/* 1 if the policy passes for this shape accept split-f16 rows (mjrl_rows.xs): the
- * K = np first layer then runs as three f16 MFMAs per product (hi*hi + hi*lo +
- * lo*hi, f32 accumulate), the rest of the network in exact f32. */
+                              const float* in_shift, const float* in_scale, const float* xc, void* xs,
+                              float* xu, float* act32, void* stream);
+/* 1 if the policy passes for this shape accept split-f16 rows (mjrl_rows.xs): every
+ * product of the passes then runs as three f16 MFMAs (hi*hi + hi*lo + lo*hi, f32
+ * accumulate) on operands split with power-of-two block scales. */
 int mjrl_split_supported(const mjrl_shape* s);
 /* ---- returns / GAE (process_samples.py:3-44) ----
  * One lane per path, reverse recurrence in fp64, multiply-then-add (no FMA),

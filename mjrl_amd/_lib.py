@@ -32,7 +32,7 @@ class Shape(C.Structure):
 
 class Rows(C.Structure):
     _fields_ = [("T", C.c_int64)] + [(k, C.c_void_p) for k in (
-        "xhat", "act", "adv", "adv_vpg", "a0", "a1", "mu0", "ll0", "gu0", "gu1", "gp", "xs", "xu")]
+        "xhat", "act", "adv", "adv_vpg", "a0", "a1", "mu0", "ll0", "gu0", "gu1", "gp", "xs", "xu", "xc")]
 
 
 class Scratch(C.Structure):
@@ -51,9 +51,11 @@ SIGNATURES = {
     "mjrl_shape_init": [SP, I32, I32, I32, I32],
     "mjrl_scratch_size": [SP, I64, C.POINTER(I64), C.POINTER(I64), C.POINTER(I32)],
     "mjrl_pack_batch": [P, P, I64, SP, P, P, P, P, P],
-    "mjrl_pack_batch_split": [P, P, I64, SP, P, P, P, P, P, P],
+    "mjrl_obs_colscale": [P, I64, SP, P, P, P, P],
+    "mjrl_obs_colscale_f32": [P, I64, SP, P, P, P, P],
+    "mjrl_pack_batch_split": [P, P, I64, SP, P, P, P, P, P, P, P],
     "mjrl_pack_batch_f32": [P, P, I64, SP, P, P, P, P, P],
-    "mjrl_pack_batch_split_f32": [P, P, I64, SP, P, P, P, P, P, P],
+    "mjrl_pack_batch_split_f32": [P, P, I64, SP, P, P, P, P, P, P, P],
     "mjrl_split_supported": [SP],
     "mjrl_gae": [P, P, P, P, I64, F64, F64, I32, P, P, P, P],
     "mjrl_linear_baseline": [P, I64, I32, P, I64, P, P, P],

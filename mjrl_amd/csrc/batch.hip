@@ -44,18 +44,90 @@ __global__ void __launch_bounds__(256) k_pack_batch(const TO* __restrict__ obs, 
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < na; i += stride) act32[i] = (float)act[i];
 }
 
+// Column maxima of xhat over the batch (the input of the split rows' column
+// scales, common.h col_scale): cm[k] = max_t |xhat[t][k]| as f32 bits (atomicMax on
+// the bits of non-negative floats: order-independent, so deterministic), cm[n] =
+// 1 (the bias column).  Thread (rsub, j) of a workgroup owns the V-wide column
+// group j of rows rsub, rsub + RPP, ... of the workgroup's row stride; maxima go
+// through LDS (ds_max_u32), then one global atomicMax per column per workgroup.
+template <typename TO, int V>
+__global__ void __launch_bounds__(256) k_colmax(const TO* __restrict__ obs, int64_t T, int n,
+                                                const float* __restrict__ in_shift,
+                                                const float* __restrict__ in_scale, unsigned* __restrict__ cm) {
+    __shared__ unsigned smax[512];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < 512; i += 256) smax[i] = 0u;
+    __syncthreads();
+    const int nv = n / V;                       // V divides n (host)
+    const int span = nv < 256 ? nv : 256;       // column groups per pass
+    const int rpp = 256 / span;                 // rows per pass
+    const int rsub = tid / span, j0 = tid % span;
+    if (rsub < rpp) {
+        float mx[2][V];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int e = 0; e < V; ++e) mx[u][e] = 0.f;
+        float sh[2][V], den[2][V];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int e = 0; e < V; ++e) {
+                const int c = (j0 + 256 * u) * V + e;
+                sh[u][e] = in_shift && c < n ? in_shift[c] : 0.f;
+                den[u][e] = in_shift && c < n ? in_scale[c] + 1e-8f : 1.f;
+            }
+        for (int64_t row = (int64_t)blockIdx.x * rpp + rsub; row < T; row += (int64_t)gridDim.x * rpp) {
+            const TO* src = obs + row * n;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int j = j0 + 256 * u;
+                if (j >= nv) continue;
+                float x[V];
+                if constexpr (V == 4 && sizeof(TO) == 4) {
+                    const float4 q = *reinterpret_cast<const float4*>(src + 4 * j);
+                    x[0] = q.x; x[1] = q.y; x[2] = q.z; x[3] = q.w;
+                } else {
+#pragma unroll
+                    for (int e = 0; e < V; ++e) x[e] = (float)src[V * j + e];   // torch .float()
+                }
+#pragma unroll
+                for (int e = 0; e < V; ++e) {
+                    float v = x[e];
+                    if (in_shift) v = (v - sh[u][e]) / den[u][e];   // MuNet.forward:177, as the pack
+                    mx[u][e] = fmaxf(mx[u][e], fabsf(v));
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int e = 0; e < V; ++e) {
+                const int c = (j0 + 256 * u) * V + e;
+                if (c < n && (j0 + 256 * u) < nv) atomicMax(&smax[c], __float_as_uint(mx[u][e]));
+            }
+    }
+    __syncthreads();
+    for (int c = tid; c < n; c += 256)
+        if (smax[c]) atomicMax(&cm[c], smax[c]);
+    if (blockIdx.x == 0 && tid == 0) atomicMax(&cm[n], __float_as_uint(1.0f));
+}
+
 // obs f64 [T][n] -> split-f16 rows (mjrl_rows.xs / xu): one wave per row, lane l
 // owns columns l, l + 64, ... (np <= 512), so every load (8 B per lane) and every
-// hi / lo store (2 B per lane) is one contiguous wave-wide segment.  The row's
-// max |xhat| (>= 1: the bias column) gives xu = 2^E with |xhat / xu| < 1; then
-// hi = f16(y), lo = f16(y - hi) (split8, common.h).  The xhat values are those of
-// k_pack_batch.
+// hi / lo store (2 B per lane) is one contiguous wave-wide segment.  Each column is
+// divided by its power-of-two scale xc[k] (col_scale, common.h), then the row's
+// max |xhat / xc| (> 0: the bias column) gives xu = 2^(E-15) with the row's
+// max |y| in [2^14, 2^15), y = xhat / (xc xu); then hi = f16(y), lo = f16(y - hi).
+// Every scaling is by a power of two, so y * xc * xu is the f32 xhat of
+// k_pack_batch exactly, and the pair (hi, lo) carries it to the bound of common.h.
 constexpr int PS_MAXP = 4;   // column pairs per lane (np <= 512)
 template <typename TO>
 __global__ void __launch_bounds__(256) k_pack_split(const TO* __restrict__ obs, const TO* __restrict__ act,
                                                     int64_t T, int n, int m, int np,
                                                     const float* __restrict__ in_shift,
-                                                    const float* __restrict__ in_scale, _Float16* __restrict__ xs,
+                                                    const float* __restrict__ in_scale,
+                                                    const float* __restrict__ xc, _Float16* __restrict__ xs,
                                                     float* __restrict__ xu, float* __restrict__ act32) {
     // lane l owns the column pairs (2l + 128j, 2l + 128j + 1): 16-byte loads of the f64
     // row when n is even (8-byte otherwise), 4-byte hi / lo stores
@@ -63,6 +135,14 @@ __global__ void __launch_bounds__(256) k_pack_split(const TO* __restrict__ obs, 
     const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
     const int npair = (np + 127) / 128;
+    float icx[PS_MAXP][2];   // 1 / xc of the lane's columns (exact: powers of two)
+#pragma unroll
+    for (int j = 0; j < PS_MAXP; ++j)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int ce = 2 * lane + 128 * j + e;
+            icx[j][e] = ce < np ? 1.f / xc[ce] : 1.f;
+        }
     const bool even = (n & 1) == 0 && (reinterpret_cast<uintptr_t>(obs) & (2 * sizeof(TO) - 1)) == 0;   // pair loads
     for (int64_t row = wid; row < T; row += nw) {
         const TO* src = obs + row * n;
@@ -100,8 +180,8 @@ __global__ void __launch_bounds__(256) k_pack_split(const TO* __restrict__ obs, 
                         x = 1.0f;                                    // bias column (zero padding after)
                     }
                 }
-                v[j][e] = x;
-                mx = fmaxf(mx, fabsf(x));
+                v[j][e] = x * icx[j][e];
+                mx = fmaxf(mx, fabsf(v[j][e]));
             }
         }
 #pragma unroll
@@ -141,14 +221,15 @@ constexpr int PQ_MAXQ = 2;   // column quads per lane (np <= 512)
 __global__ void __launch_bounds__(256) k_pack_split_q(const float* __restrict__ obs, const float* __restrict__ act,
                                                       int64_t T, int n, int m, int np,
                                                       const float* __restrict__ in_shift,
-                                                      const float* __restrict__ in_scale, _Float16* __restrict__ xs,
+                                                      const float* __restrict__ in_scale,
+                                                      const float* __restrict__ xc, _Float16* __restrict__ xs,
                                                       float* __restrict__ xu, float* __restrict__ act32) {
     typedef _Float16 half4 __attribute__((ext_vector_type(4)));
     const int lane = threadIdx.x & 63;
     const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
     const int nq = (np + 255) / 256;
-    float sh[PQ_MAXQ][4], den[PQ_MAXQ][4];
+    float sh[PQ_MAXQ][4], den[PQ_MAXQ][4], icx[PQ_MAXQ][4];
 #pragma unroll
     for (int j = 0; j < PQ_MAXQ; ++j)
 #pragma unroll
@@ -156,6 +237,7 @@ __global__ void __launch_bounds__(256) k_pack_split_q(const float* __restrict__ 
             const int ce = 4 * lane + 256 * j + e;
             sh[j][e] = in_shift && ce < n ? in_shift[ce] : 0.f;
             den[j][e] = in_shift && ce < n ? in_scale[ce] + 1e-8f : 1.f;
+            icx[j][e] = ce < np ? 1.f / xc[ce] : 1.f;   // exact: powers of two
         }
     for (int64_t row = wid; row < T; row += nw) {
         const float* src = obs + row * n;
@@ -187,8 +269,8 @@ __global__ void __launch_bounds__(256) k_pack_split_q(const float* __restrict__ 
                         x = 1.0f;                                    // bias column (zero padding after)
                     }
                 }
-                v[j][e] = x;
-                mx = fmaxf(mx, fabsf(x));
+                v[j][e] = x * icx[j][e];
+                mx = fmaxf(mx, fabsf(v[j][e]));
             }
         }
 #pragma unroll
@@ -782,8 +864,9 @@ static int pack_batch(const TO* obs, const TO* act, int64_t T, const mjrl_shape*
 extern "C++" {
 template <typename TO>
 static int pack_batch_split(const TO* obs, const TO* act, int64_t T, const mjrl_shape* s, const float* in_shift,
-                            const float* in_scale, void* xs, float* xu, float* act32, void* stream) {
-    if (!s || T < 0 || (T > 0 && (!obs || !act || !xs || !xu || !act32))) return MJRL_EINVAL;
+                            const float* in_scale, const float* xc, void* xs, float* xu, float* act32,
+                            void* stream) {
+    if (!s || T < 0 || (T > 0 && (!obs || !act || !xc || !xs || !xu || !act32))) return MJRL_EINVAL;
     if ((in_shift == nullptr) != (in_scale == nullptr)) return MJRL_EINVAL;
     if (s->np > 128 * PS_MAXP) return MJRL_ESHAPE;
     if (T == 0) return MJRL_OK;
@@ -791,12 +874,40 @@ static int pack_batch_split(const TO* obs, const TO* act, int64_t T, const mjrl_
     if constexpr (sizeof(TO) == 4) {
         if (s->n % 4 == 0 && (reinterpret_cast<uintptr_t>(obs) & 15) == 0 && s->np % 4 == 0 && s->np <= 256 * PQ_MAXQ) {
             hipLaunchKernelGGL(k_pack_split_q, dim3(g), dim3(256), 0, (hipStream_t)stream, obs, act, T, s->n, s->m,
-                               s->np, in_shift, in_scale, (_Float16*)xs, xu, act32);
+                               s->np, in_shift, in_scale, xc, (_Float16*)xs, xu, act32);
             return err(hipGetLastError());
         }
     }
     hipLaunchKernelGGL(k_pack_split<TO>, dim3(g), dim3(256), 0, (hipStream_t)stream, obs, act, T, s->n, s->m, s->np,
-                       in_shift, in_scale, (_Float16*)xs, xu, act32);
+                       in_shift, in_scale, xc, (_Float16*)xs, xu, act32);
+    return err(hipGetLastError());
+}
+
+// column maxima -> power-of-two column scales, in place (one workgroup)
+__global__ void k_colscale(float* xc, int np) {
+    for (int k = threadIdx.x; k < np; k += blockDim.x) xc[k] = col_scale(xc[k]);
+}
+
+template <typename TO>
+static int obs_colscale(const TO* obs, int64_t T, const mjrl_shape* s, const float* in_shift, const float* in_scale,
+                        float* xc, void* stream) {
+    if (!s || T < 0 || !xc || (T > 0 && !obs)) return MJRL_EINVAL;
+    if ((in_shift == nullptr) != (in_scale == nullptr)) return MJRL_EINVAL;
+    if (s->np > 512 || s->n >= s->np) return MJRL_ESHAPE;
+    hipStream_t st = (hipStream_t)stream;
+    hipError_t e = hipMemsetAsync(xc, 0, sizeof(float) * s->np, st);
+    if (e != hipSuccess) return (int)e;
+    const bool q4 = sizeof(TO) == 4 && s->n % 4 == 0 && (reinterpret_cast<uintptr_t>(obs) & 15) == 0;
+    const int nv = q4 ? s->n / 4 : s->n;
+    const int rpp = 256 / (nv < 256 ? nv : 256);
+    const int g = T > 0 ? grid_for(T, rpp * 8, 2048) : 1;
+    if (q4)
+        hipLaunchKernelGGL((k_colmax<TO, 4>), dim3(g), dim3(256), 0, st, obs, T, s->n, in_shift, in_scale,
+                           reinterpret_cast<unsigned*>(xc));
+    else
+        hipLaunchKernelGGL((k_colmax<TO, 1>), dim3(g), dim3(256), 0, st, obs, T, s->n, in_shift, in_scale,
+                           reinterpret_cast<unsigned*>(xc));
+    hipLaunchKernelGGL(k_colscale, dim3(1), dim3(512), 0, st, xc, s->np);
     return err(hipGetLastError());
 }
 }  // extern "C++"
@@ -811,16 +922,26 @@ int mjrl_pack_batch_f32(const float* obs, const float* act, int64_t T, const mjr
     return pack_batch(obs, act, T, s, in_shift, in_scale, xhat, act32, stream);
 }
 
+int mjrl_obs_colscale(const double* obs, int64_t T, const mjrl_shape* s, const float* in_shift,
+                      const float* in_scale, float* xc, void* stream) {
+    return obs_colscale(obs, T, s, in_shift, in_scale, xc, stream);
+}
+
+int mjrl_obs_colscale_f32(const float* obs, int64_t T, const mjrl_shape* s, const float* in_shift,
+                          const float* in_scale, float* xc, void* stream) {
+    return obs_colscale(obs, T, s, in_shift, in_scale, xc, stream);
+}
+
 int mjrl_pack_batch_split(const double* obs, const double* act, int64_t T, const mjrl_shape* s,
-                          const float* in_shift, const float* in_scale, void* xs, float* xu, float* act32,
-                          void* stream) {
-    return pack_batch_split(obs, act, T, s, in_shift, in_scale, xs, xu, act32, stream);
+                          const float* in_shift, const float* in_scale, const float* xc, void* xs, float* xu,
+                          float* act32, void* stream) {
+    return pack_batch_split(obs, act, T, s, in_shift, in_scale, xc, xs, xu, act32, stream);
 }
 
 int mjrl_pack_batch_split_f32(const float* obs, const float* act, int64_t T, const mjrl_shape* s,
-                              const float* in_shift, const float* in_scale, void* xs, float* xu, float* act32,
-                              void* stream) {
-    return pack_batch_split(obs, act, T, s, in_shift, in_scale, xs, xu, act32, stream);
+                              const float* in_shift, const float* in_scale, const float* xc, void* xs, float* xu,
+                              float* act32, void* stream) {
+    return pack_batch_split(obs, act, T, s, in_shift, in_scale, xc, xs, xu, act32, stream);
 }
 
 int mjrl_gae(const double* rew, const double* base, const int64_t* path_off, const uint8_t* terminated, int64_t P,

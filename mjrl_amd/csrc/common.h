@@ -36,14 +36,21 @@ __device__ __forceinline__ floatx4 mfma_k16(const float4& a, const float4& b, fl
 
 // ---------------------------------------------------------------------------
 // Split-f16 operands ("fp16x3"): an f32 value y of a block scaled by a power of
-// two so max |y| < 1 is carried as hi = f16(y) and lo = f16(y - hi) (round to
-// nearest; y - hi is exact).  A product of two split operands is hi*hi + hi*lo +
-// lo*hi, three v_mfma_f32_16x16x32_f16 into ONE f32 accumulator (f16 products are
-// exact), dropping only lo*lo.  Error of one operand: <= 2^-24 |y| while lo is
-// normal (|y| >= 2^-2), and <= 2^-25 of the block max below that (lo is then an
-// f16 subnormal): 24-bit block floating point, the f32 mantissa width.  Three f16
-// MFMAs carry 8x the k of one v_mfma_f32_16x16x4_f32 in half its cycles: 5.3x
-// the f32 matrix rate.
+// two is carried as hi = f16(y) and lo = f16(y - hi) (round to nearest; y - hi is
+// exact).  A product of two split operands is hi*hi + hi*lo + lo*hi, three
+// v_mfma_f32_16x16x32_f16 into ONE f32 accumulator (f16 products are exact),
+// dropping only lo*lo.  Three f16 MFMAs carry 8x the k of one
+// v_mfma_f32_16x16x4_f32 in half its cycles: 5.3x the f32 matrix rate.
+//
+// Block scale with headroom: the block's max |y| goes to [2^14, 2^15), the top of
+// the f16 range (not [1/2, 1)).  Element error of the pair, for every y of the block:
+//     |hi + lo - y| <= 2^-23 |y| + 2^-25,
+// the second term being lo's subnormal floor (f16 subnormals are 2^-24 apart).
+// Relative to the block max B that is 2^-23 |y| + 2^-40 B: every element down to
+// 2^-17 of its block max keeps 23 bits (f32 rounding is 2^-24), and the absolute
+// floor sits 40 binades below the max, where a [1/2, 1) block had it at 2^-25 B
+// (an element 1e-6 of its row max then lost everything).  Products stay far inside
+// f32: |hi * hi| < 2^30, a K = 384 sum < 2^39.
 // ---------------------------------------------------------------------------
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef short short4v __attribute__((ext_vector_type(4)));
@@ -60,8 +67,11 @@ __device__ __forceinline__ floatx4 mfma_x3(const half8& ah, const half8& al, con
     return mfma_h(al, bh, c);
 }
 
-// Power-of-two scale for a block whose max |value| is M: returns s = 2^-E with
-// M * s in [0.5, 1) and sets inv = 2^E (s = inv = 1 for M == 0 / non-finite).
+constexpr int SPLIT_HR = 15;   // block max -> [2^(SPLIT_HR-1), 2^SPLIT_HR)
+
+// Power-of-two scale for a block whose max |value| is M: returns s = 2^(15-E) with
+// M * s in [2^14, 2^15) and sets inv = 1 / s = 2^(E-15) (s = inv = 1 for M == 0 /
+// non-finite; blocks below 2^-111 keep s = 2^126).
 __device__ __forceinline__ float pow2_scale(float M, float& inv) {
     if (!(M > 0.f) || !(M < 3.0e38f)) {
         inv = 1.f;
@@ -69,10 +79,29 @@ __device__ __forceinline__ float pow2_scale(float M, float& inv) {
     }
     int E;
     frexpf(M, &E);
-    E = E < -120 ? -120 : E;
-    inv = ldexpf(1.f, E);
-    return ldexpf(1.f, -E);
+    E = E < -111 ? -111 : E;
+    inv = ldexpf(1.f, E - SPLIT_HR);
+    return ldexpf(1.f, SPLIT_HR - E);
 }
+
+// Split xhat rows (mjrl_rows.xs): column k carries xhat / xc[k] with xc[k] = 2^E the
+// power of two with colmax[k] 2^-E in [1/2, 1) over the batch (1 for an all-zero
+// column), then each row is scaled by its own power of two (xu[t], headroom as
+// above).  Then |xc xu (hi + lo) - xhat| <= 2^-23 |xhat| + 2^-39 xc_k r_t, r_t =
+// max_j |xhat[t][j]| / xc_j < 1, so at most 2^-23 |xhat| + 2^-38 colmax_k: a
+// small-scale feature keeps 23 bits in rows dominated by large ones.
+__device__ __forceinline__ float col_scale(float cmax) {
+    if (!(cmax > 0.f) || !(cmax < 3.0e38f)) return 1.f;
+    int E;
+    frexpf(cmax, &E);
+    E = E < -100 ? -100 : (E > 100 ? 100 : E);
+    return ldexpf(1.f, E);
+}
+
+// Cached tanh activations (|a| <= 1) are split into their LDS images with the fixed
+// scale 2^14 (the same headroom); consumers multiply by AHR_INV (exact).
+constexpr float AHR = 16384.f;
+constexpr float AHR_INV = 1.f / 16384.f;
 
 typedef float float8v __attribute__((ext_vector_type(8)));
 typedef short short8v __attribute__((ext_vector_type(8)));

@@ -15,33 +15,22 @@
 // row chain of k_rows; gW1 / gW2 / biases accumulate in registers too.  Slabs
 // are written at the end in k_gather's layout.
 //
-// SX = true: the two K = NP products of the first layer (xhat W0^T and the gW0
-// update) run as split-f16 ("fp16x3", common.h) on v_mfma_f32_16x16x32_f16:
-//   - xhat arrives pre-split from mjrl_pack_batch_split: per row [hi NP][lo NP]
-//     f16 of y = xhat / u_r, u_r a power of two (row scale xu[r]);
-//   - the W0 / dW0 slice is scaled per hidden unit and split once per launch;
-//   - gW0's left operand (gu0 * u_r) is scaled per (tile, hidden unit) and split
-//     per tile; its right operand is read from the xhat image with the gfx950
-//     transposing LDS read (ds_read_b64_tr_b16).
-// The LDS images of xhat hi / lo use 16-byte chunks XOR-swizzled by row so both
-// the row reads (phase 1) and the transposed reads (gW0) are bank-conflict free.
-// The 64-wide layers stay on exact-f32 MFMA.
+// The split-f16 form of this tile walk, with every product on f16 MFMA, is k_kx
+// (kx.h); this kernel is the exact-f32 path (precision = 'f32').
 #pragma once
 
 namespace {
 
 constexpr int KT = 512;
 
-template <int MP, int KG, bool SX>
+template <int MP, int KG>
 struct KLayout {
     static constexpr int H = 64, BT = 32, RB = 2;
     static constexpr int NP = 32 * KG, KH = NP / 2;
     static constexpr int LDX = NP + 16;   // rows 4 apart fall 16 banks apart for the b32 gW0 reads
     static constexpr int LD = H + 4, LDP = MP + 4;
-    static constexpr int LDG = BT + 4;    // SX: gu0 tile stored transposed, [H][LDG]
-    static constexpr int RBYTES = NP * 2; // SX: bytes of one f16 row of the hi / lo image
     static_assert(KT == BT * H / 4, "tanh_tile: one float4 per thread");
-    static constexpr int XFLOATS = SX ? 2 * BT * RBYTES / 4 : BT * LDX;
+    static constexpr int XFLOATS = BT * LDX;
     static constexpr int oXT = 0;
     static constexpr int oD0 = oXT + XFLOATS;
     static constexpr int oA0 = oD0 + BT * LD;
@@ -52,17 +41,14 @@ struct KLayout {
     static constexpr int odW1 = oW1 + H * LD;      // [64][LD]  dW1 (FVP)
     static constexpr int oW2 = odW1 + H * LD;      // [MP][LD]  W2p
     static constexpr int odW2 = oW2 + MP * LD;     // [MP][LD]  dW2p (FVP)
-    static constexpr int oG0T = odW2 + MP * LD;    // SX: [H][LDG] gu0 * u_r, transposed
-    static constexpr int oU = oG0T + (SX ? H * LDG : 0);   // SX: [BT] row scales
-    static constexpr int total = oU + (SX ? BT : 0);
+    static constexpr int total = odW2 + MP * LD;
     static constexpr int bytes = total * 4;
     static_assert(bytes <= 160 * 1024, "LDS");
     static constexpr int XPER = BT * NP / 4 / KT;  // 16-byte pieces of the xhat tile per thread
     static_assert(XPER * KT * 4 == BT * NP, "NP must be a multiple of 64");
-    static_assert(!SX || NP % 128 == 0, "SX: the chunk swizzle needs NP % 128 == 0");
 };
 
-// XOR swizzle of the 16-byte chunks of row `row` in the SX xhat images (rows of
+// XOR swizzle of the 16-byte chunks of row `row` in k_kx's xhat images (rows of
 // NP halves, a multiple of 256 B): ds_read_b128 of 16 rows (lane groups
 // {0-3,12-15,20-27}, ... of MI355X_MICROARCH.md §LDS) and ds_read_b64_tr_b16 of
 // rows {8q + 4h + 0..3} (32-lane halves) both touch 64 distinct banks (found by
@@ -120,15 +106,13 @@ __device__ __forceinline__ void tanh_tile(const float* U, float* A, float* cache
     if (cache && gr < T) *reinterpret_cast<float4*>(cache + gr * 64 + c) = v;
 }
 
-template <int MP, int KG, int MODE, bool SX>
+template <int MP, int KG, int MODE>
 __global__ void __launch_bounds__(KT, 1) k_ks(RowArgs a, FOut o) {
-    using L = KLayout<MP, KG, SX>;
+    using L = KLayout<MP, KG>;
     constexpr int H = 64, BT = L::BT, NP = L::NP, KH = L::KH;
     constexpr bool GRAD = MODE != EVAL;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float* XT = smem + L::oXT;
-    char* XHb = reinterpret_cast<char*>(smem + L::oXT);   // SX: hi image, then lo image
-    char* XLb = XHb + BT * L::RBYTES;
     float* D0 = smem + L::oD0;
     float* A0s = smem + L::oA0;
     float* D1 = smem + L::oD1;
@@ -138,8 +122,6 @@ __global__ void __launch_bounds__(KT, 1) k_ks(RowArgs a, FOut o) {
     float* sdW1 = smem + L::odW1;
     float* sW2 = smem + L::oW2;
     float* sdW2 = smem + L::odW2;
-    float* G0T = smem + L::oG0T;
-    float* Us = smem + L::oU;
 
     if (MODE == FVP && a.done && *a.done) return;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -163,26 +145,10 @@ __global__ void __launch_bounds__(KT, 1) k_ks(RowArgs a, FOut o) {
         sW2[row * L::LD + col] = P[pk.W2 + i];
         if (MODE == FVP) sdW2[row * L::LD + col] = a.V[pk.W2 + i];
     }
-    constexpr int KS = SX ? KH / 32 : 1;   // SX: k32 steps per observation half
-    float4 wb[SX ? 1 : KG];   // f32: B fragments W0[cb*16 + r][kh*KH + 16g + 4q .. +3]
-    half8 wh[KS], wl[KS];     // SX: split B fragments W0[cb*16 + r][kh*KH + 32s + 8q .. +7]
-    float wsc = 1.f;          // SX: 2^E of this lane's hidden unit (undoes the split scale)
-    if constexpr (SX) {
-        float8v v[KS];
-        float mx = 0.f;
+    float4 wb[KG];   // B fragments W0[cb*16 + r][kh*KH + 16g + 4q .. +3]
 #pragma unroll
-        for (int s = 0; s < KS; ++s) {
-            v[s] = load8(W0src + (cb * 16 + r16) * NP + kh * KH + 32 * s + 8 * q);
-            mx = fmaxf(mx, absmax8(v[s]));
-        }
-        const float sc = pow2_scale(max_over_groups(mx), wsc);
-#pragma unroll
-        for (int s = 0; s < KS; ++s) split8(v[s], sc, wh[s], wl[s]);
-    } else {
-#pragma unroll
-        for (int g = 0; g < KG; ++g)
-            wb[g] = *reinterpret_cast<const float4*>(W0src + (cb * 16 + r16) * NP + kh * KH + 16 * g + 4 * q);
-    }
+    for (int g = 0; g < KG; ++g)
+        wb[g] = *reinterpret_cast<const float4*>(W0src + (cb * 16 + r16) * NP + kh * KH + 16 * g + 4 * q);
 
     // accumulators (FWD / FVP)
     floatx4 g0[KG];   // gW0[cb*16 ..][kh*KH + 16g ..]
@@ -223,29 +189,7 @@ __global__ void __launch_bounds__(KT, 1) k_ks(RowArgs a, FOut o) {
         const int nrow = (int)(T - row_base < BT ? T - row_base : BT);   // valid rows of this tile
         // ---- publish this tile's xhat (L2-warm from the previous tile's touch) ----
         asm volatile("" ::"v"(touch));
-        if constexpr (SX) {
-            // 16 threads per row (row = ltid / 16), piece c = ltid % 16 + 16 u of the row's
-            // NP/4 16-byte pieces: pieces u < NP/128 are hi chunks, the rest lo chunks;
-            // every address is a per-thread base plus an immediate
-            const char* src = reinterpret_cast<const char*>(a.xs);
-            const int row = ltid >> 4, c16 = ltid & 15;
-            const int64_t gr = row_base + row;
-            float4 xr[L::XPER];
-#pragma unroll
-            for (int u = 0; u < L::XPER; ++u)
-                xr[u] = gr < T ? *reinterpret_cast<const float4*>(src + gr * (4 * NP) + 16 * (c16 + 16 * u))
-                               : make_float4(0.f, 0.f, 0.f, 0.f);
-            char* dst = XHb + row * L::RBYTES + 16 * (c16 ^ chunk_swz(row));
-#pragma unroll
-            for (int u = 0; u < L::XPER; ++u) {
-                constexpr int UH = NP / 128;   // pieces per thread in each of hi / lo
-                *reinterpret_cast<float4*>(dst + (u / UH) * (BT * L::RBYTES) + 256 * (u % UH)) = xr[u];
-            }
-            if (ltid < BT) {
-                const int64_t gu = row_base + ltid;
-                Us[ltid] = gu < T ? a.xu[gu] : 1.f;
-            }
-        } else {
+        {
             float4 xr[L::XPER];
 #pragma unroll
             for (int u = 0; u < L::XPER; ++u) {
@@ -283,50 +227,24 @@ __global__ void __launch_bounds__(KT, 1) k_ks(RowArgs a, FOut o) {
         // value is only kept alive until the next publish, 1 VGPR)
         {
             const int64_t nt = tile + gridDim.x;
-            constexpr int LPR = (SX ? 4 * NP : 4 * NP) / 128;   // lines per row
+            constexpr int LPR = 4 * NP / 128;   // lines per row
             if (nt < ntiles && ltid < BT * LPR) {
                 const int64_t gr = nt * BT + ltid / LPR;
-                if (gr < T) {
-                    if constexpr (SX)
-                        touch = reinterpret_cast<const float*>(a.xs)[gr * NP + (ltid % LPR) * 32];
-                    else
-                        touch = a.xhat[gr * NP + (ltid % LPR) * 32];
-                }
+                if (gr < T) touch = a.xhat[gr * NP + (ltid % LPR) * 32];
             }
         }
 
         // ---- phase 1: partial [32 x 16] over this wave's observation half ----
         floatx4 acc1[2] = {zero4(), zero4()};
-        if constexpr (SX) {
-            const int swz1 = chunk_swz(lr16);   // rows 16i + r16: same swizzle for both i
 #pragma unroll
-            for (int s = 0; s < KS; ++s) {
-                const int ch = kh * (KH / 8) + 4 * s + lq;
+        for (int g = 0; g < KG; ++g) {
+            const int k = kh * KH + 16 * g + 4 * lq;
 #pragma unroll
-                for (int i = 0; i < 2; ++i) {
-                    const int row = i * 16 + lr16;
-                    const int off = row * L::RBYTES + 16 * (ch ^ swz1);
-                    const half8 xh = *reinterpret_cast<const half8*>(XHb + off);
-                    const half8 xl = *reinterpret_cast<const half8*>(XLb + off);
-                    acc1[i] = mfma_x3(xh, xl, wh[s], wl[s], acc1[i]);
-                }
-                if (s & 1) __builtin_amdgcn_sched_barrier(0);
+            for (int i = 0; i < 2; ++i) {
+                const float4 x = *reinterpret_cast<const float4*>(XT + (i * 16 + lr16) * L::LDX + k);
+                acc1[i] = mfma_k16(x, wb[g], acc1[i]);
             }
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int rr = 0; rr < 4; ++rr) acc1[i][rr] *= Us[i * 16 + 4 * lq + rr] * wsc;
-        } else {
-#pragma unroll
-            for (int g = 0; g < KG; ++g) {
-                const int k = kh * KH + 16 * g + 4 * lq;
-#pragma unroll
-                for (int i = 0; i < 2; ++i) {
-                    const float4 x = *reinterpret_cast<const float4*>(XT + (i * 16 + lr16) * L::LDX + k);
-                    acc1[i] = mfma_k16(x, wb[g], acc1[i]);
-                }
-                if ((g & 3) == 3) __builtin_amdgcn_sched_barrier(0);   // bound the hoisting of LDS reads
-            }
+            if ((g & 3) == 3) __builtin_amdgcn_sched_barrier(0);   // bound the hoisting of LDS reads
         }
         // fold the two halves: kh = 1 publishes, kh = 0 finishes
         if (kh == 1) {
@@ -443,56 +361,14 @@ __global__ void __launch_bounds__(KT, 1) k_ks(RowArgs a, FOut o) {
                     const float av = A0s[row * L::LD + col];
                     g[rr] = row < nrow ? (1.f - av * av) * acc[0][rr] : 0.f;
                 }
-                if constexpr (SX) {
-                    // transposed, times the row scale: gW0 = sum_r (gu0_r u_r) (hi_r + lo_r 2^-12)
-                    const int r0 = kh * 16 + 4 * lq;
-                    *reinterpret_cast<float4*>(G0T + col * L::LDG + r0) =
-                        make_float4(g[0] * Us[r0], g[1] * Us[r0 + 1], g[2] * Us[r0 + 2], g[3] * Us[r0 + 3]);
-                } else {
 #pragma unroll
-                    for (int rr = 0; rr < 4; ++rr) D0[(kh * 16 + 4 * lq + rr) * L::LD + col] = g[rr];
-                }
+                for (int rr = 0; rr < 4; ++rr) D0[(kh * 16 + 4 * lq + rr) * L::LD + col] = g[rr];
             }
             __syncthreads();
             // ---- weight gradients (registers) ----
-            if constexpr (SX) {
-                // left operand: gu0 rows 8q..8q+7 of hidden unit cb*16 + lr16, split per (tile, unit)
-                half8 gh, gl;
-                float sc4[4];
-                {
-                    const float8v v = load8(G0T + (cb * 16 + lr16) * L::LDG + 8 * lq);
-                    float inv;
-                    const float s = pow2_scale(max_over_groups(absmax8(v)), inv);
-                    split8(v, s, gh, gl);
-#pragma unroll
-                    for (int rr = 0; rr < 4; ++rr) sc4[rr] = __shfl(inv, 4 * lq + rr, 64);
-                }
-                // right operand: xhat rows 8q..8q+7 of columns kh*KH + 16g + lr16 (transposed reads)
-                const int tq = lr16 >> 2, tp = lr16 & 3;
-                const int cl = (kh * KH) / 8 + (tp >> 1);
-#pragma unroll
-                for (int g = 0; g < KG; ++g) {
-                    const int c0 = cl + 2 * g;
-                    short4v th[2], tl[2];
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const int row = 8 * lq + 4 * h + tq;
-                        const int off = row * L::RBYTES + 16 * (c0 ^ chunk_swz(row)) + 8 * (tp & 1);
-                        th[h] = ds_read_tr16(XHb + off);
-                        tl[h] = ds_read_tr16(XLb + off);
-                    }
-                    const half8 bh = __builtin_bit_cast(half8, __builtin_shufflevector(th[0], th[1], 0, 1, 2, 3, 4, 5, 6, 7));
-                    const half8 bl = __builtin_bit_cast(half8, __builtin_shufflevector(tl[0], tl[1], 0, 1, 2, 3, 4, 5, 6, 7));
-                    const floatx4 t = mfma_x3(gh, gl, bh, bl, zero4());
-#pragma unroll
-                    for (int rr = 0; rr < 4; ++rr) g0[g][rr] += t[rr] * sc4[rr];
-                    if (g & 1) __builtin_amdgcn_sched_barrier(0);   // bound the hoisting of the operand reads
-                }
-            }
-            constexpr int WUNR = SX ? BT / 4 : 1;   // SX: only the 64-wide sums remain, unroll fully
-#pragma unroll WUNR
+#pragma unroll 1
             for (int t = 0; t < BT; t += 4) {
-                if constexpr (!SX) {
+                {
                     const float gu = D0[(t + lq) * L::LD + cb * 16 + lr16];
 #pragma unroll
                     for (int g = 0; g < KG; ++g) {

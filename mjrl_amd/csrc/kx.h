@@ -12,8 +12,8 @@
 //              forward product (row reads) and its backward product (transposed
 //              reads, ds_read_b64_tr_b16) when it is column-scaled, the column
 //              scale being folded into the dynamic left operand;
-//   cached activations a0 / a1 (|a| < 1) — split without scaling into
-//              [feature][row] images read both ways;
+//   cached activations a0 / a1 (|a| <= 1) — split at the fixed scale 2^14
+//              (common.h AHR) into [feature][row] images read both ways;
 //   dynamic operands (tangents, upstream gradients) — scaled by a power of two
 //              per row (over the K of the product, max over the 4 lane groups)
 //              or, for the weight-gradient sums, per (tile, unit) column, split
@@ -125,28 +125,25 @@ __device__ __forceinline__ void acol(const char* img, int f, int q, half8& h, ha
     h = *reinterpret_cast<const half8*>(img + off);
     l = *reinterpret_cast<const half8*>(img + AIMG_BYTES + off);
 }
-// a at (feature f, row) from an activation image (hi + lo)
-__device__ __forceinline__ float aval(const char* img, int f, int row) {
-    const int off = aoff(f, row);
-    return mix_add_lo(*reinterpret_cast<const unsigned short*>(img + off),
-                      *reinterpret_cast<const unsigned short*>(img + AIMG_BYTES + off));
-}
+// Activation images hold a * AHR (common.h: the 2^14 headroom of every split
+// block); aval4 returns a itself, MFMA consumers fold AHR_INV into their scales.
 // a at (feature f, rows row0 .. row0 + 3), row0 % 4 == 0: one 8-byte read each of hi and lo
 __device__ __forceinline__ void aval4(const char* img, int f, int row0, float (&v)[4]) {
     typedef unsigned uint2v __attribute__((ext_vector_type(2)));
     const int off = aoff(f, row0);
     const uint2v h = *reinterpret_cast<const uint2v*>(img + off);
     const uint2v l = *reinterpret_cast<const uint2v*>(img + AIMG_BYTES + off);
-    v[0] = mix_add_lo(h[0], l[0]);
-    v[1] = mix_add_hi(h[0], l[0]);
-    v[2] = mix_add_lo(h[1], l[1]);
-    v[3] = mix_add_hi(h[1], l[1]);
+    v[0] = mix_add_lo(h[0], l[0]) * AHR_INV;
+    v[1] = mix_add_hi(h[0], l[0]) * AHR_INV;
+    v[2] = mix_add_lo(h[1], l[1]) * AHR_INV;
+    v[3] = mix_add_hi(h[1], l[1]) * AHR_INV;
 }
 // store 4 consecutive rows (row0..row0+3, row0 % 4 == 0) of feature f into an activation image
-__device__ __forceinline__ void astore4(char* img, int f, int row0, const float (&v)[4]) {
+__device__ __forceinline__ void astore4(char* img, int f, int row0, const float (&a)[4]) {
     typedef _Float16 half4 __attribute__((ext_vector_type(4)));
     typedef unsigned uint2v __attribute__((ext_vector_type(2)));
     typedef float float4v __attribute__((ext_vector_type(4)));
+    const float v[4] = {a[0] * AHR, a[1] * AHR, a[2] * AHR, a[3] * AHR};
     const float4v x = {v[0], v[1], v[2], v[3]};
     const half4 h = __builtin_convertvector(x, half4);
     const uint2v hb = __builtin_bit_cast(uint2v, h);
@@ -334,9 +331,14 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
     half8 wh[KS], wl[KS];
     float wsc;
     {
+        // W0 xc: the split rows carry xhat / (xc xu) (common.h col_scale), so the slice
+        // takes the column scales (exact: powers of two)
         float8v v[KS];
 #pragma unroll
-        for (int s = 0; s < KS; ++s) v[s] = load8(W0src + (cb * 16 + r16) * NP + kh * KH + 32 * s + 8 * q);
+        for (int s = 0; s < KS; ++s) {
+            const int k0 = kh * KH + 32 * s + 8 * q;
+            v[s] = load8(W0src + (cb * 16 + r16) * NP + k0) * load8(a.xc + k0);
+        }
         float mx = 0.f;
 #pragma unroll
         for (int s = 0; s < KS; ++s) mx = fmaxf(mx, absmax8(v[s]));
@@ -602,7 +604,7 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
                 for (int s = 0; s < 2; ++s) {
                     arow(A0i, kh, s, lq, lr16, xh[s], xl[s]);
                     const int o = (kh * 16 + lr16) * L::LD + 32 * s + 8 * lq;
-                    const float8v av = hilo8(xh[s], xl[s]);
+                    const float8v av = hilo8(xh[s], xl[s]) * AHR_INV;
                     dv[s] = (load8(D0 + o) + load8(D0B + o)) * (1.f - av * av);   // W1c column scale folded in P1
                     mx = fmaxf(mx, absmax8(dv[s]));
                 }
@@ -620,7 +622,7 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
                     wrow(S2, L::WIMG, j, s, lq, bh, bl);
                     accb = mfma_x3(xh[s], xl[s], bh, bl, accb);
                 }
-                const float dsc = sc2[j];
+                const float dsc = sc2[j] * AHR_INV;
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) acc[rr] = acc[rr] * ri[rr] + accb[rr] * dsc;
             } else {
@@ -633,7 +635,7 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
                     wrow(img, L::WIMG, j, s, lq, bh, bl);
                     acc = mfma_x3(xh, xl, bh, bl, acc);
                 }
-                const float rsc = (MODE == FWD ? sc2 : sc1)[j];
+                const float rsc = (MODE == FWD ? sc2 : sc1)[j] * AHR_INV;
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) acc[rr] *= rsc;
             }
@@ -674,7 +676,7 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
                     wrow(S4, L::WIMG2, col3, s, lq, bh, bl);
                     accb = mfma_x3(xh, xl, bh, bl, accb);
                 }
-                const float dsc = sc4v[col3];
+                const float dsc = sc4v[col3] * AHR_INV;
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) acc[rr] = acc[rr] * ri[rr] + accb[rr] * dsc;
             } else {
@@ -686,7 +688,7 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
                     wrow(img, L::WIMG2, col3, s, lq, bh, bl);
                     acc = mfma_x3(xh, xl, bh, bl, acc);
                 }
-                const float rsc = (MODE == FWD ? sc4v : sc3)[col3];
+                const float rsc = (MODE == FWD ? sc4v : sc3)[col3] * AHR_INV;
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) acc[rr] *= rsc;
             }
@@ -769,7 +771,7 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
                 const float sc = pow2_scale(max_over_groups(absmax8(v)), inv);
                 split8(v, sc, gh, gl);
 #pragma unroll
-                for (int rr = 0; rr < 4; ++rr) s4[rr] = __shfl(inv, 4 * lq + rr, 64);
+                for (int rr = 0; rr < 4; ++rr) s4[rr] = __shfl(inv, 4 * lq + rr, 64) * AHR_INV;
                 if ((w & 3) == 0) {
                     b2acc += sum_over_groups(((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7])));
                 }
@@ -822,7 +824,7 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
                 const float sc = pow2_scale(max_over_groups(absmax8(v)), inv);
                 split8(v, sc, gh, gl);
 #pragma unroll
-                for (int rr = 0; rr < 4; ++rr) s4[rr] = __shfl(inv, 4 * lq + rr, 64);
+                for (int rr = 0; rr < 4; ++rr) s4[rr] = __shfl(inv, 4 * lq + rr, 64) * AHR_INV;
                 if (kh == 0) {
                     b1acc += sum_over_groups(((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7])));
                 }
@@ -885,16 +887,18 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
         auto put = [&](int f, float v) { o.wpart[(((int64_t)(f >> 6)) * S + blk) * 64 + (f & 63)] = v; };
         const int fb0 = H * n, fW1 = fb0 + H, fb1 = fW1 + H * H, fW2 = fb1 + H, fb2 = fW2 + mm * H;
 #pragma unroll
-        for (int g = 0; g < KG; ++g)
+        for (int g = 0; g < KG; ++g) {
+            const int k = kh * KH + 16 * g + r16;
+            const float xck = a.xc[k];   // the rows' column scale (exact)
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr) {
                 const int hid = cb * 16 + 4 * q + rr;
-                const int k = kh * KH + 16 * g + r16;
                 if (k < n)
-                    put(hid * n + k, g0[g][rr]);
+                    put(hid * n + k, g0[g][rr] * xck);
                 else if (k == n)
-                    put(fb0 + hid, g0[g][rr]);   // b0 rides in the bias column
+                    put(fb0 + hid, g0[g][rr] * xck);   // b0 rides in the bias column
             }
+        }
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll

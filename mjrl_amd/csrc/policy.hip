@@ -45,8 +45,9 @@ struct RowArgs {
     double* rpart;        // per-workgroup partials
     const int32_t* done;
     float llc;            // -0.5 * m * log(2 pi) rounded to f32
-    const void* xs;       // split-f16 xhat rows [T][hi NP | lo NP] (k_ks<.., SX>), or null
+    const void* xs;       // split-f16 xhat rows [T][hi NP | lo NP] (k_kx), or null
     const float* xu;      // [T] power-of-two row scales of xs
+    const float* xc;      // [NP] power-of-two column scales of xs
 };
 
 // rows per k_rows tile for a hidden width.  128-wide layers: 32 rows keep the f32
@@ -911,7 +912,7 @@ RowArgs row_args(const mjrl_shape* s, const mjrl_rows* r, int64_t T) {
     ra.xhat = r->xhat; ra.act = r->act; ra.adv = r->adv; ra.adv_vpg = r->adv_vpg;
     ra.a0 = r->a0; ra.a1 = r->a1; ra.mu0 = r->mu0; ra.ll0 = r->ll0;
     ra.gu0 = r->gu0; ra.gu1 = r->gu1; ra.gp = r->gp;
-    ra.xs = r->xs; ra.xu = r->xu;
+    ra.xs = r->xs; ra.xu = r->xu; ra.xc = r->xc;
     ra.llc = (float)(-0.5 * (double)s->m * log(2.0 * M_PI));
     return ra;
 }
@@ -958,10 +959,10 @@ inline int grad_slices(const mjrl_shape* s, int64_t T) {
 // the split-f16 first layer additionally needs NP % 128 == 0 (chunk swizzle)
 bool ksx_supported(const mjrl_shape* s) { return ks_supported(s) && s->np % 128 == 0; }
 
-template <int MP, int KG, int MODE, bool SX>
+template <int MP, int KG, int MODE>
 int launch_ks_t(const RowArgs& ra, const FOut& fo, int grid, hipStream_t st) {
-    using L = KLayout<MP, KG, SX>;
-    auto fn = k_ks<MP, KG, MODE, SX>;
+    using L = KLayout<MP, KG>;
+    auto fn = k_ks<MP, KG, MODE>;
     static bool attr = false;
     if (!attr) {
         hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, L::bytes);
@@ -986,23 +987,12 @@ int launch_kx_t(const RowArgs& ra, const FOut& fo, int grid, hipStream_t st) {
     return (int)hipGetLastError();
 }
 
-// MJRL_AMD_SPLIT_LAYERS=1 keeps the 64-wide layers of the split path on exact f32
-// (k_ks<.., SX>: only the first layer split), for A/B measurement
-static bool first_layer_only() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("MJRL_AMD_SPLIT_LAYERS");
-        v = (e && e[0] == '1') ? 1 : 0;
-    }
-    return v == 1;
-}
-
-// rows given as split-f16 (ra.xs) run the all-split kernel k_kx (or k_ks<.., SX>);
-// f32 xhat the exact-f32 k_ks
+// rows given as split-f16 (ra.xs) run the all-split kernel k_kx; f32 xhat the
+// exact-f32 k_ks
 template <int MODE>
 int launch_ks(const mjrl_shape* s, const RowArgs& ra, const FOut& fo, int grid, hipStream_t st) {
     const int kg = s->np / 32;
-    if (ra.xs && !first_layer_only()) {
+    if (ra.xs) {
 #define MJRL_K(MP_, KG_) \
     if (s->mp == MP_ && kg == KG_) return launch_kx_t<MP_, KG_, MODE>(ra, fo, grid, st);
 #define MJRL_KN(MP_) MJRL_K(MP_, 4) MJRL_K(MP_, 8) MJRL_K(MP_, 12)
@@ -1012,18 +1002,8 @@ int launch_ks(const mjrl_shape* s, const RowArgs& ra, const FOut& fo, int grid, 
 #undef MJRL_K
         return MJRL_ESHAPE;
     }
-    if (ra.xs) {
 #define MJRL_K(MP_, KG_) \
-    if (s->mp == MP_ && kg == KG_) return launch_ks_t<MP_, KG_, MODE, true>(ra, fo, grid, st);
-#define MJRL_KN(MP_) MJRL_K(MP_, 4) MJRL_K(MP_, 8) MJRL_K(MP_, 12)
-        MJRL_KN(16)
-        MJRL_KN(32)
-#undef MJRL_KN
-#undef MJRL_K
-        return MJRL_ESHAPE;
-    }
-#define MJRL_K(MP_, KG_) \
-    if (s->mp == MP_ && kg == KG_) return launch_ks_t<MP_, KG_, MODE, false>(ra, fo, grid, st);
+    if (s->mp == MP_ && kg == KG_) return launch_ks_t<MP_, KG_, MODE>(ra, fo, grid, st);
 #define MJRL_KN(MP_) MJRL_K(MP_, 2) MJRL_K(MP_, 4) MJRL_K(MP_, 6) MJRL_K(MP_, 8) MJRL_K(MP_, 12)
     MJRL_KN(16)
     MJRL_KN(32)
@@ -1086,7 +1066,7 @@ int run_fused(int mode, const mjrl_shape* s, const mjrl_rows* r, int64_t T, cons
 int run_gather(const mjrl_shape* s, const mjrl_rows* r, int64_t T, const mjrl_scratch* sc, const double* lspart,
                const int32_t* done, float* gsum, hipStream_t st, CgZ cz = CgZ{}) {
     const int S = grad_slices(s, T);
-    if (acc_path(s, T) == 2 && r->xs && !first_layer_only()) {   // k_kx: flat slab layout
+    if (acc_path(s, T) == 2 && r->xs) {   // k_kx: flat slab layout
         const int d_mu = s->d - s->m;
         hipLaunchKernelGGL(k_gather_flat, dim3((s->d + 63) / 64), dim3(64 * GATHER_WAVES), 0, st, sc->wpart, S, d_mu,
                            s->d, lspart, ks_grid(T), s->mp, gsum, done, cz);
@@ -1143,7 +1123,7 @@ int run_wgrad_only(const mjrl_shape* s, const mjrl_rows* r, int64_t T, const mjr
 bool rows_ok(const mjrl_shape* s, const mjrl_rows* r) {
     if (!s || !r || r->T < 0) return false;
     // split-f16 rows (xs + xu) only feed the K-split kernel; every other path reads f32 xhat
-    if (r->xs ? (!r->xu || !ksx_supported(s)) : !r->xhat) return false;
+    if (r->xs ? (!r->xu || !r->xc || !ksx_supported(s)) : !r->xhat) return false;
     if (s->h0 && (!r->a0 || !r->a1 || !r->gu0 || !r->gu1)) return false;
     return r->gp != nullptr;
 }

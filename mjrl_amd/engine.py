@@ -438,9 +438,11 @@ class UpdateEngine:
         self.ws = {}
         w = self.ws
         if self.split:
-            # split-f16 rows [hi np | lo np] + power-of-two row scales (mjrl_rows.xs / xu)
+            # split-f16 rows [hi np | lo np] + power-of-two row and column scales
+            # (mjrl_rows.xs / xu / xc)
             w["xs"] = torch.empty((T_all, 2 * s.np), dtype=torch.float16, device=dev)
             w["xu"] = torch.empty(T_all, **f32)
+            w["xc"] = torch.empty(s.np, **f32)
         else:
             w["xhat"] = torch.empty((T_all, s.np), **f32)
         w["act32"] = torch.empty((T_all, s.m), **f32)
@@ -487,7 +489,7 @@ class UpdateEngine:
                        ("mu0", "mu0"), ("ll0", "ll0"), ("gu0", "gu0"), ("gu1", "gu1"), ("gp", "gp")):
             setattr(r, k, w[key].data_ptr())
         if self.split:
-            r.xs, r.xu = w["xs"].data_ptr(), w["xu"].data_ptr()
+            r.xs, r.xu, r.xc = w["xs"].data_ptr(), w["xu"].data_ptr(), w["xc"].data_ptr()
         else:
             r.xhat = w["xhat"].data_ptr()
         r.adv_vpg = adv_vpg.data_ptr()
@@ -525,9 +527,13 @@ class UpdateEngine:
         if f32 != (act.dtype == torch.float32):
             raise ValueError("observations and actions must be staged in the same dtype")
         if self.split:
+            # column scales of this batch (one read pass), then the split rows
+            cs = self.lib.mjrl_obs_colscale_f32 if f32 else self.lib.mjrl_obs_colscale
+            _lib.check(cs(_lib.ptr(obs), T, sp, _lib.ptr(ins), _lib.ptr(isc), _lib.ptr(w["xc"]), st),
+                       "mjrl_obs_colscale")
             fn = self.lib.mjrl_pack_batch_split_f32 if f32 else self.lib.mjrl_pack_batch_split
-            _lib.check(fn(_lib.ptr(obs), _lib.ptr(act), T, sp, _lib.ptr(ins), _lib.ptr(isc), _lib.ptr(w["xs"]),
-                          _lib.ptr(w["xu"]), _lib.ptr(w["act32"]), st), "mjrl_pack_batch_split")
+            _lib.check(fn(_lib.ptr(obs), _lib.ptr(act), T, sp, _lib.ptr(ins), _lib.ptr(isc), _lib.ptr(w["xc"]),
+                          _lib.ptr(w["xs"]), _lib.ptr(w["xu"]), _lib.ptr(w["act32"]), st), "mjrl_pack_batch_split")
         else:
             fn = self.lib.mjrl_pack_batch_f32 if f32 else self.lib.mjrl_pack_batch
             _lib.check(fn(_lib.ptr(obs), _lib.ptr(act), T, sp, _lib.ptr(ins), _lib.ptr(isc), _lib.ptr(w["xhat"]),

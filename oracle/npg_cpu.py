@@ -361,15 +361,25 @@ def cg_rows(c):
     return [np.random.choice(N, size=int(frac * N)) for _ in range(k)]
 
 
-def regen_inputs(seed, n, m, lengths):
+def regen_inputs(seed, n, m, lengths, col_scale=None, spiky=None, act_scale=None):
     """The synthetic paths of tests/golden/make_golden.py:make_paths, replayed from
     np.random.RandomState(seed) (legacy stream, stable across numpy versions): per
-    path obs randn(H, n) and act randn(H, m) rounded to f32, then rewards randn(H)."""
+    path obs randn(H, n) (spiky columns zeroed where |draw| <= 1.5, times the column
+    scales) and act randn(H, m) (times act_scale) rounded to f32, then rewards
+    randn(H)."""
     rs = np.random.RandomState(int(seed))
     obs, act, rew = [], [], []
     for H in lengths:
-        obs.append(rs.randn(int(H), n).astype(np.float32))
-        act.append(rs.randn(int(H), m).astype(np.float32))
+        o = rs.randn(int(H), n)
+        if spiky is not None:
+            o[:, spiky] *= np.abs(o[:, spiky]) > 1.5
+        if col_scale is not None:
+            o = o * col_scale
+        obs.append(o.astype(np.float32))
+        a = rs.randn(int(H), m)
+        if act_scale is not None:
+            a = a * act_scale
+        act.append(a.astype(np.float32))
         rew.append(rs.randn(int(H)))
     return np.concatenate(obs), np.concatenate(act), np.concatenate(rew)
 
@@ -396,7 +406,10 @@ def load_case(path):
     c = {k: z[k] for k in z.files}
     if "gen_seed" in c:
         n, m = int(c["n"]), int(c["m"])
-        c["obs"], c["act"], c["rewards"] = regen_inputs(c["gen_seed"], n, m, c["lengths"])
+        c["obs"], c["act"], c["rewards"] = regen_inputs(
+            c["gen_seed"], n, m, c["lengths"], col_scale=c.get("col_scale"),
+            spiky=c["spiky"].astype(bool) if "spiky" in c else None,
+            act_scale=float(c["act_scale"]) if "act_scale" in c else None)
         if _sha(c["obs"], c["act"], c["rewards"]) != str(c["inputs_sha256"]):
             raise ValueError("%s: regenerated inputs do not match the fixture's checksum" % path)
         lam = None if np.isnan(c["gae_lambda"]) else float(c["gae_lambda"])

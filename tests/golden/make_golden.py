@@ -61,14 +61,26 @@ OUT = os.path.dirname(os.path.abspath(__file__))
 MEAN_ROWS = 2000   # regenerated cases keep the first MEAN_ROWS rows of mean0 / ll0
 
 
-def make_paths(rs, n, m, lengths, terminated):
+def make_paths(rs, n, m, lengths, terminated, col_scale=None, spiky=None, act_scale=None):
     """Synthetic paths in the sampler wire format (samplers/base_sampler.py:76-83).
     obs / act are drawn as f32-representable doubles so the fixture can store them
-    as float32 losslessly."""
+    as float32 losslessly.  col_scale: per-column observation scales; spiky: a
+    column mask whose entries are zeroed where the draw is below 1.5 in magnitude
+    (contact-force-like columns: mostly zero, occasionally large); act_scale: a
+    factor on the actions (the draw order is unchanged by all three, so
+    oracle.npg_cpu.regen_inputs replays them)."""
     paths = []
     for H, term in zip(lengths, terminated):
-        obs = rs.randn(H, n).astype(np.float32).astype(np.float64)
-        act = rs.randn(H, m).astype(np.float32).astype(np.float64)
+        obs = rs.randn(H, n)
+        if spiky is not None:
+            obs[:, spiky] *= np.abs(obs[:, spiky]) > 1.5
+        if col_scale is not None:
+            obs = obs * col_scale
+        obs = obs.astype(np.float32).astype(np.float64)
+        act = rs.randn(H, m)
+        if act_scale is not None:
+            act = act * act_scale
+        act = act.astype(np.float32).astype(np.float64)
         rew = rs.randn(H)
         paths.append(dict(observations=obs, actions=act, rewards=rew,
                           agent_infos={}, env_infos={}, terminated=bool(term)))
@@ -146,6 +158,7 @@ def concat(paths, key):
 
 
 ONLY = set(sys.argv[1:])   # optional: regenerate only the named cases
+SEED_CLAMP = 60           # a seed whose NPG step takes log_std below -3 (checked in run_case)
 
 
 def run_case(name, reverse_alt=True, **kw):
@@ -203,6 +216,16 @@ def _err64(name, out):
         z["err64_x"], z["err64_theta"], z["err64_alpha"], z["err64_kl"], z["err64_surr"]))
 
 
+def _colrel(a, b, h0, n):
+    """Largest per-column error of the W0 block (h0 x n, the first h0 n entries of a
+    flat gradient): max over columns k of max_j |a[j,k] - b[j,k]| / max_j |b[j,k]|."""
+    a = np.asarray(a, np.float64)[:h0 * n].reshape(h0, n)
+    b = np.asarray(b, np.float64)[:h0 * n].reshape(h0, n)
+    den = np.abs(b).max(0)
+    ok = den > 0
+    return float((np.abs(a - b).max(0)[ok] / den[ok]).max())
+
+
 def _nrel(a, b):
     a = np.asarray(a, np.float64)
     b = np.asarray(b, np.float64)
@@ -212,7 +235,8 @@ def _nrel(a, b):
 def _run(name, *, n, m, hidden, lengths, terminated, algo, algo_kwargs,
          gamma=0.995, gae_lambda=0.97, seed=123, policy_seed=0,
          log_std=None, transforms=None, demo=None, linear=False,
-         baseline_fit=True, alt=None, reverse=False, np_seed=None, regen=False, perm_seed=None, exact_ls=False):
+         baseline_fit=True, alt=None, reverse=False, np_seed=None, regen=False, perm_seed=None, exact_ls=False,
+         col_scale=None, spiky=None, act_scale=None, w0_col_scale=False):
     rs = np.random.RandomState(seed)
     spec = EnvSpec(n, m, max(lengths), 1)
     if linear:
@@ -226,7 +250,14 @@ def _run(name, *, n, m, hidden, lengths, terminated, algo, algo_kwargs,
         th = policy.get_param_values()
         th[-m:] = log_std
         policy.set_param_values(th, set_new=True, set_old=True)
-    paths = make_paths(rs, n, m, lengths, terminated)
+    if w0_col_scale:
+        # a first layer adapted to the feature scales: W0 column k / col_scale[k], so
+        # every column contributes O(1) to the pre-activations (none saturate)
+        th = policy.get_param_values()
+        h0 = hidden[0]
+        th[:h0 * n] = (th[:h0 * n].reshape(h0, n) / col_scale[None, :]).ravel()
+        policy.set_param_values(th, set_new=True, set_old=True)
+    paths = make_paths(rs, n, m, lengths, terminated, col_scale=col_scale, spiky=spiky, act_scale=act_scale)
     demo_paths = None
     if demo is not None:
         demo_paths = make_paths(rs, n, m, demo, [True] * len(demo))
@@ -281,8 +312,14 @@ def _run(name, *, n, m, hidden, lengths, terminated, algo, algo_kwargs,
         rec.cg = dict(b=rec.vpg[0], p=np.zeros((0, policy.d), np.float32), z=np.zeros((0, policy.d), np.float32),
                       x=rec.vpg[0])
 
+    colspread = lambda k, v: (max(_colrel(a[k], v, hidden[0], n) for a in alt)
+                              if alt and not linear else 0.0)
     out = dict(
         spread_x=max(_nrel(a["cg_x"], rec.cg["x"]) for a in alt) if alt else 0.0,
+        # the reference's own per-W0-column change (threads, path orders) of the VPG
+        # and of HVP(v): the per-column tolerance of the split-row parity test
+        spread_vpg_col=colspread("vpg_grad", rec.vpg[0]),
+        spread_hvp_col=colspread("hvp_out", hvp_out),
         spread_theta=max(_nrel(a["theta1"], theta1) for a in alt) if alt else 0.0,
         spread_kl=max(abs(a["log_kl_dist"] / agent.logger.log["kl_dist"][-1] - 1) for a in alt) if alt else 0.0,
         spread_alpha=max(abs(float(a["log_alpha"]) / agent.logger.log["alpha"][-1] - 1) for a in alt) if alt else 0.0,
@@ -312,6 +349,12 @@ def _run(name, *, n, m, hidden, lengths, terminated, algo, algo_kwargs,
         base_stats=np.array(base_stats, dtype=np.float64),
         running_score=agent.running_score,
     )
+    if col_scale is not None:
+        out["col_scale"] = np.asarray(col_scale, np.float64)
+    if spiky is not None:
+        out["spiky"] = np.asarray(spiky, np.uint8)
+    if act_scale is not None:
+        out["act_scale"] = np.float64(act_scale)
     if regen:
         # large cases: the inputs are NOT stored.  oracle.npg_cpu.regen_inputs replays
         # make_paths' RandomState stream from gen_seed and load_case checks the
@@ -414,6 +457,28 @@ def main():
     run_case("c4_humanoid", n=376, m=17, hidden=(64, 64),
              lengths=[1000] * 60, terminated=[False] * 60, algo="npg",
              algo_kwargs=dict(normalized_step_size=0.01), regen=True)
+    # C4s: the Humanoid shape with observation columns of very different scales
+    # (10^U(-4, 3), every 7th column contact-force-like: mostly zero), a first layer
+    # adapted to them (W0 column k / scale k) and 60 x 1000 rows: each row spans
+    # ~12 decades, the case a per-row block-floating-point row format gets wrong
+    # for its small columns (pins the split rows' column scales)
+    crs = np.random.RandomState(404)
+    col_scale = 10.0 ** crs.uniform(-4, 3, size=376)
+    spiky = np.zeros(376, bool)
+    spiky[::7] = True
+    run_case("c4_humanoid_scaled", n=376, m=17, hidden=(64, 64),
+             lengths=[1000] * 60, terminated=[False] * 60, algo="npg",
+             algo_kwargs=dict(normalized_step_size=0.01), regen=True, seed=404,
+             col_scale=col_scale, spiky=spiky, w0_col_scale=True)
+    # C2l: log_std starting AT min_log_std (-3) with a step that drives part of it
+    # below: set_param_values clamps it (gaussian_mlp.py:74-78,86-88), and the
+    # post-step surrogate / KL are evaluated at the clamped parameters
+    out = run_case("c2_logstd_clamp", n=8, m=2, hidden=(64, 64), lengths=[200] * 10,
+                   terminated=[False] * 10, algo="npg", algo_kwargs=dict(normalized_step_size=0.5),
+                   seed=SEED_CLAMP, log_std=np.array([-3.0, -3.0]), act_scale=0.05)
+    if out is not None:
+        step = out["theta0"][-2:] + out["log_alpha"] * out["cg_x"][-2:]
+        assert step.min() < -3.0 - 1e-3 and out["theta1"][-2:].min() == -3.0, (step, out["theta1"][-2:])
     # C5: door shape, DAPG with BC-style in/out transformations and demos
     rs = np.random.RandomState(9)
     n, m = 39, 28

@@ -608,7 +608,7 @@ def test_pack_split_f32_input_matches_f64(n):
             a = torch.from_numpy(act).to(dev, dt)
             eng._pack(o, a, T, _lib_stream())
             torch.cuda.synchronize()
-            outs.append([eng.ws[k][:T].cpu().clone() for k in ("xs", "xu", "act32")])
+            outs.append([eng.ws[k][:T].cpu().clone() for k in ("xs", "xu", "xc", "act32")])
         for x64, x32 in zip(*outs):
             assert torch.equal(x64.view(torch.int16) if x64.dtype == torch.float16 else x64,
                                x32.view(torch.int16) if x32.dtype == torch.float16 else x32)

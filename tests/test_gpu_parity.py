@@ -158,3 +158,45 @@ def test_fvp_and_teacher_forced_cg(name, precision):
     for p, z, rows in zip(c["cg_p"], c["cg_z"], O.cg_rows(c)):
         zz = eng.fvp(torch.from_numpy(p.astype(np.float32)).to(dev), damping=damping, idx=ix(rows)).cpu().numpy()
         assert nrel(zz, z) < 1e-5, nrel(zz, z)
+
+
+def colrel(a, b, h0, n):
+    """Per-W0-column error: max over columns k (one observation feature) of
+    max_j |a[j,k] - b[j,k]| / max_j |b[j,k]|, over the first h0 n entries (W0)."""
+    a = np.asarray(a, np.float64)[:h0 * n].reshape(h0, n)
+    b = np.asarray(b, np.float64)[:h0 * n].reshape(h0, n)
+    den = np.abs(b).max(0)
+    ok = den > 0
+    return float((np.abs(a - b).max(0)[ok] / den[ok]).max())
+
+
+COL_CASES = [n for n in ("c4_humanoid_scaled", "c4_humanoid") if n in CASES]
+
+
+@pytest.mark.parametrize("name,precision", [(n, p) for n in COL_CASES for p in (None, "f32")])
+def test_w0_columns_match_reference(name, precision):
+    """Element-wise parity of the split rows: the VPG and F v (fixed v) of every W0
+    column — one observation feature — against the reference and against an fp64
+    evaluation (the oracle in float64 on the same inputs), per column, not in norm.
+    c4_humanoid_scaled's observation columns span 10^-4 .. 10^3.
+    Bar: against the reference, max(3 x the reference's own per-column spread
+    (1 vs 8 / 3 threads, path orders), 1e-5); against fp64, within 2x the
+    reference's own fp32 per-column error + 1e-6."""
+    c, kw, eng, res = run_case(name, precision)
+    from oracle import npg_cpu as O
+    n, h0 = int(c["n"]), int(c["hidden_t"][0])
+    dev = torch.device("cuda:0")
+    g = eng.vec["g"].cpu().numpy()
+    fv = eng.fvp(torch.from_numpy(c["hvp_v"]).to(dev), damping=kw.get("damping", 1e-4)).cpu().numpy()
+    pol = O.Policy(n, int(c["m"]), c["hidden_t"], c["theta0"].astype(np.float64), c["transforms"],
+                   dtype=torch.float64)
+    g64 = pol.flat_vpg(c["obs64"], c["act64"], c["adv_whitened"])
+    fv64 = pol.fvp(c["obs64"], c["act64"], c["hvp_v"].astype(np.float64), kw.get("damping", 1e-4))
+    e = dict(vpg_ref=colrel(g, c["vpg_grad"], h0, n), fvp_ref=colrel(fv, c["hvp_out"], h0, n),
+             vpg_64=colrel(g, g64, h0, n), fvp_64=colrel(fv, fv64, h0, n),
+             ref_vpg_64=colrel(c["vpg_grad"], g64, h0, n), ref_fvp_64=colrel(c["hvp_out"], fv64, h0, n))
+    print(name, precision, {k: "%.2e" % v for k, v in e.items()})
+    assert e["vpg_ref"] <= max(3 * float(c["spread_vpg_col"]), 1e-5), e
+    assert e["fvp_ref"] <= max(3 * float(c["spread_hvp_col"]), 1e-5), e
+    assert e["vpg_64"] <= 2 * e["ref_vpg_64"] + 1e-6, e
+    assert e["fvp_64"] <= 2 * e["ref_fvp_64"] + 1e-6, e

@@ -1,8 +1,9 @@
 """GPU tests of the split-f16 first layer (precision='split').
 
-  - the packed rows: (hi + lo) * xu reproduces the f32 xhat of
-    mjrl_pack_batch to <= 2^-23 of the row scale, on rows with columns spanning
-    10^-6 .. 10^3 and with the input normalisation;
+  - the packed rows: (hi + lo) * xu * xc reproduces the f32 xhat of
+    mjrl_pack_batch element by element to 2^-23 |xhat| + 2^-38 of the column's
+    max, on rows with columns spanning 10^-6 .. 10^3 and with the input
+    normalisation;
   - accuracy against fp64 truth: the VPG, the Fisher-vector product and the
     post-step surrogate / KL of the split kernels are compared with an fp64
     evaluation of the same closed forms (torch float64 on the GPU, jvp / vjp of
@@ -34,6 +35,10 @@ def _obs(T, rs):
 
 
 def test_pack_split_roundtrip():
+    """The split rows carry the f32 xhat of mjrl_pack_batch to the element bound of
+    common.h: |xc xu (hi + lo) - xhat| <= 2^-23 |xhat| + 2^-38 colmax_k, with xc a
+    power of two per column (colmax / xc in [1/2, 1)) and xu one per row (the row's
+    max |xhat / xc| / xu in [2^14, 2^15))."""
     from mjrl_amd import _lib
     from mjrl_amd.engine import UpdateEngine
     rs = np.random.RandomState(0)
@@ -49,13 +54,22 @@ def test_pack_split_roundtrip():
         x = ef.ws["xhat"][:T].double().cpu().numpy()
         xs = es.ws["xs"][:T].float().double().cpu().numpy()
         xu = es.ws["xu"][:T].double().cpu().numpy()
+        xc = es.ws["xc"].double().cpu().numpy()
         np_ = ef.shape.np
-        rec = (xs[:, :np_] + xs[:, np_:]) * xu[:, None]
-        # power-of-two row scales with |xhat / xu| < 1
-        assert np.all(np.log2(xu) == np.round(np.log2(xu)))
-        assert np.all(np.abs(x).max(1) < xu) and np.all(np.abs(x).max(1) >= xu / 2)
-        err = np.abs(rec - x).max(1) / xu
-        assert err.max() <= 2.0 ** -23, err.max()
+        pow2 = lambda a: np.all(np.log2(a) == np.round(np.log2(a)))
+        assert pow2(xu) and pow2(xc)
+        colmax = np.abs(x).max(0)
+        nz = colmax > 0
+        assert np.all(colmax[nz] < xc[nz]) and np.all(colmax[nz] >= xc[nz] / 2) and np.all(xc[~nz] == 1)
+        assert colmax[N] == 1.0 and xc[N] == 2.0          # the bias column
+        y = x / xc[None, :]
+        assert np.all(np.abs(y).max(1) / xu >= 2.0 ** 14) and np.all(np.abs(y).max(1) / xu < 2.0 ** 15)
+        rec = (xs[:, :np_] + xs[:, np_:]) * xu[:, None] * xc[None, :]
+        err = np.abs(rec - x)
+        bound = 2.0 ** -23 * np.abs(x) + 2.0 ** -38 * colmax[None, :]
+        assert np.all(err <= bound), (err / np.maximum(bound, 1e-300)).max()
+        # a [1/2, 1) row block (the round-2 form) breaks that bound on these rows
+        assert np.abs(x).max() / np.abs(x[x != 0]).min() > 2.0 ** 30
         assert np.array_equal(es.ws["act32"][:T].cpu().numpy(), ef.ws["act32"][:T].cpu().numpy())
         _lib.load()
 

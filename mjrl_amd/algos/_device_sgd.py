@@ -79,8 +79,14 @@ class DeviceTrainer:
         dev = self.device
         f = lambda v, fill, k: torch.from_numpy(np.float32(v)).to(dev) if v is not None else \
             torch.full((k,), float(fill), device=dev)
-        self._tf = (f(t["in_shift"], 0.0, self.policy.n), f(t["in_scale"], 1.0, self.policy.n),
-                    f(t["out_shift"], 0.0, self.policy.m), f(t["out_scale"], 1.0, self.policy.m))
+        tf = (f(t["in_shift"], 0.0, self.policy.n), f(t["in_scale"], 1.0, self.policy.n),
+              f(t["out_shift"], 0.0, self.policy.m), f(t["out_scale"], 1.0, self.policy.m))
+        if self._tf is None:
+            self._tf = tf
+        else:
+            # copied into the existing buffers: a captured step reads them by address
+            for d, s in zip(self._tf, tf):
+                d.copy_(s)
 
     def push(self):
         """device params + optimizer state -> the CPU policy / optimizer (the

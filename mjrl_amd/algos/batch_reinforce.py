@@ -171,10 +171,12 @@ class BatchREINFORCE:
     def _sample_shard(self, trajectory_sampler, batch_sampler, comm, N, sample_mode, env_name, T, num_cpu):
         """This rank's share of the sampling.  'trajectories': shard_count(N) paths
         with pegasus seed `seed + first` (the offset trajectory_sampler.py:40-44
-        gives worker i); 'samples': ceil(N / world) timesteps with seed `seed + r N`
-        (disjoint per rank: batch_sampler.py:41-48 advances its seed by at most
-        the paths it draws, fewer than N).  num_cpu='max' becomes this rank's share
-        of the host cores."""
+        gives worker i); 'samples': n_r = ceil(N / world) timesteps with seed
+        `seed + r n_r`, rank r's slot of the iteration's N-seed window (the
+        reference itself advances the seed by N per iteration, batch_reinforce.py:84;
+        an offset of r N would hand rank r - 1 of the next iteration exactly rank
+        r's starting seed of this one).  num_cpu='max' becomes this rank's share of
+        the host cores."""
         if num_cpu is None or num_cpu == "max":
             num_cpu = max(1, mp.cpu_count() // comm.world_size)
         if sample_mode == "trajectories":
@@ -185,7 +187,7 @@ class BatchREINFORCE:
             seed = self.seed + first if self.seed is not None else None
             return trajectory_sampler.sample_paths_parallel(n_r, self.policy, T, env_name, seed, num_cpu)
         n_r = int(np.ceil(N / comm.world_size))
-        seed = self.seed + comm.rank * N if self.seed is not None else None
+        seed = self.seed + comm.rank * n_r if self.seed is not None else None
         return batch_sampler.sample_paths(n_r, self.policy, T, env_name=env_name, pegasus_seed=seed,
                                           num_cpu=num_cpu)
 

@@ -81,11 +81,14 @@ class BC:
             return -torch.mean(tr.log_likelihood(O.index_select(0, idx), A.index_select(0, idx)))
 
         ts = timer.time()
+        # the captured step reads this call's O / A: a new key per call (an id() of a
+        # freed tensor can come back for the next call's data)
+        self._ncall = getattr(self, "_ncall", 0) + 1
         for ep in range(self.epochs):
             self.logger.log_kv("epoch", ep)
             self.logger.log_kv("loss", np.float32(full_loss()))
             self.logger.log_kv("time", timer.time() - ts)
-            tr.epoch(("bc", id(O)), mb_loss,
+            tr.epoch(("bc", self._ncall), mb_loss,
                      choice_batches(num_samples, self.mb_size, tr.device))
         tr.push()
         params_after_opt = self.policy.get_param_values()

@@ -170,24 +170,29 @@ class MLPBaseline:
         saved = [p.detach().clone() for p in model.parameters()]
         saved_state = {p: {k: v.clone() for k, v in opt.state[p].items()} for p in model.parameters()
                        if opt.state.get(p)}
-        s = torch.cuda.Stream(device=dev)
-        s.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(s):
-            body()
-        torch.cuda.current_stream(dev).wait_stream(s)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            body()
-        with torch.no_grad():
-            for p, v in zip(model.parameters(), saved):
-                p.copy_(v)
-            for p in model.parameters():
-                if p in saved_state:
-                    for k, v in saved_state[p].items():
-                        opt.state[p][k].copy_(v)
-                else:
-                    for k, v in opt.state[p].items():
-                        v.zero_()
+        try:
+            s = torch.cuda.Stream(device=dev)
+            s.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(s):
+                body()
+            torch.cuda.current_stream(dev).wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                body()
+        finally:
+            # restored whether or not the capture succeeded (a failed capture falls
+            # back to eager steps, which must start from the untouched state)
+            with torch.no_grad():
+                for p, v in zip(model.parameters(), saved):
+                    p.copy_(v)
+                for p in model.parameters():
+                    if p in saved_state:
+                        for k, v in saved_state[p].items():
+                            opt.state[p][k].copy_(v)
+                    else:
+                        for k, v in opt.state[p].items():
+                            if torch.is_tensor(v):
+                                v.zero_()
         st.update(graph=g, gkey=key, idx=idx)
         return st
 

@@ -436,6 +436,11 @@ class UpdateEngine:
         f32 = dict(dtype=torch.float32, device=dev)
         f64 = dict(dtype=torch.float64, device=dev)
         self.ws = {}
+        # workspace generation: part of the update-graph key (an id() of a freed dict
+        # can come back for the next workspace)
+        self._ws_gen = getattr(self, "_ws_gen", 0) + 1
+        if hasattr(self, "_gstate"):
+            self._gstate.clear()   # a captured graph reads the old workspace
         w = self.ws
         if self.split:
             # split-f16 rows [hi np | lo np] + power-of-two row and column scales
@@ -854,7 +859,7 @@ class UpdateEngine:
         ptrs = tuple(0 if t is None else t.data_ptr() for t in (
             batch.obs, batch.act, batch.rewards, batch.baseline, batch.path_off, batch.terminated, batch.advantages)
             + tuple(self.transforms))
-        return (ptrs, batch.T, batch.T_demo, batch.P, float(T_global), id(self.ws), self.kernel_timing is not None,
+        return (ptrs, batch.T, batch.T_demo, batch.P, float(T_global), self._ws_gen, self.kernel_timing is not None,
                 tuple(args))
 
     def _maybe_capture(self, key, launch, theta, delta, T_global):
@@ -880,11 +885,13 @@ class UpdateEngine:
                 graph_prof = self.kernel_timing
                 self.kernel_timing = prof_saved
             gs.update(key=key, graph=g, theta_in=theta_in, timing=out[4], delta=delta, prof=graph_prof)
+            self.st = _lib.stream_ptr()    # launch() cached the capture stream
             return
         import warnings
         warnings.warn("mjrl_amd: hipGraph capture of the update failed (%s); staying eager" % (err,))
         self.graphs = False
         gs.clear()
+        self.st = _lib.stream_ptr()
 
     def graph_kernel_timing(self):
         """(start, accumulate done, gather done) external events of every FVP of the

@@ -509,6 +509,25 @@ def test_bc_on_gpu_matches_reference():
     assert np.linalg.norm(policy.get_param_values() - ref) <= 1e-3 * np.linalg.norm(ref)
 
 
+def test_bc_train_twice_on_gpu_matches_cpu():
+    """A second BC.train() on new expert data (the same trainer, the Adam state
+    carried over) replays a graph captured for THAT call's rows, not the first
+    call's: the GPU run tracks the CPU-device run of the same sequence."""
+    from test_bc_ppo import run_bc
+    out = {}
+    for dev in ("cpu", "cuda:0"):
+        bc, policy, z = run_bc(dev)
+        rs = np.random.RandomState(99)
+        bc.expert_paths = [dict(observations=p["observations"] * 0.5 + rs.randn(*p["observations"].shape) * 0.1,
+                                actions=p["actions"][::-1].copy()) for p in bc.expert_paths]
+        np.random.seed(123)
+        bc.train()
+        out[dev] = (policy.get_param_values(), np.array(bc.logger.log["loss"], dtype=np.float64))
+    np.testing.assert_allclose(out["cuda:0"][1], out["cpu"][1], rtol=1e-4)
+    ref = out["cpu"][0]
+    assert np.linalg.norm(out["cuda:0"][0] - ref) <= 1e-3 * np.linalg.norm(ref)
+
+
 def test_ppo_on_gpu_matches_reference():
     """PPO.train_from_paths (ppo_clip.py:57-120) twice (the Adam state carries
     over), against the reference run: base_stats exact; parameters in norm to

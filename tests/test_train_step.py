@@ -164,11 +164,16 @@ def test_train_step_sharded_two_ranks(kind):
 def test_train_step_sharded_samples_mode():
     N = 250
     out = _sharded("linear", N, "samples")
+    starts = []
     for it in range(2):
         base = 1000 + N * it
         assert out[0][it]["calls"] == [("samples", 125, base, 1)]
-        assert out[1][it]["calls"] == [("samples", 125, base + N, 1)]
+        assert out[1][it]["calls"] == [("samples", 125, base + 125, 1)]   # rank 1's slot of the window
         assert out[0][it]["seed"] == base + N
+        starts += [out[r][it]["calls"][0][2] for r in range(2)]
+    # no rank starts where any rank started before (the next iteration's rank 0 vs
+    # this one's rank 1 included): no two shards replay the same env resets
+    assert len(set(starts)) == len(starts), starts
 
 
 def test_dapg_demo_share():

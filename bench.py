@@ -136,10 +136,21 @@ def pmc_traffic(kernel_key):
     if not files:
         return None, None
     data = json.load(open(files[-1]))
+    src = os.path.relpath(files[-1], ROOT)
     for name, v in data.items():
-        if kernel_key in name:
-            return v["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+        if isinstance(v, dict) and kernel_key in name:
+            # the commit the PMC passes measured (recorded when the summary was filed)
+            head = data.get("_measured_at_commit")
+            return v["hbm_bytes_per_launch"], src + (" @ " + head if head else "")
     return None, None
+
+
+def _commit():
+    """The commit this tree was stamped with before a GPU run (tools/stamp_head.sh), if any."""
+    try:
+        return open(os.path.join(ROOT, "HEAD_COMMIT")).read().strip() or None
+    except OSError:
+        return None
 
 
 def make_paths(p0, p1, seed=123, cfg=None):
@@ -236,14 +247,38 @@ def update_args(cfg, T_total):
     return upd
 
 
+def _cpu_list(cpus):
+    """'0-15' / '0-7,16-23' form of a CPU id set."""
+    cpus = sorted(cpus)
+    out, a = [], None
+    for i, c in enumerate(cpus):
+        if a is None:
+            a = c
+        if i + 1 == len(cpus) or cpus[i + 1] != c + 1:
+            out.append(str(a) if a == c else "%d-%d" % (a, c))
+            a = None
+    return ",".join(out)
+
+
 def cpu_baseline(rows, base, reps=3, cfg=None):
     """The oracle (CPU restatement of the reference update) on `rows` timesteps,
-    torch on all the host cores this process may use: one warm-up update on a
-    tenth of the sample, then the median of `reps`."""
+    torch on the host cores this process may use, pinned: the process's affinity
+    is narrowed to the first host_cores() CPUs of its allowed set for the
+    duration (and restored), so the threads do not migrate over a box shared with
+    other jobs; the set is recorded.  One warm-up update on a tenth of the sample,
+    then the median of `reps` (>= 3 at Humanoid 1M, >= 10 for the
+    smaller configs)."""
     from oracle import npg_cpu as O
     cfg = cfg or CONFIGS["c4"]
     H, n, m, hidden = cfg["horizon"], cfg["n"], cfg["m"], cfg["hidden"]
     cores = host_cores()
+    saved_aff = None
+    try:
+        saved_aff = os.sched_getaffinity(0)
+        pinned = set(sorted(saved_aff)[:cores])
+        os.sched_setaffinity(0, pinned)
+    except (AttributeError, OSError):
+        pinned = None
     torch.set_num_threads(cores)
     P = max(1, rows // H)
     obs, act, rew = make_paths(0, P, cfg=cfg)
@@ -274,18 +309,28 @@ def cpu_baseline(rows, base, reps=3, cfg=None):
         return time.perf_counter() - t0
 
     log("cpu baseline: %d timesteps on %d threads" % (P * H, cores))
-    one(max(H, (P * H // 10) // H * H))
-    ts = []
-    for i in range(reps):
-        ts.append(one(P * H))
-        log("cpu baseline update %d: %.2f s" % (i + 1, ts[-1]))
+    try:
+        one(max(H, (P * H // 10) // H * H))
+        ts = []
+        for i in range(reps):
+            ts.append(one(P * H))
+            log("cpu baseline update %d: %.2f s" % (i + 1, ts[-1]))
+    finally:
+        if saved_aff is not None:
+            os.sched_setaffinity(0, saved_aff)
     ts.sort()
     dt = ts[len(ts) // 2]
+    full = P * H >= cfg["paths"] * H
     return dict(value=round(P * H / dt, 1), unit="timesteps/s", cores=cores, kind="port", cpu=cpu_model(),
-                sample="%d paths x %d steps (%d timesteps) of the same %s workload, one update "
-                       "(returns + GAE + train_from_paths), oracle/npg_cpu.py on %d torch threads (the process's "
-                       "CPU affinity): median of %d updates %.2f s (all: %s)"
-                       % (P, H, P * H, cfg["workload"], cores, reps, dt, ", ".join("%.2f" % t for t in ts)))
+                affinity=_cpu_list(pinned) if pinned else None, reps=reps, median_s=round(dt, 4),
+                spread=round((ts[-1] - ts[0]) / dt, 4),
+                sample="%s: %d paths x %d steps (%d timesteps) of the %s workload%s, one update (returns + GAE + "
+                       "train_from_paths), oracle/npg_cpu.py on %d torch threads pinned to CPUs %s: median of %d "
+                       "updates %.3f s (all: %s)"
+                       % ("the full batch" if full else "a bounded sample", P, H, P * H, cfg["workload"],
+                          "" if full else " (the rate is the sample's; --cpu-full times the whole batch)",
+                          cores, _cpu_list(pinned) if pinned else "(affinity not settable)", reps, dt,
+                          ", ".join("%.3f" % t for t in ts)))
 
 
 def host_threads():
@@ -362,6 +407,8 @@ def main():
     ap.add_argument("--cpu-rows", type=int, default=200000,
                     help="timesteps of the bounded CPU-baseline sample (c4; the other configs use their full batch)")
     ap.add_argument("--cpu-full", action="store_true", help="CPU baseline on the full batch of the config")
+    ap.add_argument("--cpu-reps", type=int, default=None,
+                    help="timed CPU-baseline updates (default: 3 at c4, 10 for the smaller configs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end-from-host-paths measurement")
     ap.add_argument("--no-f32", action="store_true", help="skip the exact-f32 companion timing")
@@ -542,6 +589,7 @@ def main():
                                algo=cfg["algo"], timesteps=T_total, paths=cfg["paths"], horizon=H,
                                demo_timesteps=cfg.get("demos", 0) * H, cg_iters=CG_ITERS,
                                parallelism="dp%d" % world),
+                   commit=_commit(),
                    hipgraph=bool(graphed), eager_ms_per_step=None if eager_ms is None else round(eager_ms, 3),
                    f32_ms_per_step=None if f32_ms is None else round(f32_ms, 3),
                    roofline=roof)
@@ -550,8 +598,9 @@ def main():
             log("end-to-end from host paths")
             out["e2e_from_host"] = e2e_from_host((p0, p1), eng, th, base, upd, device, cfg)
         if world == 1 and not args.no_cpu_baseline:
-            rows = T_total if (args.cpu_full or args.config != "c4") else args.cpu_rows
-            out["cpu_baseline"] = cpu_baseline(rows, base, cfg=cfg)
+            rows = T_total if (args.cpu_full or args.config != "c4") else min(args.cpu_rows, T_total)
+            reps = args.cpu_reps or (3 if args.config == "c4" else 10)
+            out["cpu_baseline"] = cpu_baseline(rows, base, reps=reps, cfg=cfg)
         print(json.dumps(out))
     if world > 1:
         torch.distributed.destroy_process_group()

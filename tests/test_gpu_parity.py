@@ -180,8 +180,11 @@ def test_w0_columns_match_reference(name, precision):
     evaluation (the oracle in float64 on the same inputs), per column, not in norm.
     c4_humanoid_scaled's observation columns span 10^-4 .. 10^3.
     Bar: against the reference, max(3 x the reference's own per-column spread
-    (1 vs 8 / 3 threads, path orders), 1e-5); against fp64, within 2x the
-    reference's own fp32 per-column error + 1e-6."""
+    (1 vs 8 / 3 threads, path orders), 2e-6); against fp64, at most 1.25x the
+    reference's own fp32 per-column error + 2e-7.  Measured (r03b): split VPG
+    6.3e-7 / F v 5.4e-7 per column against fp64, the reference 1.2e-6 / 8.0e-7;
+    the round-2 row format (one block per row) is 0.73 on these rows
+    (tests/test_split_format.py)."""
     c, kw, eng, res = run_case(name, precision)
     from oracle import npg_cpu as O
     n, h0 = int(c["n"]), int(c["hidden_t"][0])
@@ -196,7 +199,7 @@ def test_w0_columns_match_reference(name, precision):
              vpg_64=colrel(g, g64, h0, n), fvp_64=colrel(fv, fv64, h0, n),
              ref_vpg_64=colrel(c["vpg_grad"], g64, h0, n), ref_fvp_64=colrel(c["hvp_out"], fv64, h0, n))
     print(name, precision, {k: "%.2e" % v for k, v in e.items()})
-    assert e["vpg_ref"] <= max(3 * float(c["spread_vpg_col"]), 1e-5), e
-    assert e["fvp_ref"] <= max(3 * float(c["spread_hvp_col"]), 1e-5), e
-    assert e["vpg_64"] <= 2 * e["ref_vpg_64"] + 1e-6, e
-    assert e["fvp_64"] <= 2 * e["ref_fvp_64"] + 1e-6, e
+    assert e["vpg_ref"] <= max(3 * float(c["spread_vpg_col"]), 2e-6), e
+    assert e["fvp_ref"] <= max(3 * float(c["spread_hvp_col"]), 2e-6), e
+    assert e["vpg_64"] <= 1.25 * e["ref_vpg_64"] + 2e-7, e
+    assert e["fvp_64"] <= 1.25 * e["ref_fvp_64"] + 2e-7, e

@@ -45,6 +45,11 @@ def main(root, json_out=None):
                       correction="2 x FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE counts half of wide "
                                  "streaming reads, MI355X_MICROARCH.md HBM)")
               for k, c in out.items() if "FETCH_SIZE" in c and "WRITE_SIZE" in c}
+        # the commit the passes measured: written into the tree before the gpurun
+        # call (tools/stamp_head.sh), as the box has no .git
+        head = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "HEAD_COMMIT")
+        if os.path.exists(head):
+            tr["_measured_at_commit"] = open(head).read().strip()
         with open(json_out, "w") as f:
             json.dump(tr, f, indent=1)
 

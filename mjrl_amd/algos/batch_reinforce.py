@@ -7,12 +7,18 @@ baseline.fit on the paths.  Here the paths are staged into HBM once; the GAE
 scan, the whole update and the statistics run on the GPU; returns / baseline /
 advantages are written back into the path dicts for baseline.fit.
 
-Several GPUs (one process per GPU, e.g. an unchanged train_agent script under
-`torchrun --nproc-per-node 8`): the communicator comes from comm.auto_comm();
-rank r samples its ceil(N / world) share of the N paths with the pegasus seed
-offset of that share (the per-worker split of trajectory_sampler.py:37-45), the
-update all-reduces its sums over RCCL, every rank ends with the same
-parameters, and the baseline is fitted on the union of the shards.
+Several GPUs, two ways:
+  - devices=[0, ..., 7] (or MJRL_AMD_DEVICES): this process stays the only one
+    running the training loop (an unchanged train_agent: its directories,
+    pickles and results.txt are written once) and never touches a GPU; each
+    update runs on N worker processes, one per GPU (mjrl_amd/pool.py), over the
+    sharded device path below;
+  - one process per GPU (e.g. the script under `torchrun --nproc-per-node 8`):
+    the communicator comes from comm.auto_comm(); rank r samples its
+    ceil(N / world) share of the N paths with the pegasus seed offset of that
+    share (the per-worker split of trajectory_sampler.py:37-45).
+Either way the update all-reduces its sums over RCCL, every rank ends with the
+same parameters, and the baseline is fitted on the union of the shards.
 """
 import logging
 import time as timer
@@ -60,7 +66,7 @@ class BatchREINFORCE:
     staging_dtype = np.float32
 
     def __init__(self, env, policy, baseline, learn_rate=0.01, seed=None, save_logs=False, device=None,
-                 comm=None):
+                 comm=None, devices=None):
         self.env = env
         self.policy = policy
         _check_policy(policy)
@@ -74,6 +80,7 @@ class BatchREINFORCE:
         self._device = device
         self._comm = comm
         self._engine = None
+        self._devices = devices
 
     # ---- device engine (never pickled: agents stay CPU-picklable) -----------
     def __getstate__(self):
@@ -94,6 +101,32 @@ class BatchREINFORCE:
                                         comm=comm, min_log_std=self.policy.min_log_std)
         self._engine.set_transformations(*self.policy.transformations())
         return self._engine
+
+    def _pool(self):
+        """The GPU worker pool of this agent (mjrl_amd/pool.py) when it runs on
+        several devices from one controller process, else None."""
+        from ..comm import launched_world
+        from ..pool import resolve_devices, get_pool
+        if self._comm is not None or launched_world() is not None:
+            return None
+        devices = resolve_devices(getattr(self, "_devices", None))
+        return None if devices is None else get_pool(devices)
+
+    def _apply_pool(self, out, paths):
+        """Rank 0's reply of a pooled update: parameters, the agent state the
+        update changed, the iteration's log entries (then the success rate, as
+        _update logs it), the fitted baseline."""
+        import pickle
+        self.policy.set_param_values(np.asarray(out["theta"], np.float32), set_new=True, set_old=True)
+        for k, v in out["sync"].items():
+            setattr(self, k, v)
+        if self.save_logs:
+            for k, v in out["logs"]:
+                self.logger.log_kv(k, v)
+            self._log_success(paths)
+        if out.get("baseline") is not None:
+            self.baseline.__dict__.update(pickle.loads(out["baseline"]).__dict__)
+        return list(out["stats"])
 
     def comm(self):
         """The agent's communicator: the one passed in, else comm.auto_comm()
@@ -142,7 +175,8 @@ class BatchREINFORCE:
             print("sample_mode in NPG must be either 'trajectories' or 'samples'")
             quit()
         trajectory_sampler, batch_sampler = _samplers()
-        comm = self.comm()
+        pool = self._pool()
+        comm = self.comm() if pool is None else LocalComm()
         ts = timer.time()
         if comm.world_size > 1:
             paths = self._sample_shard(trajectory_sampler, batch_sampler, comm, N, sample_mode, env_name, T,
@@ -155,6 +189,19 @@ class BatchREINFORCE:
         if self.save_logs:
             self.logger.log_kv("time_sampling", timer.time() - ts)
         self.seed = self.seed + N if self.seed is not None else self.seed
+
+        if pool is not None:
+            # the update and the baseline fit on the GPU workers; this process keeps
+            # the paths (returns / baseline / advantages written back), the logs and
+            # the policy / baseline objects the caller pickles
+            out = pool.step(self, paths, "samples", gamma, gae_lambda, fit=True, return_errors=self.save_logs)
+            eval_statistics = self._apply_pool(out, paths)
+            eval_statistics.append(N)
+            if self.save_logs:
+                self.logger.log_kv("time_VF", out["time_VF"])
+                self.logger.log_kv("VF_error_before", out["fit_errors"][0])
+                self.logger.log_kv("VF_error_after", out["fit_errors"][1])
+            return eval_statistics
 
         eval_statistics = self.train_from_samples(paths, gamma, gae_lambda)
         eval_statistics.append(N)
@@ -232,6 +279,9 @@ class BatchREINFORCE:
         return out
 
     def train_from_paths(self, paths):
+        pool = self._pool()
+        if pool is not None:
+            return self._apply_pool(pool.step(self, paths, "paths"), paths)
         eng = self.engine()
         batch = DeviceBatch.from_paths(paths, eng.device, use_advantages=True, demo_paths=self._demo_paths(),
                                        obs_dtype=self.staging_dtype, reuse=True)

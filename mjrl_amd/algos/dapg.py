@@ -12,7 +12,7 @@ class DAPG(NPG):
 
     def __init__(self, env, policy, baseline, demo_paths=None, normalized_step_size=0.01,
                  FIM_invert_args={"iters": 10, "damping": 1e-4}, hvp_sample_frac=1.0, seed=None, save_logs=False,
-                 kl_dist=None, lam_0=1.0, lam_1=0.95, device=None, comm=None):
+                 kl_dist=None, lam_0=1.0, lam_1=0.95, device=None, comm=None, devices=None):
         self.env = env
         self.policy = policy
         _check_policy(policy)
@@ -32,6 +32,7 @@ class DAPG(NPG):
         self._device = device
         self._comm = comm
         self._engine = None
+        self._devices = devices   # several GPUs from this process: mjrl_amd/pool.py
 
     def _use_demos(self):
         return self.demo_paths is not None and self.lam_0 > 0.0

@@ -13,7 +13,7 @@ class NPG(BatchREINFORCE):
 
     def __init__(self, env, policy, baseline, normalized_step_size=0.01, const_learn_rate=None,
                  FIM_invert_args={"iters": 10, "damping": 1e-4}, hvp_sample_frac=1.0, seed=None,
-                 save_logs=False, kl_dist=None, device=None, comm=None):
+                 save_logs=False, kl_dist=None, device=None, comm=None, devices=None):
         self.env = env
         self.policy = policy
         _check_policy(policy)
@@ -30,6 +30,7 @@ class NPG(BatchREINFORCE):
         self._device = device
         self._comm = comm
         self._engine = None
+        self._devices = devices   # several GPUs from this process: mjrl_amd/pool.py
 
     def HVP(self, observations, actions, vector, regu_coef=None):
         """F v + damping v at the current (old == new) parameters (npg_cg.py:55-74);

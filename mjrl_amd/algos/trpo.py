@@ -12,7 +12,7 @@ class TRPO(NPG):
 
     def __init__(self, env, policy, baseline, kl_dist=0.01, FIM_invert_args={"iters": 10, "damping": 1e-4},
                  hvp_sample_frac=1.0, seed=None, save_logs=False, normalized_step_size=0.01, device=None,
-                 comm=None):
+                 comm=None, devices=None):
         self.env = env
         self.policy = policy
         _check_policy(policy)
@@ -28,6 +28,7 @@ class TRPO(NPG):
         self._device = device
         self._comm = comm
         self._engine = None
+        self._devices = devices   # several GPUs from this process: mjrl_amd/pool.py
 
     def _update_args(self):
         return dict(algo="trpo", kl_dist=self.kl_dist, cg_iters=self.FIM_invert_args["iters"],

@@ -1,0 +1,396 @@
+"""One controller process, N GPU workers: multi-GPU behind an unchanged,
+single-process train_agent (SURVEY.md §5, §8 row e).
+
+mjrl's training loop (mjrl/utils/train_agent.py:14-88) is single-process: it
+creates the job directories, samples, calls agent.train_step, evaluates and
+pickles the policy / baseline / logs.  With `devices` (agent kwarg or
+MJRL_AMD_DEVICES="0,1,...,7") the agent keeps ALL of that in the calling process,
+which never touches a GPU, and hands each update to N worker processes, one per
+GPU, started once:
+
+  controller (train_agent, samplers, pickles)          worker r (cuda:devices[r])
+  ---------------------------------------------         --------------------------
+  sample N paths (mjrl samplers, host CPUs)
+  partition_paths by timestep count; shard r's
+  obs / act / rewards / lengths / terminated
+  (+ advantages) into shared-memory segment r  --step-->  attach; the agent from its
+                                                           pickled state (policy,
+                                                           baseline, hyperparameters),
+                                                           comm = torch.distributed
+                                                           group of the N workers
+                                                           (RCCL; gloo in the tests)
+                                                           train_from_samples(shard):
+                                                           the sharded device update
+                                                           with its all-reduces,
+                                                           then the baseline fit on
+                                                           the union of the shards
+  returns / baseline / advantages into the    <--reply--  rank 0: statistics, theta,
+  caller's path dicts, policy params, the                  the iteration's log entries,
+  iteration's log entries, baseline state,                 baseline state, RNG state;
+  numpy RNG state                                          every rank: its shard's
+                                                           returns / advantages
+                                                           (shared memory)
+
+Every rank ends the update with the same parameters, so rank 0
+speaks for all.  The workers are fresh interpreters (`python -m mjrl_amd.pool`,
+started with subprocess, not multiprocessing's spawn: a training script without
+an `if __name__ == "__main__"` guard is never re-imported) and talk to the
+controller over multiprocessing.connection on 127.0.0.1.
+"""
+import os
+import pickle
+import secrets
+import socket
+import subprocess
+import sys
+import time
+import traceback
+from multiprocessing import connection, shared_memory
+
+import numpy as np
+
+# agent attributes that stay with the controller / are rebuilt in a worker
+_LOCAL = ("env", "logger", "_engine", "_comm", "_last_batch", "_pool", "_devices", "_device", "_backend")
+# agent attributes a worker's update changes and the controller takes back
+_SYNC = ("running_score", "iter_count", "last_update")
+
+
+def resolve_devices(devices=None):
+    """The worker devices of an agent: `devices` (a list of GPU ordinals or a
+    count), else MJRL_AMD_DEVICES ("0,1,2,3" or "4"); None for one device (the
+    in-process engine)."""
+    if devices is None:
+        env = os.environ.get("MJRL_AMD_DEVICES", "").strip()
+        if not env:
+            return None
+        devices = [int(d) for d in env.split(",")] if "," in env else int(env)
+    if isinstance(devices, int):
+        devices = list(range(devices))
+    devices = [int(d) for d in devices]
+    return devices if len(devices) > 1 else None
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class _Layout:
+    """Byte offsets of one shard in its shared-memory segment (8-byte aligned)."""
+
+    def __init__(self, T, P, n, m, with_adv):
+        self.T, self.P, self.n, self.m = T, P, n, m
+        off = 0
+        self.fields = {}
+        for name, count in (("obs", T * n), ("act", T * m), ("rew", T), ("lengths", P), ("term", P),
+                            ("adv_in", T if with_adv else 0), ("ret", T), ("base", T), ("adv", T)):
+            self.fields[name] = (off, count)
+            off += 8 * count
+        self.nbytes = max(off, 8)
+
+    def view(self, buf, name):
+        off, count = self.fields[name]
+        dt = np.int64 if name in ("lengths", "term") else np.float64
+        return np.ndarray((count,), dtype=dt, buffer=buf, offset=off)
+
+
+class DevicePool:
+    """N worker processes, one per GPU of `devices`, driven from this process."""
+
+    def __init__(self, devices, backend="nccl", timeout=900.0):
+        self.devices = list(devices)
+        self.world = len(self.devices)
+        self.backend = backend
+        self.timeout = timeout
+        self._shm = [None] * self.world
+        authkey = secrets.token_bytes(16)
+        self._listener = connection.Listener(("127.0.0.1", 0), authkey=authkey)
+        host, port = self._listener.address
+        dist_port = _free_port()
+        env = dict(os.environ)
+        env["MJRL_AMD_DEVICES"] = ""          # a worker never starts a pool of its own
+        env["PYTHONPATH"] = os.pathsep.join([p for p in sys.path if p and os.path.isdir(p)])
+        self._procs = []
+        for r, d in enumerate(self.devices):
+            cmd = [sys.executable, "-u", "-m", "mjrl_amd.pool", "--address", "%s:%d" % (host, port),
+                   "--authkey", authkey.hex(), "--rank", str(r), "--world", str(self.world), "--device", str(d),
+                   "--backend", backend, "--dist-port", str(dist_port)]
+            self._procs.append(subprocess.Popen(cmd, env=env))
+        self._conns = [None] * self.world
+        # a worker that dies before it connects would leave accept() waiting: a
+        # watchdog closes the listener then
+        import threading
+        done = threading.Event()
+
+        def watch():
+            while not done.wait(0.5):
+                if any(p.poll() is not None for p in self._procs):
+                    self._listener.close()
+                    return
+        threading.Thread(target=watch, daemon=True).start()
+        try:
+            for _ in range(self.world):
+                c = self._listener.accept()
+                rank = c.recv()
+                self._conns[rank] = c
+        except OSError:
+            for p in self._procs:
+                if p.poll() is None:
+                    p.kill()
+            raise RuntimeError("mjrl_amd pool: a worker exited before connecting (codes %s)"
+                               % [p.poll() for p in self._procs]) from None
+        finally:
+            done.set()
+        for r, c in enumerate(self._conns):
+            msg = self._recv(r)
+            if msg[0] != "ready":
+                raise RuntimeError("mjrl_amd pool worker %d failed to start: %s" % (r, msg[1]))
+
+    # ---- plumbing -------------------------------------------------------------
+    def _recv(self, r):
+        c = self._conns[r]
+        t0 = time.time()
+        while not c.poll(1.0):
+            if self._procs[r].poll() is not None:
+                raise RuntimeError("mjrl_amd pool worker %d exited with code %s" % (r, self._procs[r].returncode))
+            if time.time() - t0 > self.timeout:
+                raise TimeoutError("mjrl_amd pool worker %d did not answer within %.0f s" % (r, self.timeout))
+        return c.recv()
+
+    def _segment(self, r, nbytes):
+        s = self._shm[r]
+        if s is None or s.size < nbytes:
+            if s is not None:
+                s.close()
+                s.unlink()
+            s = self._shm[r] = shared_memory.SharedMemory(create=True, size=nbytes)
+        return s
+
+    def close(self):
+        for r, c in enumerate(self._conns):
+            try:
+                c.send(("close",))
+            except Exception:
+                pass
+        for p in self._procs:
+            try:
+                p.wait(timeout=60)
+            except Exception:
+                p.kill()
+        for s in self._shm:
+            if s is not None:
+                s.close()
+                s.unlink()
+        self._shm = [None] * self.world
+        self._listener.close()
+
+    # ---- one update -------------------------------------------------------------
+    def step(self, agent, paths, mode, gamma=0.995, gae_lambda=0.98, fit=False, return_errors=False):
+        """The update of `agent` on `paths` by the workers.  mode 'samples':
+        train_from_samples (returns / GAE on the device, written back into the
+        paths) and, with fit, the baseline fit on the union; mode 'paths':
+        train_from_paths (the paths carry advantages).  Returns rank 0's reply."""
+        from .comm import partition_paths
+        lengths = np.array([len(p["rewards"]) for p in paths], dtype=np.int64)
+        n = int(np.asarray(paths[0]["observations"]).shape[1])
+        m = int(np.asarray(paths[0]["actions"]).shape[1])
+        parts = partition_paths(lengths, self.world)
+        if any(p1 <= p0 for p0, p1 in parts):
+            raise ValueError("%d paths over %d GPU workers: every worker needs at least one path"
+                             % (len(paths), self.world))
+        state = pickle.dumps(dict(cls=type(agent), d={k: v for k, v in agent.__dict__.items() if k not in _LOCAL}))
+        with_adv = mode == "paths"
+        layouts = []
+        import concurrent.futures as cf
+
+        def fill(r):
+            p0, p1 = parts[r]
+            sh = paths[p0:p1]
+            L = _Layout(int(lengths[p0:p1].sum()), p1 - p0, n, m, with_adv)
+            seg = self._segment(r, L.nbytes)
+            if sh:
+                np.concatenate([np.asarray(p["observations"], np.float64).reshape(-1) for p in sh],
+                               out=L.view(seg.buf, "obs"))
+                np.concatenate([np.asarray(p["actions"], np.float64).reshape(-1) for p in sh],
+                               out=L.view(seg.buf, "act"))
+                np.concatenate([np.asarray(p["rewards"], np.float64) for p in sh], out=L.view(seg.buf, "rew"))
+                if with_adv:
+                    np.concatenate([np.asarray(p["advantages"], np.float64) for p in sh], out=L.view(seg.buf, "adv_in"))
+            L.view(seg.buf, "lengths")[:] = lengths[p0:p1]
+            L.view(seg.buf, "term")[:] = [int(bool(p.get("terminated", False))) for p in sh]
+            return L
+
+        with cf.ThreadPoolExecutor(self.world) as ex:
+            layouts = list(ex.map(fill, range(self.world)))
+        rng = np.random.get_state()
+        for r in range(self.world):
+            L = layouts[r]
+            self._conns[r].send(("step", dict(state=state, shm=self._shm[r].name, T=L.T, P=L.P, n=n, m=m,
+                                              mode=mode, gamma=gamma, gae_lambda=gae_lambda, fit=fit,
+                                              return_errors=return_errors, rng=rng, with_adv=with_adv)))
+        replies = [self._recv(r) for r in range(self.world)]
+        for r, msg in enumerate(replies):
+            if msg[0] != "ok":
+                raise RuntimeError("mjrl_amd pool worker %d failed:\n%s" % (r, msg[1]))
+        if mode == "samples":
+            for r in range(self.world):
+                p0, p1 = parts[r]
+                L, buf = layouts[r], self._shm[r].buf
+                ret, base, adv = (L.view(buf, k).copy() for k in ("ret", "base", "adv"))
+                o = 0
+                for p in paths[p0:p1]:
+                    h = len(p["rewards"])
+                    p["returns"], p["baseline"], p["advantages"] = ret[o:o + h], base[o:o + h], adv[o:o + h]
+                    o += h
+        out = replies[0][1]
+        np.random.set_state(out["rng"])
+        return out
+
+
+_POOLS = {}
+
+
+def get_pool(devices, backend=None):
+    """The process-wide pool for `devices` (started on first use, closed at
+    exit).  backend: MJRL_AMD_POOL_BACKEND, default "nccl" (RCCL); "gloo" runs
+    several workers on one GPU (tests)."""
+    backend = backend or os.environ.get("MJRL_AMD_POOL_BACKEND", "nccl")
+    key = (tuple(devices), backend)
+    pool = _POOLS.get(key)
+    if pool is None:
+        if not _POOLS:
+            import atexit
+            atexit.register(close_pools)
+        pool = _POOLS[key] = DevicePool(devices, backend)
+    return pool
+
+
+def close_pools():
+    while _POOLS:
+        _, pool = _POOLS.popitem()
+        try:
+            pool.close()
+        except Exception:
+            pass
+
+
+def _worker_paths(L, buf):
+    """The shard's paths as dicts of views into the shared segment."""
+    obs = L.view(buf, "obs").reshape(L.T, L.n)
+    act = L.view(buf, "act").reshape(L.T, L.m)
+    rew = L.view(buf, "rew")
+    adv = L.view(buf, "adv_in") if L.fields["adv_in"][1] else None
+    lengths = L.view(buf, "lengths")
+    term = L.view(buf, "term")
+    paths, o = [], 0
+    for i in range(L.P):
+        h = int(lengths[i])
+        p = dict(observations=obs[o:o + h], actions=act[o:o + h], rewards=rew[o:o + h], agent_infos={},
+                 env_infos={}, terminated=bool(term[i]))
+        if adv is not None:
+            p["advantages"] = adv[o:o + h]
+        paths.append(p)
+        o += h
+    return paths
+
+
+def _worker_main(args):
+    host, port = args.address.rsplit(":", 1)
+    conn = connection.Client((host, int(port)), authkey=bytes.fromhex(args.authkey))
+    conn.send(args.rank)
+    try:
+        import torch
+        import torch.distributed as dist
+        if args.backend == "nccl":
+            torch.cuda.set_device(args.device)
+            dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % args.dist_port, rank=args.rank,
+                                    world_size=args.world, device_id=torch.device("cuda", args.device))
+        else:
+            if torch.cuda.is_available():
+                torch.cuda.set_device(args.device)
+            dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % args.dist_port, rank=args.rank,
+                                    world_size=args.world)
+        from .comm import DistComm
+        from .utils.logger import DataLog
+        comm = DistComm()
+    except Exception:
+        conn.send(("error", traceback.format_exc()))
+        return 1
+    conn.send(("ready",))
+    engines = {}
+    shm = None
+    while True:
+        msg = conn.recv()
+        if msg[0] == "close":
+            break
+        try:
+            a = msg[1]
+            if shm is None or shm.name != a["shm"]:
+                if shm is not None:
+                    shm.close()
+                shm = shared_memory.SharedMemory(name=a["shm"])
+                _untrack(shm)
+            L = _Layout(a["T"], a["P"], a["n"], a["m"], a["with_adv"])
+            paths = _worker_paths(L, shm.buf)
+            st = pickle.loads(a["state"])
+            agent = st["cls"].__new__(st["cls"])
+            agent.__dict__.update(st["d"])
+            agent.env = None
+            agent.logger = DataLog()
+            agent._comm = comm
+            agent._device = None
+            agent._devices = None
+            key = (agent.policy.n, agent.policy.m, agent.policy.hidden)
+            agent._engine = engines.get(key)
+            np.random.set_state(a["rng"])
+            out = {}
+            if a["mode"] == "samples":
+                stats = agent.train_from_samples(paths, a["gamma"], a["gae_lambda"])
+                for name, k in (("ret", "returns"), ("base", "baseline"), ("adv", "advantages")):
+                    v = L.view(shm.buf, name)
+                    if paths:
+                        np.concatenate([np.asarray(p[k], np.float64) for p in paths], out=v)
+                if a["fit"]:
+                    ts = time.time()
+                    errs = agent._fit_baseline(paths, return_errors=a["return_errors"])
+                    out["time_VF"] = time.time() - ts
+                    out["fit_errors"] = errs if a["return_errors"] else None
+                    out["baseline"] = pickle.dumps(agent.baseline) if args.rank == 0 else None
+            else:
+                stats = agent.train_from_paths(paths)
+            engines[key] = agent._engine
+            if args.rank == 0:
+                out.update(stats=[float(s) for s in stats], theta=agent.policy.get_param_values(),
+                           logs=list(agent.logger.get_current_log().items()) if agent.save_logs else [],
+                           sync={k: agent.__dict__[k] for k in _SYNC if k in agent.__dict__},
+                           rng=np.random.get_state())
+            conn.send(("ok", out))
+        except Exception:
+            conn.send(("error", traceback.format_exc()))
+    if shm is not None:
+        shm.close()
+    dist.destroy_process_group()
+    return 0
+
+
+def _untrack(shm):
+    """The controller owns (and unlinks) the segment: keep this process's
+    resource tracker from unlinking it at exit."""
+    try:
+        from multiprocessing import resource_tracker
+        resource_tracker.unregister(shm._name, "shared_memory")
+    except Exception:
+        pass
+
+
+if __name__ == "__main__":
+    import argparse
+    ap = argparse.ArgumentParser()
+    for k in ("address", "authkey", "backend"):
+        ap.add_argument("--" + k, required=True)
+    for k in ("rank", "world", "device", "dist-port"):
+        ap.add_argument("--" + k, type=int, required=True)
+    sys.exit(_worker_main(ap.parse_args()))

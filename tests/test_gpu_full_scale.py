@@ -1,0 +1,94 @@
+"""Parity at the headline size: the whole NPG update on bench.py's own workload
+(Humanoid shape, 1,000 paths x 1,000 steps = 1M rows, the seeded synthetic batch,
+the LinearBaseline and initial parameters bench.py uses) against the oracle run
+on the same batch on the host (oracle/npg_cpu.py, fp32 torch as the reference
+computes; ~1 min on the GPU box's 16 host threads).
+
+Checked at 1M rows, for the split-f16 kernels (the bench's form) and the
+exact-f32 kernels:
+  - returns / advantages bit-exact, path statistics 1e-12;
+  - the VPG (CG right-hand side) norm-relative 1e-5;
+  - every CG iteration teacher-forced: our F p_k on the oracle's p_k against
+    its z_k, norm-relative 1e-5;
+  - end to end: npg_grad / theta 1e-3, alpha / KL / surrogate improvement
+    2e-3 (the floors of tests/test_gpu_parity.py; the reference's own spread
+    at 60k rows is 6e-4 on npg_grad, c4_humanoid.npz);
+  - the post-step surrogate / KL at OUR new parameters against the oracle's
+    evaluation at those parameters, rtol 1e-4.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def nrel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
+
+
+@pytest.fixture(scope="module")
+def workload():
+    import bench
+    from oracle import npg_cpu as O
+    cfg = bench.CONFIGS["c4"]
+    obs, act, rew = bench.make_paths(0, cfg["paths"], cfg=cfg)
+    base = bench.baseline_coeffs(cfg)
+    bl = np.concatenate([base.predict(dict(observations=o.astype(np.float64), rewards=r)) for o, r in zip(obs, rew)])
+    obs = np.concatenate(obs).astype(np.float64)
+    act = np.concatenate(act).astype(np.float64)
+    rew = np.concatenate(rew)
+    lengths = np.full(cfg["paths"], cfg["horizon"], dtype=np.int64)
+    theta = bench.initial_theta(cfg)
+    ret, adv = O.returns_and_advantages(rew, bl, lengths, np.zeros(len(lengths), bool), bench.GAMMA, bench.LAM)
+    torch.set_num_threads(bench.host_cores())
+    pol = O.Policy(cfg["n"], cfg["m"], cfg["hidden"], theta.astype(np.float64), None)
+    trace = []
+    ref = O.update(pol, obs, act, adv, rew, lengths, algo="npg", n_step_size=cfg["step"]["n_step_size"],
+                   cg_iters=bench.CG_ITERS, damping=bench.DAMPING, trace=trace)
+    ref["cg_trace"] = trace
+    return dict(cfg=cfg, obs=obs, act=act, rew=rew, bl=bl, lengths=lengths, theta=theta, ret=ret, adv=adv, ref=ref)
+
+
+@pytest.mark.parametrize("precision", [None, "f32"])
+def test_full_update_1M_matches_oracle(workload, precision):
+    import bench
+    from mjrl_amd.engine import DeviceBatch, UpdateEngine
+    from oracle import npg_cpu as O
+    w = workload
+    cfg, ref = w["cfg"], w["ref"]
+    dev = torch.device("cuda:0")
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    off = np.concatenate([[0], np.cumsum(w["lengths"])]).astype(np.int64)
+    batch = DeviceBatch(t(w["obs"].astype(np.float32)), t(w["act"].astype(np.float32)), t(w["rew"]), t(w["bl"]),
+                        t(off), t(np.zeros(len(w["lengths"]), np.uint8)))
+    eng = UpdateEngine(cfg["n"], cfg["m"], cfg["hidden"], device=dev, precision=precision)
+    assert eng.split == (precision is None)
+    res = eng.update(batch, t(w["theta"]), **bench.update_args(cfg, batch.T))
+    T = batch.T
+    assert T == 1_000_000
+    assert np.array_equal(eng.ws["ret"][:T].cpu().numpy(), w["ret"])
+    assert np.array_equal(eng.ws["adv64"][:T].cpu().numpy(), w["adv"])
+    np.testing.assert_allclose(res["base_stats"], ref["base_stats"], rtol=1e-12)
+    g = eng.vec["g"].cpu().numpy()
+    assert nrel(g, ref["vpg_grad"]) < 1e-5, nrel(g, ref["vpg_grad"])
+    for k, (p, z) in enumerate(ref["cg_trace"]):
+        zz = eng.fvp(t(p.astype(np.float32)), damping=bench.DAMPING).cpu().numpy()
+        assert nrel(zz, z) < 1e-5, (k, nrel(zz, z))
+    x = eng.vec["x"].cpu().numpy()
+    th1 = eng.vec["theta_new"].cpu().numpy()
+    errs = dict(x=nrel(x, ref["npg_grad"]), theta=nrel(th1, ref["theta1"]),
+                alpha=abs(res["alpha"] / float(ref["alpha"]) - 1), kl=abs(res["kl_dist"] / ref["kl_dist"] - 1),
+                surr=abs((res["surr_after"] - res["surr_before"]) / (ref["surr_after"] - ref["surr_before"]) - 1))
+    print("1M", precision, {k: "%.2e" % v for k, v in errs.items()})
+    assert errs["x"] < 1e-3 and errs["theta"] < 1e-3, errs
+    assert errs["alpha"] < 2e-3 and errs["kl"] < 2e-3 and errs["surr"] < 2e-3, errs
+    # teacher-forced evaluation at our new parameters
+    pol = O.Policy(cfg["n"], cfg["m"], cfg["hidden"], w["theta"].astype(np.float64), None)
+    pol.set_params(th1.astype(np.float64), set_new=True, set_old=False)
+    kl_o = float(pol.kl(w["obs"], w["act"]).detach().numpy())
+    surr_o = float(pol.surrogate(w["obs"], w["act"], ref["adv_whitened"]).detach().numpy())
+    np.testing.assert_allclose(res["kl_dist"], kl_o, rtol=1e-4, atol=1e-8)
+    np.testing.assert_allclose(res["surr_after"], surr_o, rtol=1e-4, atol=1e-7)

@@ -62,6 +62,7 @@ def test_pool_npg_two_workers_one_gpu(tmp_path, monkeypatch):
     finally:
         pool.close_pools()
     a1, s1, adv1, j1 = _loop(str(tmp_path / "one"), None)
+    stub_samplers.CALLS.clear()
     np.testing.assert_allclose(np.array(s2), np.array(s1), rtol=1e-10)
     np.testing.assert_allclose(adv2, adv1, rtol=1e-9, atol=1e-12)
     th1, th2 = a1.policy.get_param_values(), a2.policy.get_param_values()

@@ -61,6 +61,7 @@ def pool_env(monkeypatch):
     yield
     from mjrl_amd import pool
     pool.close_pools()
+    stub_samplers.CALLS.clear()
 
 
 def test_pool_matches_one_process(tmp_path, pool_env):

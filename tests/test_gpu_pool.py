@@ -64,7 +64,9 @@ def test_pool_npg_two_workers_one_gpu(tmp_path, monkeypatch):
     a1, s1, adv1, j1 = _loop(str(tmp_path / "one"), None)
     stub_samplers.CALLS.clear()
     np.testing.assert_allclose(np.array(s2), np.array(s1), rtol=1e-10)
-    np.testing.assert_allclose(adv2, adv1, rtol=1e-9, atol=1e-12)
+    # advantages of the last iteration: its baseline came from an fp64 Gram summed
+    # over two shards (all-reduced) against one sum: 1e-11-level differences
+    np.testing.assert_allclose(adv2, adv1, rtol=1e-9, atol=1e-9)
     th1, th2 = a1.policy.get_param_values(), a2.policy.get_param_values()
     assert np.linalg.norm(th2 - th1) / np.linalg.norm(th1) < 1e-3
     np.testing.assert_allclose(a2.baseline._coeffs, a1.baseline._coeffs, rtol=1e-6, atol=1e-8)

@@ -21,6 +21,7 @@ Either way the update all-reduces its sums over RCCL, every rank ends with the
 same parameters, and the baseline is fitted on the union of the shards.
 """
 import logging
+import os
 import time as timer
 
 import multiprocessing as mp
@@ -60,6 +61,15 @@ def _samplers():
 
 class BatchREINFORCE:
     algo = "vpg"
+    # sampler of train_step's 'trajectories' mode: "reference" (mjrl's process-pool
+    # samplers, policy.get_action per observation on the CPU) or "vector"
+    # (samplers/vector_sampler.py, SURVEY.md §8f row f3: lock-stepped environments,
+    # one device policy forward per step, the same trajectories for the same seeds);
+    # default from MJRL_AMD_SAMPLER.  env_factory / num_envs configure "vector"
+    # (default factory: mjrl.utils.get_environment(env_name)).
+    sampler = None
+    env_factory = None
+    num_envs = 64
     # dtype the sampled observations / actions are staged to HBM in: float32 (the
     # policy's own input precision, half the PCIe bytes) or float64 (the device
     # LinearBaseline then predicts / fits from the sampler's exact values)
@@ -101,6 +111,12 @@ class BatchREINFORCE:
                                         comm=comm, min_log_std=self.policy.min_log_std)
         self._engine.set_transformations(*self.policy.transformations())
         return self._engine
+
+    def _sampler_kind(self):
+        kind = self.sampler or os.environ.get("MJRL_AMD_SAMPLER", "reference")
+        if kind not in ("reference", "vector"):
+            raise ValueError("sampler must be 'reference' or 'vector', got %r" % kind)
+        return kind
 
     def _pool(self):
         """The GPU worker pool of this agent (mjrl_amd/pool.py) when it runs on
@@ -174,13 +190,22 @@ class BatchREINFORCE:
         if sample_mode != "trajectories" and sample_mode != "samples":
             print("sample_mode in NPG must be either 'trajectories' or 'samples'")
             quit()
-        trajectory_sampler, batch_sampler = _samplers()
         pool = self._pool()
         comm = self.comm() if pool is None else LocalComm()
+        vector = sample_mode == "trajectories" and comm.world_size == 1 and self._sampler_kind() == "vector"
+        trajectory_sampler, batch_sampler = (None, None) if vector else _samplers()
         ts = timer.time()
         if comm.world_size > 1:
             paths = self._sample_shard(trajectory_sampler, batch_sampler, comm, N, sample_mode, env_name, T,
                                        num_cpu)
+        elif vector:
+            if pool is not None:
+                raise ValueError("the vector sampler runs the policy on a GPU; with devices=... the controller "
+                                 "process keeps off the GPUs: use the reference samplers there")
+            from ..samplers.vector_sampler import sample_paths_vectorized
+            paths = sample_paths_vectorized(N, self.policy, T, env=self.env_factory, env_name=env_name,
+                                            pegasus_seed=self.seed, num_envs=self.num_envs,
+                                            device=self.engine().device)
         elif sample_mode == "trajectories":
             paths = trajectory_sampler.sample_paths_parallel(N, self.policy, T, env_name, self.seed, num_cpu)
         else:

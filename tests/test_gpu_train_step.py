@@ -167,3 +167,48 @@ def test_train_from_paths_graph_replay_bitwise():
     assert agents[0].engine()._gstate.get("graph") is not None
     assert agents[1].engine()._gstate.get("graph") is None
     np.testing.assert_array_equal(agents[0].policy.get_param_values(), agents[1].policy.get_param_values())
+
+
+def test_train_step_vector_sampler_matches_reference_sampler():
+    """train_step with the opt-in vectorised sampler (agent.sampler = "vector",
+    SURVEY.md §8f row f3) against train_step with a reference-style serial
+    sampler (base_sampler.do_rollout's loop, tests/stub_env.py) over the same
+    environment and seeds: the same trajectories (to f32 rounding of the policy
+    mean), hence the same update."""
+    import sys
+    import types
+    from mjrl_amd.algos.npg_cg import NPG
+    from mjrl_amd.baselines.linear_baseline import LinearBaseline
+    from mjrl_amd.policies.gaussian_mlp import MLP
+    from mjrl_amd.utils.gym_env import EnvSpec
+    from stub_env import StubEnv, serial_rollout
+
+    def serial(N, policy, T, env_name, seed, num_cpu, **kw):
+        ps = serial_rollout(N, policy, T, StubEnv, seed)
+        return [dict(observations=p["observations"], actions=p["actions"], rewards=p["rewards"], agent_infos={},
+                     env_infos={}, terminated=p["terminated"]) for p in ps]
+    mods = {"mjrl": types.ModuleType("mjrl"), "mjrl.samplers": types.ModuleType("mjrl.samplers"),
+            "mjrl.samplers.trajectory_sampler": types.ModuleType("mjrl.samplers.trajectory_sampler"),
+            "mjrl.samplers.batch_sampler": types.ModuleType("mjrl.samplers.batch_sampler")}
+    mods["mjrl.samplers.trajectory_sampler"].sample_paths_parallel = serial
+    saved = {k: sys.modules.get(k) for k in mods}
+    sys.modules.update(mods)
+    try:
+        out = []
+        for kind in ("reference", "vector"):
+            spec = EnvSpec(6, 2, 40, 1)
+            agent = NPG(_Env(), MLP(spec, hidden_sizes=(64, 64), seed=3, init_log_std=-1.0), LinearBaseline(spec),
+                        normalized_step_size=0.05, seed=200, save_logs=True)
+            agent.sampler, agent.env_factory, agent.num_envs = kind, StubEnv, 16
+            stats = [agent.train_step(N=150, gamma=0.99, gae_lambda=0.95) for _ in range(2)]
+            out.append((stats, agent.policy.get_param_values(), agent.seed))
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                sys.modules.pop(k, None)
+            else:
+                sys.modules[k] = v
+    (s_ref, th_ref, seed_ref), (s_vec, th_vec, seed_vec) = out
+    assert seed_ref == seed_vec == 200 + 2 * 150
+    np.testing.assert_allclose(np.array(s_vec), np.array(s_ref), rtol=1e-5)
+    assert np.linalg.norm(th_vec - th_ref) / np.linalg.norm(th_ref) < 1e-3

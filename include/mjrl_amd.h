@@ -134,6 +134,15 @@ int mjrl_gae(const double* rew, const double* base, const int64_t* path_off,
              const uint8_t* terminated, int64_t P, double gamma, double gae_lambda,
              int32_t use_gae, double* ret, double* adv, double* path_ret, void* stream);
 
+/* The same outputs by a wave-parallel scan (one wave per path, 64 lane chunks per
+ * window of 1024 steps composed with wave shuffles): not bit-identical to
+ * discount_sum — the products are regrouped — but within ~1e-14 of each path's
+ * largest |value|; path_ret is a fixed-order wave reduction.  mjrl_gae stays the
+ * exact default (UpdateEngine.gae_mode = "serial" | "scan"). */
+int mjrl_gae_scan(const double* rew, const double* base, const int64_t* path_off,
+                  const uint8_t* terminated, int64_t P, double gamma, double gae_lambda,
+                  int32_t use_gae, double* ret, double* adv, double* path_ret, void* stream);
+
 /* ---- LinearBaseline.predict on device (baselines/linear_baseline.py:10-18, 46-49) ----
  * out[t] = [clip(obs_t, +-10), a, a^2, a^3, 1] . coeffs[n+4], a = (t - path start)/1000,
  * for every row of every path (the input of mjrl_gae, process_samples.py:23). */

@@ -339,6 +339,61 @@ def test_gae_kernel_multiwindow_bitexact(use_gae):
     assert pr[~keep].tolist() == [0.0]
 
 
+@pytest.mark.parametrize("use_gae", [1, 0])
+def test_gae_scan_kernel(use_gae):
+    """mjrl_gae_scan (the wave-shuffle scan form of process_samples.py:21-44) on
+    paths shorter than, equal to and longer than its 1024-step window: returns and
+    advantages within 1e-12 of each path's largest |value| of the oracle's
+    discount_sum, path-return sums within 1e-12 relative; an empty path gives 0;
+    the update engine with gae_mode="scan" on a full-size fixture lands on the
+    same update as the exact scan."""
+    from mjrl_amd import _lib
+    from oracle import npg_cpu as O
+    L = _lib.lib()
+    rs = np.random.RandomState(12)
+    lengths = np.array([1, 7, 63, 64, 65, 1023, 1024, 1025, 0, 2048, 3001, 5, 1000])
+    T = int(lengths.sum())
+    rew = rs.randn(T) * 3.0
+    base = rs.randn(T)
+    term = (rs.rand(len(lengths)) < 0.5).astype(np.uint8)
+    off = np.concatenate([[0], np.cumsum(lengths)]).astype(np.int64)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    ret = torch.full((T,), np.nan, dtype=torch.float64, device="cuda")
+    adv = torch.full((T,), np.nan, dtype=torch.float64, device="cuda")
+    pret = torch.full((len(lengths),), np.nan, dtype=torch.float64, device="cuda")
+    gamma, lam = 0.995, 0.97
+    d = [t(rew), t(base), t(off), t(term)]
+    assert L.mjrl_gae_scan(*[_lib.ptr(x) for x in d], len(lengths), gamma, lam, use_gae, _lib.ptr(ret),
+                           _lib.ptr(adv), _lib.ptr(pret), _lib.stream_ptr()) == 0
+    torch.cuda.synchronize()
+    keep = lengths > 0
+    m = np.repeat(keep, lengths)
+    r_ref, a_ref = O.returns_and_advantages(rew[m], base[m], lengths[keep], term[keep].astype(bool), gamma,
+                                            lam if use_gae else None)
+    r, a = ret.cpu().numpy(), adv.cpu().numpy()
+    for x, y in ((r, r_ref), (a, a_ref)):
+        for seg_x, seg_y in zip(O.split(x, lengths[keep]), O.split(y, lengths[keep])):
+            assert np.abs(seg_x - seg_y).max() <= 1e-12 * np.abs(seg_y).max() + 1e-300
+    pr = pret.cpu().numpy()
+    np.testing.assert_allclose(pr[keep], np.array([sum(v) for v in O.split(rew[m], lengths[keep])]), rtol=1e-12)
+    assert pr[~keep].tolist() == [0.0]
+    # the whole update on the scan: the same as on the exact chain to fp32 noise
+    c, kw, pol, res = None, None, None, {}
+    from mjrl_amd.engine import UpdateEngine
+    import test_gpu_parity as TP
+    for mode in ("serial", "scan"):
+        cc, kw = TP.load("c3_halfcheetah_full")
+        eng = UpdateEngine(int(cc["n"]), int(cc["m"]), cc["hidden_t"], device=torch.device("cuda:0"))
+        eng.gae_mode = mode
+        b = TP.make_batch(cc, torch.device("cuda:0"))
+        out = eng.update(b, t(cc["theta0"].astype(np.float32)), algo="trpo", gamma=float(cc["gamma"]),
+                         gae_lambda=float(cc["gae_lambda"]), kl_dist=kw["kl_dist"], trpo_verbose=False)
+        res[mode] = (eng.vec["theta_new"].cpu().numpy(), out["kl_dist"], eng.ws["adv64"][:b.T].cpu().numpy())
+    assert np.abs(res["scan"][2] - res["serial"][2]).max() <= 1e-12 * np.abs(res["serial"][2]).max()
+    assert TP.nrel(res["scan"][0], res["serial"][0]) < 1e-5
+    np.testing.assert_allclose(res["scan"][1], res["serial"][1], rtol=1e-4)
+
+
 def test_subsampled_hvp_api():
     """NPG.HVP with hvp_sample_frac < 1 through the drop-in API: the reference's
     np.random.choice draw from numpy's global RNG (npg_cg.py:58-62)."""

@@ -77,7 +77,9 @@ __global__ void __launch_bounds__(256) k_colmax(const TO* __restrict__ obs, int6
                 sh[u][e] = in_shift && c < n ? in_shift[c] : 0.f;
                 den[u][e] = in_shift && c < n ? in_scale[c] + 1e-8f : 1.f;
             }
-        for (int64_t row = (int64_t)blockIdx.x * rpp + rsub; row < T; row += (int64_t)gridDim.x * rpp) {
+        const int64_t rstride = (int64_t)gridDim.x * rpp;
+#pragma unroll 4
+        for (int64_t row = (int64_t)blockIdx.x * rpp + rsub; row < T; row += rstride) {
             const TO* src = obs + row * n;
 #pragma unroll
             for (int u = 0; u < 2; ++u) {

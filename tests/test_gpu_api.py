@@ -378,11 +378,12 @@ def test_gae_scan_kernel(use_gae):
     np.testing.assert_allclose(pr[keep], np.array([sum(v) for v in O.split(rew[m], lengths[keep])]), rtol=1e-12)
     assert pr[~keep].tolist() == [0.0]
     # the whole update on the scan: the same as on the exact chain to fp32 noise
-    c, kw, pol, res = None, None, None, {}
+    res = {}
     from mjrl_amd.engine import UpdateEngine
     import test_gpu_parity as TP
     for mode in ("serial", "scan"):
-        cc, kw = TP.load("c3_halfcheetah_full")
+        cc, case_kwargs = TP.load("c3_halfcheetah_full")
+        kw = case_kwargs(cc)
         eng = UpdateEngine(int(cc["n"]), int(cc["m"]), cc["hidden_t"], device=torch.device("cuda:0"))
         eng.gae_mode = mode
         b = TP.make_batch(cc, torch.device("cuda:0"))

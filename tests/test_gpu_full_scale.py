@@ -45,10 +45,9 @@ def workload():
     ret, adv = O.returns_and_advantages(rew, bl, lengths, np.zeros(len(lengths), bool), bench.GAMMA, bench.LAM)
     torch.set_num_threads(bench.host_cores())
     pol = O.Policy(cfg["n"], cfg["m"], cfg["hidden"], theta.astype(np.float64), None)
-    trace = []
     ref = O.update(pol, obs, act, adv, rew, lengths, algo="npg", n_step_size=cfg["step"]["n_step_size"],
-                   cg_iters=bench.CG_ITERS, damping=bench.DAMPING, trace=trace)
-    ref["cg_trace"] = trace
+                   cg_iters=bench.CG_ITERS, damping=bench.DAMPING, trace=True)
+    assert len(ref["cg_trace"]) == bench.CG_ITERS
     return dict(cfg=cfg, obs=obs, act=act, rew=rew, bl=bl, lengths=lengths, theta=theta, ret=ret, adv=adv, ref=ref)
 
 

@@ -73,11 +73,12 @@ def test_full_update_1M_matches_oracle(workload, precision):
     np.testing.assert_allclose(res["base_stats"], ref["base_stats"], rtol=1e-12)
     g = eng.vec["g"].cpu().numpy()
     assert nrel(g, ref["vpg_grad"]) < 1e-5, nrel(g, ref["vpg_grad"])
+    # the update's results first: the standalone FVPs below reuse the engine's vectors
+    x = eng.vec["x"].cpu().numpy()
+    th1 = eng.vec["theta_new"].cpu().numpy()
     for k, (p, z) in enumerate(ref["cg_trace"]):
         zz = eng.fvp(t(p.astype(np.float32)), damping=bench.DAMPING).cpu().numpy()
         assert nrel(zz, z) < 1e-5, (k, nrel(zz, z))
-    x = eng.vec["x"].cpu().numpy()
-    th1 = eng.vec["theta_new"].cpu().numpy()
     errs = dict(x=nrel(x, ref["npg_grad"]), theta=nrel(th1, ref["theta1"]),
                 alpha=abs(res["alpha"] / float(ref["alpha"]) - 1), kl=abs(res["kl_dist"] / ref["kl_dist"] - 1),
                 surr=abs((res["surr_after"] - res["surr_before"]) / (ref["surr_after"] - ref["surr_before"]) - 1))

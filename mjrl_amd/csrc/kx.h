@@ -771,7 +771,7 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
                 const float sc = pow2_scale(max_over_groups(absmax8(v)), inv);
                 split8(v, sc, gh, gl);
 #pragma unroll
-                for (int rr = 0; rr < 4; ++rr) s4[rr] = __shfl(inv, 4 * lq + rr, 64) * AHR_INV;
+                for (int rr = 0; rr < 4; ++rr) s4[rr] = __shfl(inv * AHR_INV, 4 * lq + rr, 64);
                 if ((w & 3) == 0) {
                     b2acc += sum_over_groups(((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7])));
                 }
@@ -824,7 +824,7 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
                 const float sc = pow2_scale(max_over_groups(absmax8(v)), inv);
                 split8(v, sc, gh, gl);
 #pragma unroll
-                for (int rr = 0; rr < 4; ++rr) s4[rr] = __shfl(inv, 4 * lq + rr, 64) * AHR_INV;
+                for (int rr = 0; rr < 4; ++rr) s4[rr] = __shfl(inv * AHR_INV, 4 * lq + rr, 64);
                 if (kh == 0) {
                     b1acc += sum_over_groups(((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7])));
                 }

@@ -573,21 +573,16 @@ struct WArgs {
 };
 
 constexpr int WB = 64;        // output block edge
-constexpr int WT = 64;        // rows per staged tile (two k32 steps of the split products)
-constexpr int WLT = WT + 4;   // LDS stride (floats) of the transposed [col][row] tiles
+constexpr int WT = 64;        // rows per staged tile
+constexpr int WLD = WB + 16;  // LDS row stride (floats): rows 4 apart land 16 banks apart
 
-// C[n][k] += sum_t G[t][n] A[t][k] on split-f16 MFMA (common.h "fp16x3"): the
-// staged tiles are stored transposed ([col][row]), so a lane's operand — eight
-// consecutive rows of one column — is two ds_read_b128; each operand is scaled by
-// a power of two per (32-row step, column) — a block along the SUMMED dimension,
-// with the 2^14 headroom, so every term keeps 23 bits down to 2^-17 of its block
-// maximum (the error of an f32 sum of the same terms) — split in registers, and
-// the product unscaled on the f32 accumulator.  Three f16 MFMAs per 16x16x32 step
-// replace eight f32 ones (16x16x4): 5.3x the matrix rate.
+// (A split-f16 version — transposed LDS tiles, per-(32-row step, column) scales —
+// measured slower: HalfCheetah 87 -> 126 us, door 94 -> 134 us per launch, from
+// the transposing LDS writes and the per-step splits; profiles/r03g/rejected/.)
 __global__ void __launch_bounds__(NTHREADS, 2) k_wgrad(WArgs a) {
     if (a.done && *a.done) return;
-    __shared__ __attribute__((aligned(16))) float Gs[WB * WLT];
-    __shared__ __attribute__((aligned(16))) float As[WB * WLT];
+    __shared__ __attribute__((aligned(16))) float Gs[WT * WLD];
+    __shared__ __attribute__((aligned(16))) float As[WT * WLD];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int r16 = lane & 15, q = lane >> 4;
     const int jb = blockIdx.x / a.S, s = blockIdx.x % a.S;
@@ -622,7 +617,6 @@ __global__ void __launch_bounds__(NTHREADS, 2) k_wgrad(WArgs a) {
                                           : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     };
-    const bool active = n0 + 16 * w < J.N;
     if (r0 < r1) gload(r0);
     for (int64_t t0 = r0; t0 < r1; t0 += WT) {
         __syncthreads();
@@ -630,47 +624,25 @@ __global__ void __launch_bounds__(NTHREADS, 2) k_wgrad(WArgs a) {
         for (int u = 0; u < 4; ++u) {
             const int idx = tid + u * NTHREADS;
             const int row = idx >> 4, c4 = (idx & 15) * 4;
-            Gs[(c4 + 0) * WLT + row] = g4[u].x;
-            Gs[(c4 + 1) * WLT + row] = g4[u].y;
-            Gs[(c4 + 2) * WLT + row] = g4[u].z;
-            Gs[(c4 + 3) * WLT + row] = g4[u].w;
-            As[(c4 + 0) * WLT + row] = a4[u].x;
-            As[(c4 + 1) * WLT + row] = a4[u].y;
-            As[(c4 + 2) * WLT + row] = a4[u].z;
-            As[(c4 + 3) * WLT + row] = a4[u].w;
+            *reinterpret_cast<float4*>(Gs + row * WLD + c4) = g4[u];
+            *reinterpret_cast<float4*>(As + row * WLD + c4) = a4[u];
         }
         __syncthreads();
         if (t0 + WT < r1) gload(t0 + WT);
-        if (active) {
-#pragma unroll
-            for (int st = 0; st < WT / 32; ++st) {
-                // left operand: G rows 32 st + 8q .. +7 of column n = n0 + 16 w + r16
-                half8 ah, al;
-                float sg[4];
-                {
-                    const float8v v = load8(Gs + (16 * w + r16) * WLT + 32 * st + 8 * q);
-                    float inv;
-                    const float sc = pow2_scale(max_over_groups(absmax8(v)), inv);
-                    split8(v, sc, ah, al);
-#pragma unroll
-                    for (int rr = 0; rr < 4; ++rr) sg[rr] = __shfl(inv, 4 * q + rr, 64);
-                }
+        if (n0 + 16 * w < J.N) {
+#pragma unroll 4
+            for (int tt = 0; tt < WT; tt += 4) {
+                const float ga = Gs[(tt + q) * WLD + 16 * w + r16];
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    const float8v v = load8(As + (16 * i + r16) * WLT + 32 * st + 8 * q);
-                    float inv;
-                    const float sc = pow2_scale(max_over_groups(absmax8(v)), inv);
-                    half8 bh, bl;
-                    split8(v, sc, bh, bl);
-                    const floatx4 t = mfma_x3(ah, al, bh, bl, zero4());
-#pragma unroll
-                    for (int rr = 0; rr < 4; ++rr) acc[i][rr] += t[rr] * sg[rr] * inv;
+                    const float ab = As[(tt + q) * WLD + 16 * i + r16];
+                    acc[i] = mfma4(ga, ab, acc[i]);
                 }
             }
         }
         if (do_bias && tid < WB) {
             double cs = 0.0;
-            for (int row = 0; row < WT; ++row) cs += (double)Gs[tid * WLT + row];
+            for (int row = 0; row < WT; ++row) cs += (double)Gs[row * WLD + tid];
             bsum += cs;
         }
     }

@@ -47,47 +47,43 @@ __global__ void __launch_bounds__(256) k_pack_batch(const TO* __restrict__ obs, 
 // Column maxima of xhat over the batch (the input of the split rows' column
 // scales, common.h col_scale): cm[k] = max_t |xhat[t][k]| as f32 bits (atomicMax on
 // the bits of non-negative floats: order-independent, so deterministic), cm[n] =
-// 1 (the bias column).  One 512-thread workgroup per CU walks a contiguous range
-// of rows; thread (rsub, j) owns the V-wide column group j of rows rsub,
-// rsub + RPP, ... (RPP = 512 / (n / V) rows per pass: 5 at Humanoid, 92 % of the
-// lanes busy), four rows in flight; maxima go through LDS (ds_max_u32), then one
-// global atomicMax per column per workgroup — 256 per address, not one per
-// 2 rows' worth of workgroups (same-address atomics serialise in L2).
-constexpr int CM_THREADS = 512;
+// 1 (the bias column).  Thread (rsub, j) of a workgroup owns the V-wide column
+// group j of rows rsub, rsub + RPP, ... of the workgroup's row stride; maxima go
+// through LDS (ds_max_u32), then one global atomicMax per column per workgroup.
 template <typename TO, int V>
-__global__ void __launch_bounds__(CM_THREADS) k_colmax(const TO* __restrict__ obs, int64_t T, int n,
-                                                       const float* __restrict__ in_shift,
-                                                       const float* __restrict__ in_scale,
-                                                       unsigned* __restrict__ cm) {
+__global__ void __launch_bounds__(256) k_colmax(const TO* __restrict__ obs, int64_t T, int n,
+                                                const float* __restrict__ in_shift,
+                                                const float* __restrict__ in_scale, unsigned* __restrict__ cm) {
     __shared__ unsigned smax[512];
     const int tid = threadIdx.x;
-    for (int i = tid; i < 512; i += CM_THREADS) smax[i] = 0u;
+    for (int i = tid; i < 512; i += 256) smax[i] = 0u;
     __syncthreads();
-    const int nv = n / V;                                 // V divides n (host)
-    const int span = nv < CM_THREADS ? nv : CM_THREADS;   // column groups per pass
-    const int rpp = CM_THREADS / span;                    // rows per pass
+    const int nv = n / V;                       // V divides n (host)
+    const int span = nv < 256 ? nv : 256;       // column groups per pass
+    const int rpp = 256 / span;                 // rows per pass
     const int rsub = tid / span, j0 = tid % span;
-    const int64_t per = (T + gridDim.x - 1) / gridDim.x;
-    const int64_t rb = (int64_t)blockIdx.x * per, re = rb + per < T ? rb + per : T;
     if (rsub < rpp) {
-        constexpr int NJ = V == 4 ? 1 : 2;   // column groups per thread (n <= 511)
-        float mx[NJ][V];
-        float sh[NJ][V], den[NJ][V];
+        float mx[2][V];
 #pragma unroll
-        for (int u = 0; u < NJ; ++u)
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int e = 0; e < V; ++e) mx[u][e] = 0.f;
+        float sh[2][V], den[2][V];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
 #pragma unroll
             for (int e = 0; e < V; ++e) {
-                const int c = (j0 + CM_THREADS * u) * V + e;
-                mx[u][e] = 0.f;
+                const int c = (j0 + 256 * u) * V + e;
                 sh[u][e] = in_shift && c < n ? in_shift[c] : 0.f;
                 den[u][e] = in_shift && c < n ? in_scale[c] + 1e-8f : 1.f;
             }
+        const int64_t rstride = (int64_t)gridDim.x * rpp;
 #pragma unroll 4
-        for (int64_t row = rb + rsub; row < re; row += rpp) {
+        for (int64_t row = (int64_t)blockIdx.x * rpp + rsub; row < T; row += rstride) {
             const TO* src = obs + row * n;
 #pragma unroll
-            for (int u = 0; u < NJ; ++u) {
-                const int j = j0 + CM_THREADS * u;
+            for (int u = 0; u < 2; ++u) {
+                const int j = j0 + 256 * u;
                 if (j >= nv) continue;
                 float x[V];
                 if constexpr (V == 4 && sizeof(TO) == 4) {
@@ -106,15 +102,15 @@ __global__ void __launch_bounds__(CM_THREADS) k_colmax(const TO* __restrict__ ob
             }
         }
 #pragma unroll
-        for (int u = 0; u < NJ; ++u)
+        for (int u = 0; u < 2; ++u)
 #pragma unroll
             for (int e = 0; e < V; ++e) {
-                const int c = (j0 + CM_THREADS * u) * V + e;
-                if (c < n && (j0 + CM_THREADS * u) < nv) atomicMax(&smax[c], __float_as_uint(mx[u][e]));
+                const int c = (j0 + 256 * u) * V + e;
+                if (c < n && (j0 + 256 * u) < nv) atomicMax(&smax[c], __float_as_uint(mx[u][e]));
             }
     }
     __syncthreads();
-    for (int c = tid; c < n; c += CM_THREADS)
+    for (int c = tid; c < n; c += 256)
         if (smax[c]) atomicMax(&cm[c], smax[c]);
     if (blockIdx.x == 0 && tid == 0) atomicMax(&cm[n], __float_as_uint(1.0f));
 }
@@ -1003,12 +999,14 @@ static int obs_colscale(const TO* obs, int64_t T, const mjrl_shape* s, const flo
     hipError_t e = hipMemsetAsync(xc, 0, sizeof(float) * s->np, st);
     if (e != hipSuccess) return (int)e;
     const bool q4 = sizeof(TO) == 4 && s->n % 4 == 0 && (reinterpret_cast<uintptr_t>(obs) & 15) == 0;
-    const int g = T > 0 ? grid_for(T, 64, 256) : 1;   // one workgroup per CU, >= 64 rows each
+    const int nv = q4 ? s->n / 4 : s->n;
+    const int rpp = 256 / (nv < 256 ? nv : 256);
+    const int g = T > 0 ? grid_for(T, rpp * 8, 2048) : 1;
     if (q4)
-        hipLaunchKernelGGL((k_colmax<TO, 4>), dim3(g), dim3(CM_THREADS), 0, st, obs, T, s->n, in_shift, in_scale,
+        hipLaunchKernelGGL((k_colmax<TO, 4>), dim3(g), dim3(256), 0, st, obs, T, s->n, in_shift, in_scale,
                            reinterpret_cast<unsigned*>(xc));
     else
-        hipLaunchKernelGGL((k_colmax<TO, 1>), dim3(g), dim3(CM_THREADS), 0, st, obs, T, s->n, in_shift, in_scale,
+        hipLaunchKernelGGL((k_colmax<TO, 1>), dim3(g), dim3(256), 0, st, obs, T, s->n, in_shift, in_scale,
                            reinterpret_cast<unsigned*>(xc));
     hipLaunchKernelGGL(k_colscale, dim3(1), dim3(512), 0, st, xc, s->np);
     return err(hipGetLastError());

@@ -49,7 +49,8 @@ struct VLayout {
     static constexpr int H = 64, BT = 32;
     static constexpr int NP = 32 * KG;
     static constexpr int NFB = NP / 16;              // feature blocks of the gW0 sums
-    static constexpr int RBYTES = NP * 2;            // one f16 row of an xhat image
+    static constexpr int RBYTES = NP * 2;            // one f16 row of an xhat image (in HBM)
+    static constexpr int GBYTES = BT * 256;          // one 16-chunk group of an LDS image
     static constexpr int XIMG = BT * RBYTES;         // one hi (or lo) image of a tile
     static constexpr int LD = H + 4;                 // f32 [row][LD] exchange buffers
     static constexpr int LDG = 32 + 4;               // g [row][LDG] (MP padded to 32)
@@ -73,8 +74,11 @@ struct VLayout {
     static_assert((MP / 16) * 4 * 4 * 64 <= BT * LD * 2, "gW2 fold aliases DA0 / DA1");
 };
 
-// xhat images: 16-byte chunk c of row r sits at chunk c ^ vswz(r) (row bits 0-2 ->
-// chunk bits 1-3).  Conflict-free for the first layer's b128 row reads (rows r16,
+// xhat images, group-major: [NP / 128 groups][32 rows][16 chunks of 16 bytes]; chunk
+// c of row r sits in group c >> 4 at position (c & 15) ^ vswz(r) (row bits 0-2 ->
+// chunk bits 1-3).  Rows are 256 bytes apart (a multiple of the 64 banks, as the
+// 768-byte rows of a row-major image), so the banking is the row-major image's; one
+// LDS-DMA wave instruction (1 KB) fills four rows of one group.  Conflict-free for the first layer's b128 row reads (rows r16,
 // chunks 4s + q) and for the gW0 sums' transposed reads (rows 4q + tq and
 // 16 + 4q + tq: bit 4 of the row does not enter, so the second set is the first
 // plus 16 rows).
@@ -97,6 +101,9 @@ __device__ __forceinline__ void arow_v(const char* img, int rb, int s, int q, in
 
 __device__ __forceinline__ void astore4_v(char* img, int f, int row0, const float (&v)[4]) {
     astore4(img, f, vslot(row0), v);
+}
+__device__ __forceinline__ void aval4_v(const char* img, int f, int row0, float (&v)[4]) {
+    aval4(img, f, vslot(row0), v);
 }
 
 typedef _Float16 half4v __attribute__((ext_vector_type(4)));
@@ -198,6 +205,12 @@ __device__ __forceinline__ void dma16(const void* gsrc, unsigned lds) {
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
 }
+// the saddr form: address = sbase (wave-uniform SGPR pair) + voff (per-lane 32-bit)
+__device__ __forceinline__ void dma16s(const void* sbase, unsigned voff, unsigned lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds) : "memory");
+}
 __device__ __forceinline__ void dma4(const void* gsrc, unsigned lds) {
     unsigned keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
@@ -247,42 +260,44 @@ __global__ void __launch_bounds__(VT, 1) k_kv(RowArgs a, FOut o) {
     auto XB = [&](int b) { return sb + L::oX + b * 2 * L::XIMG; };   // hi image; lo at + XIMG
     auto US = [&](int b) { return reinterpret_cast<float*>(sb + L::oU) + b * 64; };
 
-    // ---- xhat tiles by LDS-DMA (global_load_lds_dwordx4): one wave instruction fills
-    // 1 KB of an image, lane l the 16-byte chunk 64 jj + l of it (row (64 jj + l) / 48,
-    // chunk (64 jj + l) % 48), read from the row's chunk c ^ vswz(row): the swizzle
-    // goes on the source address.  Wave w fills image w >> 1, pieces jj = 12 (w & 1)
-    // .. + 11 (rows 4a + rin, a = jj / 3, b = jj % 3): six per-lane source offsets,
-    // for b and the parity of a (row bit 2 enters the swizzle).  No registers hold the
-    // tile; the DMA of tile k+1 is in flight across I1 and I2.
-    const int ximg = w >> 1, a0p = 4 * (w & 1);
-    int xoff[3][2];
+    // ---- xhat tiles by LDS-DMA (global_load_lds_dwordx4): DMA piece jj (0..23) of an
+    // image fills group jj >> 3, rows 4 (jj & 7) .. + 3; lane l the row 4 (jj & 7) +
+    // (l >> 4), position l & 15, read from the row's chunk 16 (jj >> 3) + ((l & 15) ^
+    // vswz(row)): the swizzle goes on the source address.  vswz depends on the row's
+    // bits 0-2 = (l >> 4, jj & 1), so two per-lane source offsets serve every piece
+    // (the saddr form: wave-uniform base + per-lane offset).  Wave w fills image w >> 1,
+    // pieces 12 (w & 1) .. + 11.  No registers hold the tile; the DMA of tile k+1 is in
+    // flight across I1 and I2.
+    const int ximg = w >> 1, jj0 = 12 * (w & 1);
+    unsigned xoff[2];
 #pragma unroll
-    for (int bb = 0; bb < 3; ++bb) {
-        const int li = 64 * bb + lane, rin = li / 48, cl = li % 48;
-#pragma unroll
-        for (int ap = 0; ap < 2; ++ap) xoff[bb][ap] = rin * (4 * NP) + ximg * (2 * NP) + 16 * (cl ^ vswz(4 * ap + rin));
-    }
-    auto xdma = [&](int64_t t_, int b_) __attribute__((always_inline)) {
+    for (int par = 0; par < 2; ++par)
+        xoff[par] = (lane >> 4) * (4 * NP) + 16 * ((lane & 15) ^ vswz(4 * par + (lane >> 4)));
+    auto xdma = [&](int64_t t_, int b_, int u0, int u1) __attribute__((always_inline)) {
         const int64_t rb_ = t_ * BT;
         const int nr = (int)(T - rb_ < BT ? T - rb_ : BT);
-        if (w == 0) {   // row scales first: rows past T (and lanes 32..63) read row T - 1
+        if (w == 0 && u0 == 0) {   // row scales first: rows past T (and lanes 32..63) read row T - 1
             const int64_t ri = rb_ + lane < T ? rb_ + lane : T - 1;
             dma4(a.xu + ri, lds_addr(US(b_)));
         }
-        const char* src = reinterpret_cast<const char*>(a.xs) + rb_ * (4 * NP);
+        const char* src = reinterpret_cast<const char*>(a.xs) + rb_ * (4 * NP) + ximg * (2 * NP);
         const unsigned dst = lds_addr(XB(b_) + ximg * L::XIMG);
+        if (nr == BT) {   // wave-uniform: every tile but the batch's last
 #pragma unroll
-        for (int aa = 0; aa < 4; ++aa)
-#pragma unroll
-            for (int bb = 0; bb < 3; ++bb) {
-                const int av = a0p + aa, jj = 3 * av + bb;
-                int off = 4 * av * (4 * NP) + xoff[bb][av & 1];
-                if (nr < BT) {   // the last tile: rows past T read the tile's row 0 (finite; masked)
-                    const int li = 64 * bb + lane;
-                    if (4 * av + li / 48 >= nr) off = ximg * (2 * NP) + 16 * (li % 48);
-                }
-                dma16(src + off, dst + 1024 * jj);
+            for (int u = 0; u < 12; ++u) {
+                if (u < u0 || u >= u1) continue;
+                const int jj = jj0 + u, g = jj >> 3, rq = jj & 7;
+                dma16s(src + 4 * rq * (4 * NP) + 256 * g, xoff[rq & 1], dst + 1024 * jj);
             }
+        } else {   // the last tile: rows past T read the tile's row 0 (finite; masked)
+#pragma unroll
+            for (int u = 0; u < 12; ++u) {
+                if (u < u0 || u >= u1) continue;
+                const int jj = jj0 + u, g = jj >> 3, rq = jj & 7, row = 4 * rq + (lane >> 4);
+                const int off = row < nr ? 4 * rq * (4 * NP) + (int)xoff[rq & 1] : 16 * (lane & 15);
+                dma16(src + 256 * g + off, dst + 1024 * jj);
+            }
+        }
     };
     // cached activations of this wave's units at (rows 16i + 4q + rr, unit hcol); rows
     // past T read the tile's row 0 (finite; their output-layer weights are masked)
@@ -290,17 +305,19 @@ __global__ void __launch_bounds__(VT, 1) k_kv(RowArgs a, FOut o) {
     auto aload = [&](int64_t t_) __attribute__((always_inline)) {
         const int64_t rb_ = t_ * BT;
         const int nr = (int)(T - rb_ < BT ? T - rb_ : BT);
+        const float* b0p = a.a0 + rb_ * H + hcol;
+        const float* b1p = a.a1 + rb_ * H + hcol;
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr) {
                 const int row = i * 16 + 4 * q + rr;
-                const int64_t gi = (rb_ + (row < nr ? row : 0)) * H + hcol;
-                pn0[i][rr] = a.a0[gi];
-                pn1[i][rr] = a.a1[gi];
+                const int o = (row < nr ? row : 0) * H;
+                pn0[i][rr] = b0p[o];
+                pn1[i][rr] = b1p[o];
             }
     };
-    xdma(blockIdx.x, 0);
+    xdma(blockIdx.x, 0, 0, 12);
     aload(blockIdx.x);
 
     // ---- launch preamble: W1 / W2 images (column-scaled), register fragments ----
@@ -380,18 +397,16 @@ __global__ void __launch_bounds__(VT, 1) k_kv(RowArgs a, FOut o) {
     const float f1 = sc1[hcol], f2 = sc2[hcol];
     const float fw = wsc * f1;
 
-    // per-lane LDS offsets: P1 row reads (row r16, chunk 4s + q: 4 residues of s & 3;
-    // s >> 2 adds 256 bytes), P6 transposed reads (rows 4q + tq, chunk 2 fb + (tp >> 1):
-    // 8 residues of fb & 7; fb >> 3 adds 256 bytes)
-    int p1o[4], p6o[8];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) p1o[c] = r16 * L::RBYTES + 16 * ((4 * c + q) ^ vswz(r16));
-    {
-        const int row = 4 * q + (r16 >> 2);
-#pragma unroll
-        for (int c = 0; c < 8; ++c)
-            p6o[c] = row * L::RBYTES + 16 * ((2 * c + ((r16 >> 1) & 1)) ^ vswz(row)) + 8 * (r16 & 1);
-    }
+    // per-lane LDS offsets.  P1 row reads: row i*16 + r16, chunk 4s + q = group s >> 2,
+    // position (4 (s & 3) + q) ^ vswz(r16) = 4 ((s & 3) ^ k1) + (q ^ (vswz & 3)).  P6
+    // transposed reads: rows 4q + tq (+16), chunk 2 fb + (tp >> 1) = group fb >> 3,
+    // position 2 ((fb & 7) ^ k6) + (tp >> 1).  Two registers each instead of 4 + 8.
+    const int sw1 = vswz(r16), k1 = sw1 >> 2;
+    const int p1b = r16 * 256 + 16 * (q ^ (sw1 & 3));
+    const int prow = 4 * q + (r16 >> 2), k6 = vswz(prow) >> 1;
+    const int p6b = prow * 256 + 16 * ((r16 >> 1) & 1) + 8 * (r16 & 1);
+    auto p1off = [&](int s_) { return p1b + 64 * ((s_ & 3) ^ k1) + L::GBYTES * (s_ >> 2); };
+    auto p6off = [&](int fb_) { return p6b + 32 * ((fb_ & 7) ^ k6) + L::GBYTES * (fb_ >> 3); };
 
     floatx4 acc1[2];
     auto p1 = [&](int b, int s0, int s1) __attribute__((always_inline)) {
@@ -401,12 +416,11 @@ __global__ void __launch_bounds__(VT, 1) k_kv(RowArgs a, FOut o) {
             if (s < s0 || s >= s1) continue;
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                const int off = p1o[s & 3] + 256 * (s >> 2) + i * 16 * L::RBYTES;   // rows i*16 + r16: same swizzle
+                const int off = p1off(s) + i * 16 * 256;   // rows i*16 + r16: same swizzle
                 const half8 xh8 = *reinterpret_cast<const half8*>(xh + off);
                 const half8 xl8 = *reinterpret_cast<const half8*>(xh + L::XIMG + off);
                 acc1[i] = mfma_x3(xh8, xl8, wh[s], wl[s], acc1[i]);
             }
-            if (s & 1) __builtin_amdgcn_sched_barrier(0);
         }
     };
     // da0 = (1 - a0^2) dz0, dz0 = P1 * xu * wsc; times W1's column scale (fold for P2)
@@ -448,7 +462,6 @@ __global__ void __launch_bounds__(VT, 1) k_kv(RowArgs a, FOut o) {
     // gW2 keep running scales (run_rescale).
     float S0 = 0.f, S1 = 0.f, S2 = 0.f;
     bool ovf = false;   // this wave's slab entries hold gW0 sums of past-headroom tiles
-    float pa0[2][4], pa1[2][4];   // this tile's activations of the wave's units
 
     // ---- prologue: tile blockIdx.x through P1, its images, the next tile's loads ----
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of xhat(t0)
@@ -458,14 +471,6 @@ __global__ void __launch_bounds__(VT, 1) k_kv(RowArgs a, FOut o) {
     p1(0, 0, KG);
     p1_epi(0);
     next_images();
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-            pa0[i][rr] = pn0[i][rr];
-            pa1[i][rr] = pn1[i][rr];
-        }
-    if (blockIdx.x + G < ntiles) aload(blockIdx.x + G);
     __syncthreads();
 #ifdef MJRL_KX_PROF
     kx_last_ = __builtin_amdgcn_s_memtime();
@@ -482,10 +487,13 @@ __global__ void __launch_bounds__(VT, 1) k_kv(RowArgs a, FOut o) {
 
         // ===== I1: the DMA of xhat(k+1) into the free buffer; P2(k): dz1 = da0 W1^T +
         // a0 dW1^T + db1, da1 = (1 - a1^2) dz1 (times W2's column scale, P3's fold) =====
-        if (nx) xdma(kn, b ^ 1);
+        // half of the DMA of xhat(k+1) now, half between P2's row blocks (an LDS-DMA
+        // piece costs the issuing wave ~150 cycles; spread, it runs in P2's LDS waits)
+        if (nx) xdma(kn, b ^ 1, 0, 6);
         KX_STAMP(11);
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
+            if (i == 1 && nx) xdma(kn, b ^ 1, 6, 12);
             half8 ah[2], al[2];
             const float rinv = adyn<2>(DA0, L::LD, i, q, r16, nullptr, ah, al);
             floatx4 acc = zero4(), accb = zero4();
@@ -497,11 +505,13 @@ __global__ void __launch_bounds__(VT, 1) k_kv(RowArgs a, FOut o) {
                 arow_v(A0i, i, s, q, r16, xh, xl);
                 accb = mfma_x3(xh, xl, d1h[s], d1l[s], accb);
             }
+            float a4[4];   // a1 of this tile at (rows 16i + 4q + rr, unit hcol), from the image
+            aval4_v(A1i, hcol, i * 16 + 4 * q, a4);
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr) {
                 const float ri = __shfl(rinv, 4 * q + rr, 64);
                 const float v = acc[rr] * ri + accb[rr] * isd1 + db1;
-                const float av = pa1[i][rr];
+                const float av = a4[rr];
                 DA1[(i * 16 + 4 * q + rr) * L::LD + hcol] = (1.f - av * av) * v * f2;
             }
         }
@@ -555,6 +565,10 @@ __global__ void __launch_bounds__(VT, 1) k_kv(RowArgs a, FOut o) {
                 g2[hb] = mfma16_x3(gh, gl, bh, bl, g2[hb]);
             }
         }
+        // the next tile's activations (consumed in I4); their wait is the drain below.
+        // Loaded here rather than in I4: the compiler waits for every outstanding load
+        // before an asm statement with a memory clobber (the DMA issue of I1)
+        if (nx) aload(kn);
         KX_STAMP(2);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of xhat(k+1)
         __syncthreads();   // P1(k+1) reads xhat(k+1) from I3 on
@@ -562,6 +576,12 @@ __global__ void __launch_bounds__(VT, 1) k_kv(RowArgs a, FOut o) {
 
         // ===== I3: P4(k): gu1 = (1 - a1^2) (g W2) (W2's column scale on the lane's unit);
         // the gW1 sums from gu1's output registers; P1(k+1) first half =====
+        // P1(k+1) first half: no branch around it (past the last tile it reads a stale
+        // buffer; its results are never used), so it shares P4's basic block and the
+        // scheduler can issue its MFMAs into P4's LDS / shuffle latency
+        acc1[0] = zero4();
+        acc1[1] = zero4();
+        p1(b ^ 1, 0, KG / 2);
         {
             float gu[2][4];
             half8 bh, bl;
@@ -571,14 +591,17 @@ __global__ void __launch_bounds__(VT, 1) k_kv(RowArgs a, FOut o) {
                 half8 ah[1], al[1];
                 const float rinv = adyn<1>(GP, L::LDG, i, q, r16, nullptr, ah, al);
                 const floatx4 acc = mfma_x3(ah[0], al[0], bh, bl, zero4());
+                float a4[4];
+                aval4_v(A1i, hcol, i * 16 + 4 * q, a4);
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) {
                     const float ri = __shfl(rinv, 4 * q + rr, 64);
-                    const float av = pa1[i][rr];
+                    const float av = a4[rr];
                     gu[i][rr] = (1.f - av * av) * (acc[rr] * ri * f2);
                     DA1[(i * 16 + 4 * q + rr) * L::LD + hcol] = gu[i][rr];
                 }
             }
+            KX_STAMP(4);
             // gW1[j][h] += sum_rows gu1[row][j] a0[row][h]: A = gu1^T (m = j = hcol, K =
             // the interleaved rows of lane group q), B = the a0 image (slots 8q..8q+7)
             const float8v v = {gu[0][0], gu[0][1], gu[0][2], gu[0][3], gu[1][0], gu[1][1], gu[1][2], gu[1][3]};
@@ -593,13 +616,6 @@ __global__ void __launch_bounds__(VT, 1) k_kv(RowArgs a, FOut o) {
                 g1[hb] = mfma_x3(gh, gl, ch, cl, g1[hb]);
             }
         }
-        __builtin_amdgcn_sched_barrier(0);
-        KX_STAMP(4);
-        if (nx) {
-            acc1[0] = zero4();
-            acc1[1] = zero4();
-            p1(b ^ 1, 0, KG / 2);
-        }
         KX_STAMP(5);
         __syncthreads();
         KX_STAMP(6);
@@ -607,6 +623,7 @@ __global__ void __launch_bounds__(VT, 1) k_kv(RowArgs a, FOut o) {
         // ===== I4: P5(k): gu0 = (1 - a0^2) (gu1 W1) xu (W1's column scale on the lane's
         // unit; xu folds the rows' scale into the gW0 sums); P6(k): gW0 += gu0^T xhat;
         // P1(k+1) second half and epilogue, the a0 / a1 images of k+1, loads of k+2 =====
+        p1(b ^ 1, KG / 2, KG);   // P1(k+1) second half, beside P5 (no branch around it either)
         {
             float8v v;
             {
@@ -623,10 +640,12 @@ __global__ void __launch_bounds__(VT, 1) k_kv(RowArgs a, FOut o) {
                     for (int s = 0; s < 2; ++s) acc = mfma_x3(ah[s], al[s], bh[s], bl[s], acc);
                     const float4 u4 = *reinterpret_cast<const float4*>(us + i * 16 + 4 * q);
                     const float uu[4] = {u4.x, u4.y, u4.z, u4.w};
+                    float a4[4];
+                    aval4_v(A0i, hcol, i * 16 + 4 * q, a4);
 #pragma unroll
                     for (int rr = 0; rr < 4; ++rr) {
                         const float ri = __shfl(rinv, 4 * q + rr, 64);
-                        const float av = pa0[i][rr];
+                        const float av = a4[rr];
                         v[4 * i + rr] = (1.f - av * av) * (acc[rr] * ri * f1) * uu[rr];
                     }
                 }
@@ -652,15 +671,13 @@ __global__ void __launch_bounds__(VT, 1) k_kv(RowArgs a, FOut o) {
                 float s4[4];
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) s4[rr] = __shfl(inv, 4 * q + rr, 64);
-                const int prow = 4 * q + (r16 >> 2), psw = vswz(prow);
                 float* wp = o.wpart + (int64_t)blockIdx.x * 64;
                 const int64_t S64 = (int64_t)gridDim.x * 64;
 #pragma unroll 1
                 for (int fb = 0; fb < NFB; ++fb) {
-                    const int off = prow * L::RBYTES + 16 * ((2 * (fb & 7) + ((r16 >> 1) & 1)) ^ psw) + 8 * (r16 & 1) +
-                                    256 * (fb >> 3);
-                    const half8 th = cat_tr(ds_read_tr16(xh + off), ds_read_tr16(xh + off + 16 * L::RBYTES));
-                    const half8 tl = cat_tr(ds_read_tr16(xh + L::XIMG + off), ds_read_tr16(xh + L::XIMG + off + 16 * L::RBYTES));
+                    const int off = p6off(fb);
+                    const half8 th = cat_tr(ds_read_tr16(xh + off), ds_read_tr16(xh + off + 16 * 256));
+                    const half8 tl = cat_tr(ds_read_tr16(xh + L::XIMG + off), ds_read_tr16(xh + L::XIMG + off + 16 * 256));
                     const floatx4 t = mfma_x3(gh, gl, th, tl, zero4());
                     const int kf = fb * 16 + r16;
 #pragma unroll
@@ -684,28 +701,19 @@ __global__ void __launch_bounds__(VT, 1) k_kv(RowArgs a, FOut o) {
                 split8(v, tovf ? 0.f : S0, gh, gl);
 #pragma unroll
                 for (int fb = 0; fb < NFB; ++fb) {
-                    const int off = p6o[fb & 7] + 256 * (fb >> 3);
-                    const half8 th = cat_tr(ds_read_tr16(xh + off), ds_read_tr16(xh + off + 16 * L::RBYTES));
-                    const half8 tl = cat_tr(ds_read_tr16(xh + L::XIMG + off), ds_read_tr16(xh + L::XIMG + off + 16 * L::RBYTES));
+                    const int off = p6off(fb);
+                    const half8 th = cat_tr(ds_read_tr16(xh + off), ds_read_tr16(xh + off + 16 * 256));
+                    const half8 tl = cat_tr(ds_read_tr16(xh + L::XIMG + off), ds_read_tr16(xh + L::XIMG + off + 16 * 256));
                     g0[fb] = mfma_x3(gh, gl, th, tl, g0[fb]);
                     if (fb & 1) __builtin_amdgcn_sched_barrier(0);
                 }
             }
         }
         KX_STAMP(8);
-        if (nx) {
-            p1(b ^ 1, KG / 2, KG);
-            p1_epi(b ^ 1);
-            next_images();
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int rr = 0; rr < 4; ++rr) {
-                    pa0[i][rr] = pn0[i][rr];
-                    pa1[i][rr] = pn1[i][rr];
-                }
-            if (kn + G < ntiles) aload(kn + G);
-        }
+        p1_epi(b ^ 1);   // past the last tile: stale values into buffers nothing reads again
+        KX_STAMP(19);
+        next_images();
+        KX_STAMP(20);
         KX_STAMP(9);
         __syncthreads();
         KX_STAMP(10);

@@ -6,8 +6,7 @@ TAG=${1:-kv}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-K=${2:+-k "$2"}
-MJRL_AMD_FVP=kv timeout -k 10 400 python -u -m pytest tests/test_gpu_split.py tests/test_gpu_parity.py -x -v --timeout 120 --timeout-method thread $K > $OUT/t.log 2>&1 || { echo "TESTS FAILED"; grep -E "FAILED|Error|error|assert" $OUT/t.log | head -30; tail -5 $OUT/t.log; exit 1; }
+MJRL_AMD_FVP=kv timeout -k 10 400 python -u -m pytest tests/test_gpu_split.py tests/test_gpu_parity.py -x -v --timeout 120 --timeout-method thread ${2:+-k} ${2:+"$2"} > $OUT/t.log 2>&1 || { echo "TESTS FAILED"; grep -E "FAILED|Error|error|assert" $OUT/t.log | head -30; tail -5 $OUT/t.log; exit 1; }
 tail -1 $OUT/t.log
 for v in kv kx; do
   MJRL_AMD_FVP=$v timeout -k 10 200 python -u bench.py --steps 8 --warmup 2 --no-cpu-baseline --no-e2e --no-f32 > $OUT/b_$v.json 2> $OUT/b_$v.err || { echo "bench $v failed"; tail $OUT/b_$v.err; exit 1; }

@@ -15,8 +15,8 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 from mjrl_amd import _lib  # noqa: E402
 from mjrl_amd.engine import UpdateEngine  # noqa: E402
 
-NAMES = ["I1 P2", "I1 barrier", "I2 P3+gW2", "I2 DMA wait+bar", "I3 P4+gW1", "I3 P1a", "I3 barrier",
-         "I4 P5", "I4 P6", "I4 P1b+epi+img", "I4 barrier", "I1 DMA issue"]
+NAMES = ["I1 P2 (+DMA half)", "I1 barrier", "I2 P3+gW2+aload", "I2 DMA wait+bar", "I3 P1a+P4", "I3 gW1",
+         "I3 barrier", "I4 P1b+P5", "I4 P6", "I4 -", "I4 barrier", "I1 DMA issue"]
 NPROF = 24
 
 
@@ -55,7 +55,9 @@ def main(T=1000000, reps=3):
     print("cycles per tile (wave 0 of workgroup 0):")
     for i, n in enumerate(NAMES):
         print("  %-18s %8.0f" % (n, r[i] / tiles))
-    print("  %-18s %8.0f" % ("total", r[:12].sum() / tiles))
+    for i, n in ((19, " I4 epilogue"), (20, " I4 images")):
+        print("  %-18s %8.0f" % (n, r[i] / tiles))
+    print("  %-18s %8.0f" % ("total", (r[:12].sum() + r[18:21].sum()) / tiles))
     print("preamble + prologue %8.0f   tail %8.0f   past-headroom tiles %.1f" % (r[15], r[16], r[12]))
 
 

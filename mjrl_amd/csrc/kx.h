@@ -438,20 +438,39 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
     const float wsc1 = MODE == FVP ? wsc * sc1[cb * 16 + r16] : wsc;
     // P1's xhat-image offsets (row r16, chunk kh*KH/8 + 4s + q, swizzled): tile-invariant,
     // kept in KS registers instead of being recomputed per tile
+#ifndef MJRL_KX_OFFREG
+    // computed per use from three per-lane values (2 VALU each: add, xor-add) instead of
+    // KS + KG live offsets: the FVP's register file then has no spills, whose scratch
+    // reloads waited in order (vmcnt) on the next tile's HBM prefetch loads
+    const int p1A = 16 * (kh * (KH / 8) + q), p1B = 16 * chunk_swz(r16), p1C = r16 * L::RBYTES;
+    auto p1off_at = [&](int s, int opq_) { return (((p1A + opq_) + 64 * s) ^ p1B) + p1C; };
+#else
     int p1off[KS];
 #pragma unroll
     for (int s = 0; s < KS; ++s) p1off[s] = r16 * L::RBYTES + 16 * ((kh * (KH / 8) + 4 * s + q) ^ chunk_swz(r16));
+    auto p1off_at = [&](int s, int) { return p1off[s]; };
+#endif
     // and the transposed-read offsets of the gW0 sums (group g: rows 8q + tq, chunk
     // kh*KH/8 + tp/2 + 2g, half tp & 1), kept in registers (FWD / FVP)
     auto gw0_off = [&](int r_, int q_, int g) {
         const int tq = r_ >> 2, tp = r_ & 3, row = 8 * q_ + tq;
         return row * L::RBYTES + 16 * (((kh * KH) / 8 + (tp >> 1) + 2 * g) ^ chunk_swz(row)) + 8 * (tp & 1);
     };
+#ifndef MJRL_KX_OFFREG
+    // gw0_off(r16, q, g) = ((g0A + 32 g) ^ g0B) + g0C (the chunk term 16 ((kh KH/8 + tp/2 +
+    // 2g) ^ swz) with the row's swizzle bits 1-3 and the half / row terms added after)
+    const int g0row = 8 * q + (r16 >> 2);
+    const int g0A = 16 * ((kh * KH) / 8 + ((r16 & 3) >> 1)), g0B = 16 * chunk_swz(g0row),
+              g0C = g0row * L::RBYTES + 8 * (r16 & 1);
+    auto g0off_at = [&](int g, int opq_) { return (((g0A + opq_) + 32 * g) ^ g0B) + g0C; };
+#else
     int g0off[MODE != EVAL ? KG : 1];
     if constexpr (MODE != EVAL) {
 #pragma unroll
         for (int g = 0; g < KG; ++g) g0off[g] = gw0_off(r16, q, g);
     }
+    auto g0off_at = [&](int g, int) { return g0off[g]; };
+#endif
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         KX_STAMP(9);   // loop top (the wait on the previous tile's last barrier)
         // per-lane indices through an opaque zero: recomputed per tile rather than
@@ -540,7 +559,7 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
             for (int s = 0; s < KS; ++s) {
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
-                    const int off = p1off[s] + i * 16 * L::RBYTES;   // row i*16 + r16: same swizzle
+                    const int off = p1off_at(s, opq) + i * 16 * L::RBYTES;   // row i*16 + r16: same swizzle
                     const half8 xh = *reinterpret_cast<const half8*>(XHb + off);
                     const half8 xl = *reinterpret_cast<const half8*>(XLb + off);
                     acc1[i] = mfma_x3(xh, xl, wh[s], wl[s], acc1[i]);
@@ -861,7 +880,7 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
                 for (int h = 0; h < 2; ++h) {
                     // rows 8q + 4h + tq: the chunk swizzle ignores row bit 2, so h = 1 is
                     // the h = 0 offset plus four rows
-                    const int off = g0off[g] + h * 4 * L::RBYTES;
+                    const int off = g0off_at(g, opq) + h * 4 * L::RBYTES;
                     th[h] = ds_read_tr16(XHb + off);
                     tl[h] = ds_read_tr16(XLb + off);
                 }

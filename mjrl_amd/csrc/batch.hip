@@ -48,69 +48,61 @@ __global__ void __launch_bounds__(256) k_pack_batch(const TO* __restrict__ obs, 
 // scales, common.h col_scale): cm[k] = max_t |xhat[t][k]| as f32 bits (atomicMax on
 // the bits of non-negative floats: order-independent, so deterministic), cm[n] =
 // 1 (the bias column).  Thread (rsub, j) of a workgroup owns the V-wide column
-// group j of rows rsub, rsub + RPP, ... of the workgroup's row stride; maxima go
-// through LDS (ds_max_u32), then one global atomicMax per column per workgroup.
-template <typename TO, int V>
-__global__ void __launch_bounds__(256) k_colmax(const TO* __restrict__ obs, int64_t T, int n,
+// group j (n / V <= NT groups: np <= 512) of rows rsub, rsub + RPP, ... of the
+// workgroup's row stride, CR rows per batch with every load issued before the
+// first max: rows past T are clamped to row T - 1 (a max is idempotent), so the
+// batch has no branches between its loads.  Maxima go through LDS (ds_max_u32),
+// then one global atomicMax per column per workgroup.
+template <typename TO, int V, int NT>
+__global__ void __launch_bounds__(NT) k_colmax(const TO* __restrict__ obs, int64_t T, int n,
                                                 const float* __restrict__ in_shift,
                                                 const float* __restrict__ in_scale, unsigned* __restrict__ cm) {
+    constexpr int CR = 8;
     __shared__ unsigned smax[512];
     const int tid = threadIdx.x;
-    for (int i = tid; i < 512; i += 256) smax[i] = 0u;
+    for (int i = tid; i < 512; i += NT) smax[i] = 0u;
     __syncthreads();
     const int nv = n / V;                       // V divides n (host)
-    const int span = nv < 256 ? nv : 256;       // column groups per pass
-    const int rpp = 256 / span;                 // rows per pass
-    const int rsub = tid / span, j0 = tid % span;
+    const int rpp = NT / nv;                    // rows per pass
+    const int rsub = tid / nv, j = tid % nv;
     if (rsub < rpp) {
-        float mx[2][V];
+        float mx[V], sh[V], den[V];
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
-#pragma unroll
-            for (int e = 0; e < V; ++e) mx[u][e] = 0.f;
-        float sh[2][V], den[2][V];
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-#pragma unroll
-            for (int e = 0; e < V; ++e) {
-                const int c = (j0 + 256 * u) * V + e;
-                sh[u][e] = in_shift && c < n ? in_shift[c] : 0.f;
-                den[u][e] = in_shift && c < n ? in_scale[c] + 1e-8f : 1.f;
-            }
+        for (int e = 0; e < V; ++e) {
+            const int c = j * V + e;
+            mx[e] = 0.f;
+            sh[e] = in_shift ? in_shift[c] : 0.f;
+            den[e] = in_shift ? in_scale[c] + 1e-8f : 1.f;
+        }
         const int64_t rstride = (int64_t)gridDim.x * rpp;
-#pragma unroll 4
-        for (int64_t row = (int64_t)blockIdx.x * rpp + rsub; row < T; row += rstride) {
-            const TO* src = obs + row * n;
+        for (int64_t row0 = (int64_t)blockIdx.x * rpp + rsub; row0 < T; row0 += CR * rstride) {
+            float x[CR][V];
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const int j = j0 + 256 * u;
-                if (j >= nv) continue;
-                float x[V];
+            for (int i = 0; i < CR; ++i) {
+                const int64_t row = min(row0 + i * rstride, T - 1);
+                const TO* src = obs + row * n + V * j;
                 if constexpr (V == 4 && sizeof(TO) == 4) {
-                    const float4 q = *reinterpret_cast<const float4*>(src + 4 * j);
-                    x[0] = q.x; x[1] = q.y; x[2] = q.z; x[3] = q.w;
+                    const float4 q = *reinterpret_cast<const float4*>(src);
+                    x[i][0] = q.x; x[i][1] = q.y; x[i][2] = q.z; x[i][3] = q.w;
                 } else {
 #pragma unroll
-                    for (int e = 0; e < V; ++e) x[e] = (float)src[V * j + e];   // torch .float()
+                    for (int e = 0; e < V; ++e) x[i][e] = (float)src[e];   // torch .float()
                 }
+            }
+#pragma unroll
+            for (int i = 0; i < CR; ++i)
 #pragma unroll
                 for (int e = 0; e < V; ++e) {
-                    float v = x[e];
-                    if (in_shift) v = (v - sh[u][e]) / den[u][e];   // MuNet.forward:177, as the pack
-                    mx[u][e] = fmaxf(mx[u][e], fabsf(v));
+                    float v = x[i][e];
+                    if (in_shift) v = (v - sh[e]) / den[e];   // MuNet.forward:177, as the pack
+                    mx[e] = fmaxf(mx[e], fabsf(v));
                 }
-            }
         }
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
-#pragma unroll
-            for (int e = 0; e < V; ++e) {
-                const int c = (j0 + 256 * u) * V + e;
-                if (c < n && (j0 + 256 * u) < nv) atomicMax(&smax[c], __float_as_uint(mx[u][e]));
-            }
+        for (int e = 0; e < V; ++e) atomicMax(&smax[j * V + e], __float_as_uint(mx[e]));
     }
     __syncthreads();
-    for (int c = tid; c < n; c += 256)
+    for (int c = tid; c < n; c += NT)
         if (smax[c]) atomicMax(&cm[c], smax[c]);
     if (blockIdx.x == 0 && tid == 0) atomicMax(&cm[n], __float_as_uint(1.0f));
 }
@@ -1000,13 +992,16 @@ static int obs_colscale(const TO* obs, int64_t T, const mjrl_shape* s, const flo
     if (e != hipSuccess) return (int)e;
     const bool q4 = sizeof(TO) == 4 && s->n % 4 == 0 && (reinterpret_cast<uintptr_t>(obs) & 15) == 0;
     const int nv = q4 ? s->n / 4 : s->n;
-    const int rpp = 256 / (nv < 256 ? nv : 256);
-    const int g = T > 0 ? grid_for(T, rpp * 8, 2048) : 1;
+    // 512 workgroups: 512 atomicMax per column (2048 took 56 vs 41 us at 125k rows,
+    // the same 290-300 us at 1M: tools/colmax_probe.py, profiles/r03i/colmax_probe.txt)
+    constexpr int NT = 512;
+    const int rpp = NT / nv;
+    const int g = T > 0 ? grid_for(T, rpp * 16, 512) : 1;
     if (q4)
-        hipLaunchKernelGGL((k_colmax<TO, 4>), dim3(g), dim3(256), 0, st, obs, T, s->n, in_shift, in_scale,
+        hipLaunchKernelGGL((k_colmax<TO, 4, NT>), dim3(g), dim3(NT), 0, st, obs, T, s->n, in_shift, in_scale,
                            reinterpret_cast<unsigned*>(xc));
     else
-        hipLaunchKernelGGL((k_colmax<TO, 1>), dim3(g), dim3(256), 0, st, obs, T, s->n, in_shift, in_scale,
+        hipLaunchKernelGGL((k_colmax<TO, 1, NT>), dim3(g), dim3(NT), 0, st, obs, T, s->n, in_shift, in_scale,
                            reinterpret_cast<unsigned*>(xc));
     hipLaunchKernelGGL(k_colscale, dim3(1), dim3(512), 0, st, xc, s->np);
     return err(hipGetLastError());

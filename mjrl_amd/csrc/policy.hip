@@ -661,6 +661,245 @@ __global__ void __launch_bounds__(NTHREADS, 2) k_wgrad(WArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// All three weight gradients of one row slice in ONE workgroup (MLP, H0 = H1 = H):
+//   gW0[H][NP] += gu0^T xhat,  gW1[H][H] += gu1^T a0 (+ gb1),  gW2[MP][H] += gp^T a1 (+ gb2)
+// k_wgrad gives each 64 x 64 output block its own workgroup, so every row tile of
+// gu1 / a0 / ... is fetched once per block that reads it (HalfCheetah: 2x the
+// bytes it needs, and half the CUs at its 128 slices).  Here a workgroup stages
+// each row tile of the six inputs into LDS once (register prefetch of the next
+// tile under this tile's MFMAs) and every output block of all three products is
+// an accumulator in some wave: wave w owns the 16-row strips w + NW t of gW1 and
+// gW0 (a strip's gu fragment feeds all its column blocks) and BW2 blocks of gW2.
+// Slab layout, slices and gather exactly as k_wgrad's (make_jobs), fixed order.
+// ---------------------------------------------------------------------------
+__host__ __device__ constexpr int wall_ld(int w) {   // LDS row stride: w <= ld, ld % 64 in {16, 48}
+    return (w % 64 == 0) ? w + 16 : (w % 64 <= 16 ? w - w % 64 + 16 : (w % 64 <= 48 ? w - w % 64 + 48 : w - w % 64 + 80));
+}
+
+// v where c holds, else zero, component by component (a select of the whole float4
+// made the compiler select between two stack addresses and reload through scratch)
+__device__ __forceinline__ float4 sel4(bool c, float4 v) {
+    return make_float4(c ? v.x : 0.f, c ? v.y : 0.f, c ? v.z : 0.f, c ? v.w : 0.f);
+}
+
+template <int H, int MP, int NPBM>
+struct WallCfg {
+    static constexpr int NW = H / 16 < 8 ? H / 16 : 8;   // waves
+    static constexpr int NT = 64 * NW;
+    static constexpr int SPW = (H / 16) / NW;            // gW1 / gW0 strips per wave
+    static constexpr int BW2 = (MP / 16) * (H / 16) / NW;   // gW2 blocks per wave
+    static constexpr int BT = 32;                        // rows per staged tile
+    static constexpr int LDH = wall_ld(H), LDP = wall_ld(MP), LDX = wall_ld(16 * NPBM);
+    static constexpr int oG0 = 0, oG1 = oG0 + BT * LDH, oGP = oG1 + BT * LDH, oX = oGP + BT * LDP,
+                         oA0 = oX + BT * LDX, oA1 = oA0 + BT * LDH, total = oA1 + BT * LDH;
+    static constexpr int bytes = total * 4;
+};
+
+struct WallArgs {
+    const float *gu0, *gu1, *gp, *x, *a0, *a1;
+    int np, S;
+    int64_t T, rows_per_slice;
+    float* wpart;
+    int64_t off0, off1, boff1, off2, boff2;   // make_jobs slab offsets (slice 0)
+    const int32_t* done;
+};
+
+// PART 0: all three products (the kernel below); 1: gW1 + gb1 only, 2: gW0, gW2 + gb2
+// only (the two-workgroups-per-slice split measured for 256-wide layers, not used)
+template <int H, int MP, int NPBM, int PART>
+__device__ __forceinline__ void wall_body(const WallArgs& a, int s, float* sm) {
+    using C = WallCfg<H, MP, NPBM>;
+    constexpr int BT = C::BT, NW = C::NW, SPW = C::SPW, BW2 = C::BW2, HB = H / 16;
+    constexpr bool J1 = PART != 2, J02 = PART != 1;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r16 = lane & 15, q = lane >> 4;
+    const int np = a.np, npb = np / 16;
+    const int64_t r0 = (int64_t)s * a.rows_per_slice;
+    const int64_t r1 = r0 + a.rows_per_slice < a.T ? r0 + a.rows_per_slice : a.T;
+
+    // Staging of a tile: every load unconditional (rows past the slice clamped to its
+    // last row, masked to zero when stored to LDS; surplus threads of the narrow gp /
+    // x pieces re-read a valid piece and store nothing), so no load sits under a
+    // branch and none waits for another (in-order vmcnt; a branchy per-piece decode
+    // measured 114 vs 87 us for k_wgrad).  H-wide inputs: PH float4 per thread, a
+    // compile-time row / column decode.
+    constexpr int PH = BT * H / 4 / C::NT;   // float4 per thread of one H-wide input
+    static_assert(PH * C::NT == BT * H / 4, "H-wide staging");
+    constexpr int QP = BT * MP / 4, PP = (QP + C::NT - 1) / C::NT;                // gp pieces
+    constexpr int PX = (BT * 16 * NPBM / 4 + C::NT - 1) / C::NT;               // x pieces (np <= 16 NPBM)
+    const int qx = BT * np / 4;
+    int prow[PP], pc4[PP], xrow[PX], xc4[PX];
+#pragma unroll
+    for (int u = 0; u < PP; ++u) {
+        const int i = tid + u * C::NT, ic = i < QP ? i : QP - 1;
+        prow[u] = ic / (MP / 4);
+        pc4[u] = ic % (MP / 4);
+    }
+#pragma unroll
+    for (int u = 0; u < PX; ++u) {
+        const int i = tid + u * C::NT, ic = i < qx ? i : qx - 1;
+        xrow[u] = ic / (np / 4);
+        xc4[u] = ic % (np / 4);
+    }
+    float4 sG0[PH], sG1[PH], sA0[PH], sA1[PH], sp[PP], sx[PX];
+    auto hload = [&](float4 (&dst)[PH], const float* src, int64_t t0) __attribute__((always_inline)) {
+        const int64_t tl = r1 - 1;
+#pragma unroll
+        for (int u = 0; u < PH; ++u) {
+            const int i = tid + u * C::NT, row = i / (H / 4), c4 = i % (H / 4);
+            const int64_t t = t0 + row < tl ? t0 + row : tl;
+            dst[u] = *reinterpret_cast<const float4*>(src + t * H + 4 * c4);
+        }
+    };
+    auto hstore = [&](const float4 (&v)[PH], int off, int64_t t0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int u = 0; u < PH; ++u) {
+            const int i = tid + u * C::NT, row = i / (H / 4), c4 = i % (H / 4);
+            *reinterpret_cast<float4*>(sm + off + row * C::LDH + 4 * c4) = sel4(t0 + row < r1, v[u]);
+        }
+    };
+    auto gload = [&](int64_t t0) {
+        const int64_t tl = r1 - 1;
+        if constexpr (J02) hload(sG0, a.gu0, t0);
+        if constexpr (J1) hload(sG1, a.gu1, t0);
+        if constexpr (J1) hload(sA0, a.a0, t0);
+        if constexpr (J02) hload(sA1, a.a1, t0);
+        if constexpr (J02) {
+#pragma unroll
+            for (int u = 0; u < PP; ++u) {
+                const int64_t tp = t0 + prow[u] < tl ? t0 + prow[u] : tl;
+                sp[u] = *reinterpret_cast<const float4*>(a.gp + tp * MP + 4 * pc4[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < PX; ++u) {
+                const int64_t tx = t0 + xrow[u] < tl ? t0 + xrow[u] : tl;
+                sx[u] = *reinterpret_cast<const float4*>(a.x + tx * np + 4 * xc4[u]);
+            }
+        }
+    };
+    auto sstore = [&](int64_t t0) {
+        if constexpr (J02) hstore(sG0, C::oG0, t0);
+        if constexpr (J1) hstore(sG1, C::oG1, t0);
+        if constexpr (J1) hstore(sA0, C::oA0, t0);
+        if constexpr (J02) hstore(sA1, C::oA1, t0);
+        if constexpr (J02) {
+#pragma unroll
+            for (int u = 0; u < PP; ++u)
+                if (tid + u * C::NT < QP)
+                    *reinterpret_cast<float4*>(sm + C::oGP + prow[u] * C::LDP + 4 * pc4[u]) = sel4(t0 + prow[u] < r1, sp[u]);
+#pragma unroll
+            for (int u = 0; u < PX; ++u)
+                if (tid + u * C::NT < qx)
+                    *reinterpret_cast<float4*>(sm + C::oX + xrow[u] * C::LDX + 4 * xc4[u]) = sel4(t0 + xrow[u] < r1, sx[u]);
+        }
+    };
+
+    constexpr int S1 = J1 ? SPW : 0, S0 = J02 ? SPW : 0, B2 = J02 ? BW2 : 0;
+    floatx4 acc1[S1 ? S1 : 1][HB], acc0[S0 ? S0 : 1][NPBM], acc2[B2 ? B2 : 1];
+#pragma unroll
+    for (int t = 0; t < SPW; ++t) {
+#pragma unroll
+        for (int kb = 0; kb < HB; ++kb) acc1[t < S1 ? t : 0][kb] = zero4();
+#pragma unroll
+        for (int kb = 0; kb < NPBM; ++kb) acc0[t < S0 ? t : 0][kb] = zero4();
+    }
+#pragma unroll
+    for (int b = 0; b < BW2; ++b) acc2[b < B2 ? b : 0] = zero4();
+    double bsum = 0.0;   // thread c < H: gb1[c]; H <= c < H + MP: gb2[c - H]
+    const bool bias_thr = (J1 && tid < H) || (J02 && tid >= H && tid < H + MP);
+
+    if (r0 < r1) gload(r0);
+    for (int64_t t0 = r0; t0 < r1; t0 += BT) {
+        __syncthreads();
+        sstore(t0);
+        __syncthreads();
+        gload(t0 + BT);   // unconditional (rows clamped): a branch here made the compiler copy prefetch registers at the join, waiting on HBM
+#pragma unroll   // fully: a rolled loop's induction registers took prefetch registers (copies waiting on HBM)
+        for (int kk = 0; kk < BT / 4; ++kk) {
+            const int row = 4 * kk + q;
+            if constexpr (J1) {
+                float av[HB];
+#pragma unroll
+                for (int kb = 0; kb < HB; ++kb) av[kb] = sm[C::oA0 + row * C::LDH + 16 * kb + r16];
+#pragma unroll
+                for (int t = 0; t < S1; ++t) {
+                    const float g1 = sm[C::oG1 + row * C::LDH + 16 * (w + NW * t) + r16];
+#pragma unroll
+                    for (int kb = 0; kb < HB; ++kb) acc1[t][kb] = mfma4(g1, av[kb], acc1[t][kb]);
+                }
+            }
+            if constexpr (J02) {
+                float xv[NPBM];
+#pragma unroll
+                for (int kb = 0; kb < NPBM; ++kb) xv[kb] = kb < npb ? sm[C::oX + row * C::LDX + 16 * kb + r16] : 0.f;
+#pragma unroll
+                for (int t = 0; t < S0; ++t) {
+                    const float g0 = sm[C::oG0 + row * C::LDH + 16 * (w + NW * t) + r16];
+#pragma unroll
+                    for (int kb = 0; kb < NPBM; ++kb)
+                        if (kb < npb) acc0[t][kb] = mfma4(g0, xv[kb], acc0[t][kb]);
+                }
+#pragma unroll
+                for (int b = 0; b < B2; ++b) {
+                    const int blk = w * BW2 + b, sb = blk / HB, kb = blk % HB;
+                    const float gpv = sm[C::oGP + row * C::LDP + 16 * sb + r16];
+                    const float a1v = sm[C::oA1 + row * C::LDH + 16 * kb + r16];
+                    acc2[b] = mfma4(gpv, a1v, acc2[b]);
+                }
+            }
+        }
+        if (bias_thr) {   // bias sums: rows in order, fp64
+            const float* col = tid < H ? sm + C::oG1 + tid : sm + C::oGP + (tid - H);
+            const int ld = tid < H ? C::LDH : C::LDP;
+            double cs = 0.0;
+            for (int row = 0; row < BT; ++row) cs += (double)col[row * ld];
+            bsum += cs;
+        }
+    }
+    // this slice's slabs (make_jobs layout)
+    if constexpr (J1) {
+        float* o1 = a.wpart + a.off1 + (int64_t)s * H * H;
+#pragma unroll
+        for (int t = 0; t < S1; ++t) {
+            const int n0 = 16 * (w + NW * t) + 4 * q;
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+                for (int kb = 0; kb < HB; ++kb) o1[(int64_t)(n0 + rr) * H + 16 * kb + r16] = acc1[t][kb][rr];
+        }
+        if (tid < H) a.wpart[a.boff1 + (int64_t)s * H + tid] = (float)bsum;
+    }
+    if constexpr (J02) {
+        float* o0 = a.wpart + a.off0 + (int64_t)s * H * np;
+        float* o2 = a.wpart + a.off2 + (int64_t)s * MP * H;
+#pragma unroll
+        for (int t = 0; t < S0; ++t) {
+            const int n0 = 16 * (w + NW * t) + 4 * q;
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+                for (int kb = 0; kb < NPBM; ++kb)
+                    if (kb < npb) o0[(int64_t)(n0 + rr) * np + 16 * kb + r16] = acc0[t][kb][rr];
+        }
+#pragma unroll
+        for (int b = 0; b < B2; ++b) {
+            const int blk = w * BW2 + b, sb = blk / HB, kb = blk % HB;
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) o2[(int64_t)(16 * sb + 4 * q + rr) * H + 16 * kb + r16] = acc2[b][rr];
+        }
+        if (tid >= H && tid < H + MP) a.wpart[a.boff2 + (int64_t)s * MP + (tid - H)] = (float)bsum;
+    }
+}
+
+template <int H, int MP, int NPBM>
+__global__ void __launch_bounds__((WallCfg<H, MP, NPBM>::NT)) k_wgrad_all(WallArgs a) {
+    if (a.done && *a.done) return;
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    wall_body<H, MP, NPBM, 0>(a, blockIdx.x, sm);
+}
+
+// ---------------------------------------------------------------------------
 // Gather: gsum[f] = sum over slices (fixed order) of the slab element feeding
 // flat parameter f (reference order, gaussian_mlp.py:61-64).
 // ---------------------------------------------------------------------------
@@ -955,9 +1194,38 @@ inline int acc_path(const mjrl_shape* s, int64_t T) {
 }
 
 // slices of the weight-gradient slabs the accumulate step produces for (shape, T)
+// k_wgrad_all (the MLP weight gradients of a slice in one workgroup): shapes, tile
+// rows, slices (at most one per CU, equal tile counts)
+inline int wall_npbm(const mjrl_shape* s) {
+    const int npb = s->np / 16;
+    return npb <= 2 ? 2 : (npb <= 4 ? 4 : (npb <= 8 ? 8 : 0));
+}
+bool wall_off() {   // MJRL_AMD_WGRAD_OLD (read once): the per-block k_wgrad instead, for A/B runs
+    static const bool v = getenv("MJRL_AMD_WGRAD_OLD") && getenv("MJRL_AMD_WGRAD_OLD")[0] == '1';
+    return v;
+}
+bool wall_supported(const mjrl_shape* s) {
+    if (wall_off() || s->h0 == 0 || s->h0 != s->h1 || s->np % 16 || !wall_npbm(s)) return false;
+    if (s->mp != 16 && s->mp != 32 && s->mp != 64) return false;
+    // 256-wide layers keep k_wgrad: one workgroup's accumulators for all three products
+    // do not fit its registers, and gW1 alone against gW0 + gW2 on two workgroups per
+    // slice measured no faster (door DAPG 94 us either way, profiles/r03i/wgrad_all.txt)
+    return s->h0 == 128 || ((s->h0 == 32 || s->h0 == 64) && s->mp == 64);
+}
+inline int wall_cap(const mjrl_shape*) { return 256; }   // one slice per CU at most
+inline int wall_slices(const mjrl_shape* s, int64_t T) {
+    const int bt = 32;
+    int64_t tiles = (T + bt - 1) / bt;
+    if (tiles < 1) tiles = 1;
+    const int cap = wall_cap(s);
+    const int64_t tps = (tiles + cap - 1) / cap;
+    return (int)((tiles + tps - 1) / tps);
+}
+inline int rows_slices(const mjrl_shape* s, int64_t T) { return wall_supported(s) ? wall_slices(s, T) : wgrad_slices(T); }
+
 inline int grad_slices(const mjrl_shape* s, int64_t T) {
     const int p = acc_path(s, T);
-    return p == 2 ? ks_grid(T) : (p == 1 ? fused_grid(T) : wgrad_slices(T));
+    return p == 2 ? ks_grid(T) : (p == 1 ? fused_grid(T) : rows_slices(s, T));
 }
 
 // the split-f16 first layer additionally needs NP % 128 == 0 (chunk swizzle)
@@ -1128,8 +1396,52 @@ int run_gather(const mjrl_shape* s, const mjrl_rows* r, int64_t T, const mjrl_sc
     return (int)hipGetLastError();
 }
 
+template <int H, int MP, int NPBM>
+int launch_wall_t(const WallArgs& wa, int S, hipStream_t st) {
+    using C = WallCfg<H, MP, NPBM>;
+    auto fn = k_wgrad_all<H, MP, NPBM>;
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, C::bytes);
+        if (e != hipSuccess) return (int)e;
+        attr = true;
+    }
+    hipLaunchKernelGGL(fn, dim3(S), dim3(C::NT), C::bytes, st, wa);
+    return (int)hipGetLastError();
+}
+
+int run_wgrad_all(const mjrl_shape* s, const mjrl_rows* r, int64_t T, const mjrl_scratch* sc, const int32_t* done,
+                  hipStream_t st) {
+    const int S = wall_slices(s, T);
+    if (S > sc->slices) return MJRL_EINVAL;   // scratch not sized by mjrl_scratch_size for >= T rows
+    JobSet js = make_jobs(s, r, S);
+    WallArgs wa{};
+    wa.gu0 = r->gu0; wa.gu1 = r->gu1; wa.gp = r->gp; wa.x = r->xhat; wa.a0 = r->a0; wa.a1 = r->a1;
+    wa.np = s->np;
+    wa.S = S;
+    wa.T = T;
+    const int bt = 32;
+    const int64_t tiles = (T + bt - 1) / bt;
+    wa.rows_per_slice = ((tiles + S - 1) / S) * bt;
+    wa.wpart = sc->wpart;
+    wa.off0 = js.job[0].off;
+    wa.off1 = js.job[1].off; wa.boff1 = js.job[1].boff;
+    wa.off2 = js.job[2].off; wa.boff2 = js.job[2].boff;
+    wa.done = done;
+    const int nb = wall_npbm(s);
+#define MJRL_W(H_, MP_, NB_) \
+    if (s->h0 == H_ && s->mp == MP_ && nb == NB_) return launch_wall_t<H_, MP_, NB_>(wa, S, st);
+#define MJRL_WN(H_, MP_) MJRL_W(H_, MP_, 2) MJRL_W(H_, MP_, 4) MJRL_W(H_, MP_, 8)
+    MJRL_WN(128, 16) MJRL_WN(128, 32) MJRL_WN(128, 64)
+    MJRL_WN(32, 64) MJRL_WN(64, 64)
+#undef MJRL_WN
+#undef MJRL_W
+    return MJRL_ESHAPE;
+}
+
 int run_wgrad_only(const mjrl_shape* s, const mjrl_rows* r, int64_t T, const mjrl_scratch* sc, const int32_t* done,
                    hipStream_t st) {
+    if (T > 0 && wall_supported(s)) return run_wgrad_all(s, r, T, sc, done, st);
     const int S = wgrad_slices(T);
     JobSet js = make_jobs(s, r, S);
     WArgs wa{};
@@ -1197,6 +1509,9 @@ int mjrl_scratch_size(const mjrl_shape* s, int64_t T, int64_t* wpart_floats, int
                       int32_t* slices) {
     if (!s || T < 0 || !wpart_floats || !rpart_doubles || !slices) return MJRL_EINVAL;
     int S = wgrad_slices(T) > fused_grid(T) ? wgrad_slices(T) : fused_grid(T);
+    // k_wgrad_all's slice count is not monotonic in T (equal tile counts per slice):
+    // size for its cap, so a scratch sized for T holds every pass over T' <= T rows
+    if (T > 0 && wall_supported(s) && wall_cap(s) > S) S = wall_cap(s);
     if (ks_grid(T) > S) S = ks_grid(T);
     *slices = S;
     *wpart_floats = make_jobs(s, nullptr, S).floats;

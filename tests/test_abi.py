@@ -54,6 +54,26 @@ def test_shape_padding(lib, n, m, h, np_, mp, d):
     assert 1 <= sl.value <= 256 and wf.value > 0 and rd.value > 0
 
 
+@pytest.mark.parametrize("n,m,h", [(6, 2, (0, 0)), (8, 2, (64, 64)), (17, 6, (128, 128)), (376, 17, (64, 64)),
+                                   (39, 28, (256, 256)), (15, 40, (32, 32)), (45, 24, (128, 128))])
+def test_scratch_size_is_monotonic(lib, n, m, h):
+    """A scratch sized by mjrl_scratch_size for T rows must hold every pass over
+    T' <= T rows (the engine sizes it once for the batch, then runs FVPs over the
+    RL rows only, subsampled rows, ...): sizes and slice counts never shrink as T
+    grows, over the tile-count boundaries of every kernel's grid."""
+    from mjrl_amd import _lib
+    s = _lib.make_shape(n, m, h[0], h[1])
+    prev_w, prev_s = 0, 0
+    Ts = sorted(set([1, 15, 16, 17, 31, 32, 33, 63, 64, 65] + [k * 16 + d for k in range(1, 1200, 7) for d in (-1, 0, 1)]
+                    + [b * t + d for b in (16, 32, 64) for t in (128, 256) for d in (-1, 0, 1, b, b + 1)]
+                    + [8192 * 32 + d for d in (-33, -1, 0, 1, 33)] + [1000000, 1000001]))
+    for T in Ts:
+        wf, rd, sl = C.c_int64(), C.c_int64(), C.c_int32()
+        assert lib.mjrl_scratch_size(C.byref(s), T, C.byref(wf), C.byref(rd), C.byref(sl)) == 0
+        assert wf.value >= prev_w and sl.value >= prev_s, T
+        prev_w, prev_s = wf.value, sl.value
+
+
 def test_unsupported_shape_is_rejected(lib):
     from mjrl_amd import _lib
     s = _lib.Shape()

@@ -697,10 +697,9 @@ struct WallCfg {
 
 struct WallArgs {
     const float *gu0, *gu1, *gp, *x, *a0, *a1;
-    int np, S;
+    int n, m, np, S;
     int64_t T, rows_per_slice;
-    float* wpart;
-    int64_t off0, off1, boff1, off2, boff2;   // make_jobs slab offsets (slice 0)
+    float* wpart;   // flat slab layout (k_gather_flat)
     const int32_t* done;
 };
 
@@ -857,38 +856,60 @@ __device__ __forceinline__ void wall_body(const WallArgs& a, int s, float* sm) {
             bsum += cs;
         }
     }
-    // this slice's slabs (make_jobs layout)
+    // this slice's slab in the flat, parameter-chunk-major layout of k_kx:
+    // wpart[f / 64][S][64] for flat parameter f (reference order W0, b0, W1, b1, W2, b2,
+    // gaussian_mlp.py:61-64), so k_gather_flat folds each 64-parameter chunk from one
+    // contiguous run; padded columns / rows are not stored
+    const int n = a.n, m = a.m;
+    const int fb0 = H * n, fW1 = fb0 + H, fb1 = fW1 + H * H, fW2 = fb1 + H, fb2 = fW2 + m * H;
+    float* wp = a.wpart + (int64_t)s * 64;
+    const int64_t cs = (int64_t)a.S * 64;
+    auto put = [&](int f, float v) { wp[(int64_t)(f >> 6) * cs + (f & 63)] = v; };
     if constexpr (J1) {
-        float* o1 = a.wpart + a.off1 + (int64_t)s * H * H;
 #pragma unroll
         for (int t = 0; t < S1; ++t) {
             const int n0 = 16 * (w + NW * t) + 4 * q;
 #pragma unroll
-            for (int rr = 0; rr < 4; ++rr)
+            for (int rr = 0; rr < 4; ++rr) {
+                const int j = n0 + rr;
+                if constexpr (H % 64 == 0) {
+                    // fW1 = H (n + 1) is a multiple of 64: row j of gW1 is H / 64 whole chunks,
+                    // so column k lands in chunk fW1 / 64 + j H / 64 + k / 64 at k % 64 (one
+                    // address per row, immediate offsets for the 16-column steps)
+                    float* rowp = wp + (int64_t)((fW1 >> 6) + j * (H / 64)) * cs + r16;
 #pragma unroll
-                for (int kb = 0; kb < HB; ++kb) o1[(int64_t)(n0 + rr) * H + 16 * kb + r16] = acc1[t][kb][rr];
+                    for (int kb = 0; kb < HB; ++kb) rowp[(kb >> 2) * cs + 16 * (kb & 3)] = acc1[t][kb][rr];
+                } else {
+#pragma unroll
+                    for (int kb = 0; kb < HB; ++kb) put(fW1 + j * H + 16 * kb + r16, acc1[t][kb][rr]);
+                }
+            }
         }
-        if (tid < H) a.wpart[a.boff1 + (int64_t)s * H + tid] = (float)bsum;
+        if (tid < H) put(fb1 + tid, (float)bsum);
     }
     if constexpr (J02) {
-        float* o0 = a.wpart + a.off0 + (int64_t)s * H * np;
-        float* o2 = a.wpart + a.off2 + (int64_t)s * MP * H;
 #pragma unroll
         for (int t = 0; t < S0; ++t) {
             const int n0 = 16 * (w + NW * t) + 4 * q;
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr)
 #pragma unroll
-                for (int kb = 0; kb < NPBM; ++kb)
-                    if (kb < npb) o0[(int64_t)(n0 + rr) * np + 16 * kb + r16] = acc0[t][kb][rr];
+                for (int kb = 0; kb < NPBM; ++kb) {
+                    const int k = 16 * kb + r16, h = n0 + rr;
+                    if (k < n) put(h * n + k, acc0[t][kb][rr]);
+                    else if (k == n) put(fb0 + h, acc0[t][kb][rr]);   // the bias column: b0
+                }
         }
 #pragma unroll
         for (int b = 0; b < B2; ++b) {
             const int blk = w * BW2 + b, sb = blk / HB, kb = blk % HB;
 #pragma unroll
-            for (int rr = 0; rr < 4; ++rr) o2[(int64_t)(16 * sb + 4 * q + rr) * H + 16 * kb + r16] = acc2[b][rr];
+            for (int rr = 0; rr < 4; ++rr) {
+                const int j = 16 * sb + 4 * q + rr;
+                if (j < m) put(fW2 + j * H + 16 * kb + r16, acc2[b][rr]);
+            }
         }
-        if (tid >= H && tid < H + MP) a.wpart[a.boff2 + (int64_t)s * MP + (tid - H)] = (float)bsum;
+        if (tid >= H && tid < H + m) put(fb2 + (tid - H), (float)bsum);
     }
 }
 
@@ -1369,10 +1390,11 @@ int run_fused(int mode, const mjrl_shape* s, const mjrl_rows* r, int64_t T, cons
 int run_gather(const mjrl_shape* s, const mjrl_rows* r, int64_t T, const mjrl_scratch* sc, const double* lspart,
                const int32_t* done, float* gsum, hipStream_t st, CgZ cz = CgZ{}) {
     const int S = grad_slices(s, T);
-    if (acc_path(s, T) == 2 && r->xs) {   // k_kx: flat slab layout
+    const int p = acc_path(s, T);
+    if ((p == 2 && r->xs) || (p == 0 && wall_supported(s))) {   // k_kx / k_wgrad_all: flat slab layout
         const int d_mu = s->d - s->m;
         hipLaunchKernelGGL(k_gather_flat, dim3((s->d + 63) / 64), dim3(64 * GATHER_WAVES), 0, st, sc->wpart, S, d_mu,
-                           s->d, lspart, ks_grid(T), s->mp, gsum, done, cz);
+                           s->d, lspart, p == 2 ? ks_grid(T) : row_grid(s, T), s->mp, gsum, done, cz);
         return (int)hipGetLastError();
     }
     JobSet js = make_jobs(s, r, S);
@@ -1396,6 +1418,14 @@ int run_gather(const mjrl_shape* s, const mjrl_rows* r, int64_t T, const mjrl_sc
     return (int)hipGetLastError();
 }
 
+// floats of S weight-gradient slabs: the per-job layout of make_jobs or the flat,
+// parameter-chunk-major layout of k_kx / k_wgrad_all, whichever is larger
+int64_t slab_floats(const mjrl_shape* s, int S) {
+    const int64_t jobs = make_jobs(s, nullptr, S).floats;
+    const int64_t flat = (int64_t)S * 64 * ((s->d + 63) / 64);
+    return jobs > flat ? jobs : flat;
+}
+
 template <int H, int MP, int NPBM>
 int launch_wall_t(const WallArgs& wa, int S, hipStream_t st) {
     using C = WallCfg<H, MP, NPBM>;
@@ -1414,9 +1444,10 @@ int run_wgrad_all(const mjrl_shape* s, const mjrl_rows* r, int64_t T, const mjrl
                   hipStream_t st) {
     const int S = wall_slices(s, T);
     if (S > sc->slices) return MJRL_EINVAL;   // scratch not sized by mjrl_scratch_size for >= T rows
-    JobSet js = make_jobs(s, r, S);
     WallArgs wa{};
     wa.gu0 = r->gu0; wa.gu1 = r->gu1; wa.gp = r->gp; wa.x = r->xhat; wa.a0 = r->a0; wa.a1 = r->a1;
+    wa.n = s->n;
+    wa.m = s->m;
     wa.np = s->np;
     wa.S = S;
     wa.T = T;
@@ -1424,9 +1455,6 @@ int run_wgrad_all(const mjrl_shape* s, const mjrl_rows* r, int64_t T, const mjrl
     const int64_t tiles = (T + bt - 1) / bt;
     wa.rows_per_slice = ((tiles + S - 1) / S) * bt;
     wa.wpart = sc->wpart;
-    wa.off0 = js.job[0].off;
-    wa.off1 = js.job[1].off; wa.boff1 = js.job[1].boff;
-    wa.off2 = js.job[2].off; wa.boff2 = js.job[2].boff;
     wa.done = done;
     const int nb = wall_npbm(s);
 #define MJRL_W(H_, MP_, NB_) \
@@ -1514,7 +1542,7 @@ int mjrl_scratch_size(const mjrl_shape* s, int64_t T, int64_t* wpart_floats, int
     if (T > 0 && wall_supported(s) && wall_cap(s) > S) S = wall_cap(s);
     if (ks_grid(T) > S) S = ks_grid(T);
     *slices = S;
-    *wpart_floats = make_jobs(s, nullptr, S).floats;
+    *wpart_floats = slab_floats(s, S);
     const int64_t rp = (int64_t)ROW_GRID_CAP * (s->mp > 2 ? s->mp : 2);
     *rpart_doubles = rp + 4 * 256 + 16;
     return MJRL_OK;
@@ -1533,7 +1561,7 @@ int mjrl_vpg_accumulate(const mjrl_shape* s, const mjrl_rows* rows, const float*
     ra.out_scale = out_scale;
     ra.rpart = sc->rpart;
     if (T == 0) {
-        hipMemsetAsync(sc->wpart, 0, make_jobs(s, rows, grad_slices(s, 0)).floats * sizeof(float), st);
+        hipMemsetAsync(sc->wpart, 0, slab_floats(s, grad_slices(s, 0)) * sizeof(float), st);
         hipMemsetAsync(sc->rpart, 0, sizeof(double) * row_grid(s, 0) * s->mp, st);
         return (int)hipGetLastError();
     }
@@ -1555,7 +1583,7 @@ int mjrl_fvp_accumulate(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_fv
     ra.out_scale = out_scale;
     ra.done = done;
     if (T_fvp == 0) {
-        hipMemsetAsync(sc->wpart, 0, make_jobs(s, rows, grad_slices(s, 0)).floats * sizeof(float), st);
+        hipMemsetAsync(sc->wpart, 0, slab_floats(s, grad_slices(s, 0)) * sizeof(float), st);
         return (int)hipGetLastError();
     }
     if (acc_path(s, T_fvp)) return run_fused(FVP, s, rows, T_fvp, ra, sc, st);

@@ -670,7 +670,7 @@ __global__ void __launch_bounds__(NTHREADS, 2) k_wgrad(WArgs a) {
 // tile under this tile's MFMAs) and every output block of all three products is
 // an accumulator in some wave: wave w owns the 16-row strips w + NW t of gW1 and
 // gW0 (a strip's gu fragment feeds all its column blocks) and BW2 blocks of gW2.
-// Slab layout, slices and gather exactly as k_wgrad's (make_jobs), fixed order.
+// Slabs in the flat chunk-major layout of k_kx (k_gather_flat), fixed order.
 // ---------------------------------------------------------------------------
 __host__ __device__ constexpr int wall_ld(int w) {   // LDS row stride: w <= ld, ld % 64 in {16, 48}
     return (w % 64 == 0) ? w + 16 : (w % 64 <= 16 ? w - w % 64 + 16 : (w % 64 <= 48 ? w - w % 64 + 48 : w - w % 64 + 80));
@@ -741,7 +741,10 @@ __device__ __forceinline__ void wall_body(const WallArgs& a, int s, float* sm) {
         xrow[u] = ic / (np / 4);
         xc4[u] = ic % (np / 4);
     }
-    float4 sG0[PH], sG1[PH], sA0[PH], sA1[PH], sp[PP], sx[PX];
+    struct Stage {
+        float4 g0[PH], g1[PH], a0[PH], a1[PH], p[PP], x[PX];
+    };
+    Stage stA, stB;   // two tiles of prefetch in flight
     auto hload = [&](float4 (&dst)[PH], const float* src, int64_t t0) __attribute__((always_inline)) {
         const int64_t tl = r1 - 1;
 #pragma unroll
@@ -758,39 +761,39 @@ __device__ __forceinline__ void wall_body(const WallArgs& a, int s, float* sm) {
             *reinterpret_cast<float4*>(sm + off + row * C::LDH + 4 * c4) = sel4(t0 + row < r1, v[u]);
         }
     };
-    auto gload = [&](int64_t t0) {
+    auto gload = [&](Stage& st, int64_t t0) __attribute__((always_inline)) {
         const int64_t tl = r1 - 1;
-        if constexpr (J02) hload(sG0, a.gu0, t0);
-        if constexpr (J1) hload(sG1, a.gu1, t0);
-        if constexpr (J1) hload(sA0, a.a0, t0);
-        if constexpr (J02) hload(sA1, a.a1, t0);
+        if constexpr (J02) hload(st.g0, a.gu0, t0);
+        if constexpr (J1) hload(st.g1, a.gu1, t0);
+        if constexpr (J1) hload(st.a0, a.a0, t0);
+        if constexpr (J02) hload(st.a1, a.a1, t0);
         if constexpr (J02) {
 #pragma unroll
             for (int u = 0; u < PP; ++u) {
                 const int64_t tp = t0 + prow[u] < tl ? t0 + prow[u] : tl;
-                sp[u] = *reinterpret_cast<const float4*>(a.gp + tp * MP + 4 * pc4[u]);
+                st.p[u] = *reinterpret_cast<const float4*>(a.gp + tp * MP + 4 * pc4[u]);
             }
 #pragma unroll
             for (int u = 0; u < PX; ++u) {
                 const int64_t tx = t0 + xrow[u] < tl ? t0 + xrow[u] : tl;
-                sx[u] = *reinterpret_cast<const float4*>(a.x + tx * np + 4 * xc4[u]);
+                st.x[u] = *reinterpret_cast<const float4*>(a.x + tx * np + 4 * xc4[u]);
             }
         }
     };
-    auto sstore = [&](int64_t t0) {
-        if constexpr (J02) hstore(sG0, C::oG0, t0);
-        if constexpr (J1) hstore(sG1, C::oG1, t0);
-        if constexpr (J1) hstore(sA0, C::oA0, t0);
-        if constexpr (J02) hstore(sA1, C::oA1, t0);
+    auto sstore = [&](const Stage& st, int64_t t0) __attribute__((always_inline)) {
+        if constexpr (J02) hstore(st.g0, C::oG0, t0);
+        if constexpr (J1) hstore(st.g1, C::oG1, t0);
+        if constexpr (J1) hstore(st.a0, C::oA0, t0);
+        if constexpr (J02) hstore(st.a1, C::oA1, t0);
         if constexpr (J02) {
 #pragma unroll
             for (int u = 0; u < PP; ++u)
                 if (tid + u * C::NT < QP)
-                    *reinterpret_cast<float4*>(sm + C::oGP + prow[u] * C::LDP + 4 * pc4[u]) = sel4(t0 + prow[u] < r1, sp[u]);
+                    *reinterpret_cast<float4*>(sm + C::oGP + prow[u] * C::LDP + 4 * pc4[u]) = sel4(t0 + prow[u] < r1, st.p[u]);
 #pragma unroll
             for (int u = 0; u < PX; ++u)
                 if (tid + u * C::NT < qx)
-                    *reinterpret_cast<float4*>(sm + C::oX + xrow[u] * C::LDX + 4 * xc4[u]) = sel4(t0 + xrow[u] < r1, sx[u]);
+                    *reinterpret_cast<float4*>(sm + C::oX + xrow[u] * C::LDX + 4 * xc4[u]) = sel4(t0 + xrow[u] < r1, st.x[u]);
         }
     };
 
@@ -808,12 +811,7 @@ __device__ __forceinline__ void wall_body(const WallArgs& a, int s, float* sm) {
     double bsum = 0.0;   // thread c < H: gb1[c]; H <= c < H + MP: gb2[c - H]
     const bool bias_thr = (J1 && tid < H) || (J02 && tid >= H && tid < H + MP);
 
-    if (r0 < r1) gload(r0);
-    for (int64_t t0 = r0; t0 < r1; t0 += BT) {
-        __syncthreads();
-        sstore(t0);
-        __syncthreads();
-        gload(t0 + BT);   // unconditional (rows clamped): a branch here made the compiler copy prefetch registers at the join, waiting on HBM
+    auto tile = [&]() __attribute__((always_inline)) {
 #pragma unroll   // fully: a rolled loop's induction registers took prefetch registers (copies waiting on HBM)
         for (int kk = 0; kk < BT / 4; ++kk) {
             const int row = 4 * kk + q;
@@ -848,12 +846,51 @@ __device__ __forceinline__ void wall_body(const WallArgs& a, int s, float* sm) {
                 }
             }
         }
-        if (bias_thr) {   // bias sums: rows in order, fp64
+        if (bias_thr) {   // bias sums: rows in order, fp64 (the LDS reads batched ahead of the adds)
             const float* col = tid < H ? sm + C::oG1 + tid : sm + C::oGP + (tid - H);
             const int ld = tid < H ? C::LDH : C::LDP;
             double cs = 0.0;
-            for (int row = 0; row < BT; ++row) cs += (double)col[row * ld];
+#pragma unroll
+            for (int rb = 0; rb < BT; rb += 8) {   // eight reads in flight at a time
+                float v[8];
+#pragma unroll
+                for (int r = 0; r < 8; ++r) v[r] = col[(rb + r) * ld];
+#pragma unroll
+                for (int r = 0; r < 8; ++r) cs += (double)v[r];
+            }
             bsum += cs;
+        }
+    };
+    // two register stages in flight (stage A holds tile k + 2 while tile k computes)
+    // where the accumulators leave the registers for it (HalfCheetah's shape: 11
+    // blocks per wave), one otherwise; pairs of tiles: a slice with an odd tile count
+    // runs one all-zero tile (rows past the slice are zero in LDS and add nothing)
+    constexpr bool TWO = SPW * (HB + NPBM) + BW2 <= 11;
+    if constexpr (TWO) {
+        if (r0 < r1) {
+            gload(stA, r0);
+            gload(stB, r0 + BT);
+        }
+        for (int64_t t0 = r0; t0 < r1; t0 += 2 * BT) {
+            __syncthreads();
+            sstore(stA, t0);
+            __syncthreads();
+            gload(stA, t0 + 2 * BT);   // unconditional (rows clamped): a branch made the compiler copy prefetch registers at the join, waiting on HBM
+            tile();
+            __syncthreads();
+            sstore(stB, t0 + BT);
+            __syncthreads();
+            gload(stB, t0 + 3 * BT);
+            tile();
+        }
+    } else {
+        if (r0 < r1) gload(stA, r0);
+        for (int64_t t0 = r0; t0 < r1; t0 += BT) {
+            __syncthreads();
+            sstore(stA, t0);
+            __syncthreads();
+            gload(stA, t0 + BT);
+            tile();
         }
     }
     // this slice's slab in the flat, parameter-chunk-major layout of k_kx:
@@ -1231,6 +1268,7 @@ bool wall_supported(const mjrl_shape* s) {
     // 256-wide layers keep k_wgrad: one workgroup's accumulators for all three products
     // do not fit its registers, and gW1 alone against gW0 + gW2 on two workgroups per
     // slice measured no faster (door DAPG 94 us either way, profiles/r03i/wgrad_all.txt)
+    if (s->h0 == 128 && s->mp == 64 && wall_npbm(s) == 8) return false;   // spills (77 VGPRs): k_wgrad
     return s->h0 == 128 || ((s->h0 == 32 || s->h0 == 64) && s->mp == 64);
 }
 inline int wall_cap(const mjrl_shape*) { return 256; }   // one slice per CU at most
@@ -1460,7 +1498,7 @@ int run_wgrad_all(const mjrl_shape* s, const mjrl_rows* r, int64_t T, const mjrl
 #define MJRL_W(H_, MP_, NB_) \
     if (s->h0 == H_ && s->mp == MP_ && nb == NB_) return launch_wall_t<H_, MP_, NB_>(wa, S, st);
 #define MJRL_WN(H_, MP_) MJRL_W(H_, MP_, 2) MJRL_W(H_, MP_, 4) MJRL_W(H_, MP_, 8)
-    MJRL_WN(128, 16) MJRL_WN(128, 32) MJRL_WN(128, 64)
+    MJRL_WN(128, 16) MJRL_WN(128, 32) MJRL_W(128, 64, 2) MJRL_W(128, 64, 4)
     MJRL_WN(32, 64) MJRL_WN(64, 64)
 #undef MJRL_WN
 #undef MJRL_W

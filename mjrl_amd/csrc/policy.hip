@@ -811,39 +811,70 @@ __device__ __forceinline__ void wall_body(const WallArgs& a, int s, float* sm) {
     double bsum = 0.0;   // thread c < H: gb1[c]; H <= c < H + MP: gb2[c - H]
     const bool bias_thr = (J1 && tid < H) || (J02 && tid >= H && tid < H + MP);
 
-    auto tile = [&]() __attribute__((always_inline)) {
-#pragma unroll   // fully: a rolled loop's induction registers took prefetch registers (copies waiting on HBM)
-        for (int kk = 0; kk < BT / 4; ++kk) {
-            const int row = 4 * kk + q;
-            if constexpr (J1) {
-                float av[HB];
+    // One k-step's operands (4 rows): read from LDS one k-step ahead of the MFMAs that
+    // use them (the scheduler otherwise waited on each read right before its MFMA).
+    struct Ops {
+        float av[J1 ? HB : 1], g1[S1 ? S1 : 1], xv[NPBM], g0[S0 ? S0 : 1], gp[B2 ? B2 : 1], a1[B2 ? B2 : 1];
+    };
+    auto rd = [&](Ops& o, int kk) __attribute__((always_inline)) {
+        const int row = 4 * kk + q;
+        if constexpr (J1) {
 #pragma unroll
-                for (int kb = 0; kb < HB; ++kb) av[kb] = sm[C::oA0 + row * C::LDH + 16 * kb + r16];
+            for (int kb = 0; kb < HB; ++kb) o.av[kb] = sm[C::oA0 + row * C::LDH + 16 * kb + r16];
 #pragma unroll
-                for (int t = 0; t < S1; ++t) {
-                    const float g1 = sm[C::oG1 + row * C::LDH + 16 * (w + NW * t) + r16];
+            for (int t = 0; t < S1; ++t) o.g1[t] = sm[C::oG1 + row * C::LDH + 16 * (w + NW * t) + r16];
+        }
+        if constexpr (J02) {
 #pragma unroll
-                    for (int kb = 0; kb < HB; ++kb) acc1[t][kb] = mfma4(g1, av[kb], acc1[t][kb]);
-                }
+            for (int kb = 0; kb < NPBM; ++kb) o.xv[kb] = kb < npb ? sm[C::oX + row * C::LDX + 16 * kb + r16] : 0.f;
+#pragma unroll
+            for (int t = 0; t < S0; ++t) o.g0[t] = sm[C::oG0 + row * C::LDH + 16 * (w + NW * t) + r16];
+#pragma unroll
+            for (int b = 0; b < B2; ++b) {
+                const int blk = w * BW2 + b, sb = blk / HB, kb = blk % HB;
+                o.gp[b] = sm[C::oGP + row * C::LDP + 16 * sb + r16];
+                o.a1[b] = sm[C::oA1 + row * C::LDH + 16 * kb + r16];
             }
-            if constexpr (J02) {
-                float xv[NPBM];
+        }
+    };
+    auto mm = [&](const Ops& o) __attribute__((always_inline)) {
+        if constexpr (J1) {
 #pragma unroll
-                for (int kb = 0; kb < NPBM; ++kb) xv[kb] = kb < npb ? sm[C::oX + row * C::LDX + 16 * kb + r16] : 0.f;
+            for (int t = 0; t < S1; ++t)
 #pragma unroll
-                for (int t = 0; t < S0; ++t) {
-                    const float g0 = sm[C::oG0 + row * C::LDH + 16 * (w + NW * t) + r16];
+                for (int kb = 0; kb < HB; ++kb) acc1[t][kb] = mfma4(o.g1[t], o.av[kb], acc1[t][kb]);
+        }
+        if constexpr (J02) {
 #pragma unroll
-                    for (int kb = 0; kb < NPBM; ++kb)
-                        if (kb < npb) acc0[t][kb] = mfma4(g0, xv[kb], acc0[t][kb]);
-                }
+            for (int t = 0; t < S0; ++t)
 #pragma unroll
-                for (int b = 0; b < B2; ++b) {
-                    const int blk = w * BW2 + b, sb = blk / HB, kb = blk % HB;
-                    const float gpv = sm[C::oGP + row * C::LDP + 16 * sb + r16];
-                    const float a1v = sm[C::oA1 + row * C::LDH + 16 * kb + r16];
-                    acc2[b] = mfma4(gpv, a1v, acc2[b]);
-                }
+                for (int kb = 0; kb < NPBM; ++kb)
+                    if (kb < npb) acc0[t][kb] = mfma4(o.g0[t], o.xv[kb], acc0[t][kb]);
+#pragma unroll
+            for (int b = 0; b < B2; ++b) acc2[b] = mfma4(o.gp[b], o.a1[b], acc2[b]);
+        }
+    };
+    constexpr bool PIPE = SPW * (HB + NPBM) + BW2 <= 11;   // a second operand set fits the registers
+    auto tile = [&]() __attribute__((always_inline)) {
+        Ops o0, o1;
+        if constexpr (PIPE) {
+            rd(o0, 0);
+#pragma unroll   // fully: a rolled loop's induction registers took prefetch registers (copies waiting on HBM)
+            for (int kk = 0; kk < BT / 4; kk += 2) {
+                rd(o1, kk + 1);
+                __builtin_amdgcn_sched_barrier(0);
+                mm(o0);
+                __builtin_amdgcn_sched_barrier(0);
+                if (kk + 2 < BT / 4) rd(o0, kk + 2);
+                __builtin_amdgcn_sched_barrier(0);
+                mm(o1);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        } else {
+#pragma unroll
+            for (int kk = 0; kk < BT / 4; ++kk) {
+                rd(o0, kk);
+                mm(o0);
             }
         }
         if (bias_thr) {   // bias sums: rows in order, fp64 (the LDS reads batched ahead of the adds)
@@ -865,7 +896,7 @@ __device__ __forceinline__ void wall_body(const WallArgs& a, int s, float* sm) {
     // where the accumulators leave the registers for it (HalfCheetah's shape: 11
     // blocks per wave), one otherwise; pairs of tiles: a slice with an odd tile count
     // runs one all-zero tile (rows past the slice are zero in LDS and add nothing)
-    constexpr bool TWO = SPW * (HB + NPBM) + BW2 <= 11;
+    constexpr bool TWO = false;   // two stages measured no faster (71.6 vs 71.3 us); their registers hold the k-step operands instead
     if constexpr (TWO) {
         if (r0 < r1) {
             gload(stA, r0);

@@ -744,7 +744,7 @@ __device__ __forceinline__ void wall_body(const WallArgs& a, int s, float* sm) {
     struct Stage {
         float4 g0[PH], g1[PH], a0[PH], a1[PH], p[PP], x[PX];
     };
-    Stage stA, stB;   // two tiles of prefetch in flight
+    Stage stA;
     auto hload = [&](float4 (&dst)[PH], const float* src, int64_t t0) __attribute__((always_inline)) {
         const int64_t tl = r1 - 1;
 #pragma unroll
@@ -892,37 +892,16 @@ __device__ __forceinline__ void wall_body(const WallArgs& a, int s, float* sm) {
             bsum += cs;
         }
     };
-    // two register stages in flight (stage A holds tile k + 2 while tile k computes)
-    // where the accumulators leave the registers for it (HalfCheetah's shape: 11
-    // blocks per wave), one otherwise; pairs of tiles: a slice with an odd tile count
-    // runs one all-zero tile (rows past the slice are zero in LDS and add nothing)
-    constexpr bool TWO = false;   // two stages measured no faster (71.6 vs 71.3 us); their registers hold the k-step operands instead
-    if constexpr (TWO) {
-        if (r0 < r1) {
-            gload(stA, r0);
-            gload(stB, r0 + BT);
-        }
-        for (int64_t t0 = r0; t0 < r1; t0 += 2 * BT) {
-            __syncthreads();
-            sstore(stA, t0);
-            __syncthreads();
-            gload(stA, t0 + 2 * BT);   // unconditional (rows clamped): a branch made the compiler copy prefetch registers at the join, waiting on HBM
-            tile();
-            __syncthreads();
-            sstore(stB, t0 + BT);
-            __syncthreads();
-            gload(stB, t0 + 3 * BT);
-            tile();
-        }
-    } else {
-        if (r0 < r1) gload(stA, r0);
-        for (int64_t t0 = r0; t0 < r1; t0 += BT) {
-            __syncthreads();
-            sstore(stA, t0);
-            __syncthreads();
-            gload(stA, t0 + BT);
-            tile();
-        }
+    // one tile of register prefetch under the current tile's MFMAs (a second stage
+    // measured no faster: 71.6 vs 71.3 us; its registers hold the next k-step's
+    // operands instead)
+    if (r0 < r1) gload(stA, r0);
+    for (int64_t t0 = r0; t0 < r1; t0 += BT) {
+        __syncthreads();
+        sstore(stA, t0);
+        __syncthreads();
+        gload(stA, t0 + BT);   // unconditional (rows clamped): a branch made the compiler copy prefetch registers at the join, waiting on HBM
+        tile();
     }
     // this slice's slab in the flat, parameter-chunk-major layout of k_kx:
     // wpart[f / 64][S][64] for flat parameter f (reference order W0, b0, W1, b1, W2, b2,

@@ -10,8 +10,9 @@
 //   grads     gW2 += gp^T a1, gW1 += gu1^T a0, gb1 / gb2 column sums, and
 //             gW0 += gu0^T xhat with the tile re-streamed (L2-hot) — all
 //             accumulated in REGISTERS across the workgroup's tiles
-// and each workgroup writes one [H0][NP] / [H1][H0] / [MP][H1] (+ bias) slab
-// at the end, in exactly the layout k_wgrad writes, so k_gather folds them.
+// and each workgroup writes its slab at the end in the flat, parameter-chunk-major
+// layout of k_kx, so k_gather_flat folds them (each 64-parameter chunk one
+// contiguous run).
 // Replaces k_rows<FWD|FVP> + k_wgrad: the gu0 / gu1 / gp round trip through HBM
 // and k_wgrad's re-reads disappear.
 #pragma once
@@ -389,8 +390,16 @@ __global__ void __launch_bounds__(FT, 1) k_fused(RowArgs a, FOut o) {
         __syncthreads();
     }
 
-    // ---------------- this workgroup's slabs (k_gather layout, slice = blockIdx.x) ----------------
+    // ---------------- this workgroup's slab (slice = blockIdx.x) in the flat,
+    // parameter-chunk-major layout wpart[f / 64][S][64] (k_gather_flat): flat parameter
+    // f in the reference order W0, b0, W1, b1, W2, b2 (gaussian_mlp.py:61-64); padded
+    // columns / rows are not stored ----------------
     const int64_t blk = blockIdx.x;
+    const int nobs = o.n, mact = o.m;
+    const int fb0 = H0 * nobs, fW1 = fb0 + H0, fb1 = fW1 + H1 * H0, fW2 = fb1 + H1, fb2 = fW2 + mact * H1;
+    float* wp = o.wpart + blk * 64;
+    const int64_t cs = (int64_t)gridDim.x * 64;
+    auto put = [&](int f, float v) { wp[(int64_t)(f >> 6) * cs + (f & 63)] = v; };
 #pragma unroll
     for (int c = 0; c < NCH; ++c)
 #pragma unroll
@@ -401,7 +410,8 @@ __global__ void __launch_bounds__(FT, 1) k_fused(RowArgs a, FOut o) {
                 for (int rr = 0; rr < 4; ++rr) {
                     const int n = (W0S::rb0(w) + i * W0S::RBS) * 16 + 4 * q + rr;
                     const int k = c * KC + (W0S::cb0(w) + j * W0S::CBS) * 16 + r16;
-                    if (n < H0 && k < np) o.wpart[o.off0 + (blk * H0 + n) * np + k] = g0[c][i][j][rr];
+                    if (n < H0 && k < nobs) put(n * nobs + k, g0[c][i][j][rr]);
+                    else if (n < H0 && k == nobs) put(fb0 + n, g0[c][i][j][rr]);   // the bias column: b0
                 }
 #pragma unroll
     for (int i = 0; i < W1S::NRW; ++i)
@@ -411,7 +421,7 @@ __global__ void __launch_bounds__(FT, 1) k_fused(RowArgs a, FOut o) {
             for (int rr = 0; rr < 4; ++rr) {
                 const int n = (W1S::rb0(w) + i * W1S::RBS) * 16 + 4 * q + rr;
                 const int k = (W1S::cb0(w) + j * W1S::CBS) * 16 + r16;
-                if (n < H1 && k < H0) o.wpart[o.off1 + (blk * H1 + n) * H0 + k] = g1[i][j][rr];
+                if (n < H1 && k < H0) put(fW1 + n * H0 + k, g1[i][j][rr]);
             }
 #pragma unroll
     for (int i = 0; i < W2S::NRW; ++i)
@@ -421,12 +431,12 @@ __global__ void __launch_bounds__(FT, 1) k_fused(RowArgs a, FOut o) {
             for (int rr = 0; rr < 4; ++rr) {
                 const int n = (W2S::rb0(w) + i * W2S::RBS) * 16 + 4 * q + rr;
                 const int k = (W2S::cb0(w) + j * W2S::CBS) * 16 + r16;
-                if (n < MP && k < H1) o.wpart[o.off2 + (blk * MP + n) * H1 + k] = g2[i][j][rr];
+                if (n < mact && k < H1) put(fW2 + n * H1 + k, g2[i][j][rr]);
             }
     if (tid < H1)
-        o.wpart[o.boff1 + blk * H1 + tid] = b1acc;
-    else if (tid < H1 + MP)
-        o.wpart[o.boff2 + blk * MP + tid - H1] = b2acc;
+        put(fb1 + tid, b1acc);
+    else if (tid < H1 + mact)
+        put(fb2 + (tid - H1), b2acc);
     if (MODE == FWD) {
         static_assert(L::total >= 2 * FT, "row_pass_final scratch");
         __syncthreads();

@@ -52,8 +52,8 @@ struct FLayout {
 
 struct FOut {
     float* wpart;
-    int64_t off0, off1, boff1, off2, boff2;   // slab offsets (k_gather layout, S = gridDim.x)
-    int n, m;                                 // k_kx: flat layout wpart[f / 64][S][64] (k_gather_flat)
+    int64_t off0, off1, boff1, off2, boff2;   // per-job slab offsets (make_jobs; unused by the flat writers)
+    int n, m;                                 // k_kx / k_ks / k_fused: flat layout wpart[f / 64][S][64] (k_gather_flat)
 };
 
 // acc[i][j] += sum_{t<64} G[t][n-block] * A[t][k-block], both row-major in LDS.

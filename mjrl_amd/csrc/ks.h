@@ -399,13 +399,22 @@ __global__ void __launch_bounds__(KT, 1) k_ks(RowArgs a, FOut o) {
 
     const int64_t blk = blockIdx.x;
     if constexpr (GRAD) {
+        // this workgroup's slab in the flat, parameter-chunk-major layout wpart[f / 64][S][64]
+        // (k_gather_flat): flat parameter f in the reference order W0, b0, W1, b1, W2, b2
+        // (gaussian_mlp.py:61-64); padded columns / rows are not stored
+        const int nobs = o.n, mact = o.m;
+        const int fb0 = H * nobs, fW1 = fb0 + H, fb1 = fW1 + H * H, fW2 = fb1 + H, fb2 = fW2 + mact * H;
+        float* wp = o.wpart + blk * 64;
+        const int64_t cs = (int64_t)gridDim.x * 64;
+        auto put = [&](int f, float v) { wp[(int64_t)(f >> 6) * cs + (f & 63)] = v; };
 #pragma unroll
         for (int g = 0; g < KG; ++g)
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr) {
                 const int n = cb * 16 + 4 * q + rr;
                 const int k = kh * KH + 16 * g + r16;
-                o.wpart[o.off0 + (blk * H + n) * NP + k] = g0[g][rr];
+                if (k < nobs) put(n * nobs + k, g0[g][rr]);
+                else if (k == nobs) put(fb0 + n, g0[g][rr]);   // the bias column: b0
             }
 #pragma unroll
         for (int j = 0; j < 2; ++j)
@@ -413,20 +422,20 @@ __global__ void __launch_bounds__(KT, 1) k_ks(RowArgs a, FOut o) {
             for (int rr = 0; rr < 4; ++rr) {
                 const int n = cb * 16 + 4 * q + rr;
                 const int k = (kh + 2 * j) * 16 + r16;
-                o.wpart[o.off1 + (blk * H + n) * H + k] = g1[j][rr];
+                put(fW1 + n * H + k, g1[j][rr]);
             }
         if ((w >> 2) < MP / 16) {
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr) {
                 const int n = (w >> 2) * 16 + 4 * q + rr;
                 const int k = (w & 3) * 16 + r16;
-                o.wpart[o.off2 + (blk * MP + n) * H + k] = g2[rr];
+                if (n < mact) put(fW2 + n * H + k, g2[rr]);
             }
         }
         if (tid < H)
-            o.wpart[o.boff1 + blk * H + tid] = b1acc;
-        else if (tid < H + MP)
-            o.wpart[o.boff2 + blk * MP + tid - H] = b2acc;
+            put(fb1 + tid, b1acc);
+        else if (tid < H + mact)
+            put(fb2 + (tid - H), b2acc);
     }
     if (MODE != FVP) {
         static_assert(L::total >= 2 * KT, "row_pass_final scratch");

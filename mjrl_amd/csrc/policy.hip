@@ -1439,7 +1439,7 @@ int run_gather(const mjrl_shape* s, const mjrl_rows* r, int64_t T, const mjrl_sc
                const int32_t* done, float* gsum, hipStream_t st, CgZ cz = CgZ{}) {
     const int S = grad_slices(s, T);
     const int p = acc_path(s, T);
-    if ((p == 2 && r->xs) || p == 1 || (p == 0 && wall_supported(s))) {   // k_kx / k_fused / k_wgrad_all: flat slabs
+    if (p == 2 || p == 1 || (p == 0 && wall_supported(s))) {   // k_kx / k_ks / k_fused / k_wgrad_all: flat slabs
         const int d_mu = s->d - s->m;
         const int G = p == 2 ? ks_grid(T) : (p == 1 ? fused_grid(T) : row_grid(s, T));   // log-std partial rows
         hipLaunchKernelGGL(k_gather_flat, dim3((s->d + 63) / 64), dim3(64 * GATHER_WAVES), 0, st, sc->wpart, S, d_mu,

@@ -229,7 +229,18 @@ def stage_shard(p0, p1, device, base, cfg=None, demos=None, dtype=np.float32):
         T_demo = sum(len(o) for o in demos[0])
     tdt = torch.float32 if np.dtype(dtype) == np.float32 else torch.float64
     ho = torch.empty((T + T_demo, n), dtype=tdt, pin_memory=True)
-    np.concatenate(obs, out=ho.numpy(), casting="same_kind")
+    orange = None
+    if tdt == torch.float32:
+        # the staging pass (engine.host_stage, as DeviceBatch.from_paths runs it):
+        # f32 rows plus each column's range, from which the split rows' column
+        # scales follow (DeviceBatch.obs_range)
+        from mjrl_amd.engine import host_stage
+        lo, hi = np.full(n, np.inf, np.float32), np.full(n, -np.inf, np.float32)
+        offs = np.concatenate([[0], np.cumsum([len(o) for o in obs])])
+        host_stage(obs, ho.numpy(), offs, 0, len(obs), lo, hi)
+        orange = torch.from_numpy(np.stack([lo, hi])).to(device)
+    else:
+        np.concatenate(obs, out=ho.numpy(), casting="same_kind")
     ha = torch.empty((T + T_demo, m), dtype=tdt, pin_memory=True)
     np.concatenate(act, out=ha.numpy(), casting="same_kind")
     rw = np.concatenate(rew)
@@ -237,7 +248,8 @@ def stage_shard(p0, p1, device, base, cfg=None, demos=None, dtype=np.float32):
                          for o, r in zip(obs[:P], rew)])
     off = (np.arange(P + 1, dtype=np.int64) * H)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)
-    return DeviceBatch(ho.to(device), ha.to(device), t(rw), t(bl), t(off), t(np.zeros(P, np.uint8)), T_demo=T_demo)
+    return DeviceBatch(ho.to(device), ha.to(device), t(rw), t(bl), t(off), t(np.zeros(P, np.uint8)), T_demo=T_demo,
+                       obs_range=orange)
 
 
 def update_args(cfg, T_total):
@@ -398,6 +410,11 @@ def kernel_names(eng, cfg):
 
 
 def main():
+    # stdout carries the one JSON line and nothing else: libraries that print to
+    # fd 1 (RCCL's version banner at communicator init) are sent to stderr
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -418,6 +435,14 @@ def main():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only to rehearse the N > 1 "
                          "path with several ranks on one GPU)")
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "torch"],
+                    help="N > 1 over nccl: RCCL driven directly on the update's stream (comm.RcclComm: the "
+                         "sharded update is one captured hipGraph, collectives inside) or torch.distributed's "
+                         "own collectives (eager)")
+    ap.add_argument("--sharded-path", action="store_true",
+                    help="one GPU: run the sharded code path on a one-rank RCCL communicator (all-gathered "
+                         "moments, an all-reduce between every FVP and its CG step, RCCL calls inside the "
+                         "captured graph) -- the per-rank schedule of an N-GPU run, on this GPU's shard")
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
                     help="replay each update as one captured hipGraph (one GPU): auto = the engine's "
                          "default, graphs for batches up to engine.GRAPH_AUTO_ROWS rows")
@@ -443,8 +468,11 @@ def main():
             dist.init_process_group("nccl", device_id=device)
         else:
             dist.init_process_group("gloo")
-        from mjrl_amd.comm import DistComm
-        comm = DistComm()
+        from mjrl_amd.comm import DistComm, RcclComm
+        comm = RcclComm(device) if args.backend == "nccl" and args.comm == "rccl" else DistComm()
+    elif args.sharded_path:
+        from mjrl_amd.comm import RcclComm
+        comm = RcclComm.local(device)
     from mjrl_amd.comm import partition_paths
     from mjrl_amd.engine import UpdateEngine
 
@@ -458,7 +486,7 @@ def main():
     th0 = torch.from_numpy(initial_theta(cfg)).to(device)
     th = th0.clone()
     upd = update_args(cfg, T_total)
-    eng.graphs = {"auto": "auto", "on": True, "off": False}[args.graph] if world == 1 else False
+    eng.graphs = {"auto": "auto", "on": True, "off": False}[args.graph]
     # per-FVP (start, accumulate done, gather done) events on eager steps; a captured
     # graph is kept free of them (30 event nodes per update measured +3 % on the
     # replay) and the kernel timings come from eager steps after the timed region
@@ -588,7 +616,9 @@ def main():
                    config=dict(workload=cfg["workload"], obs_dim=n, act_dim=m, hidden=list(hidden),
                                algo=cfg["algo"], timesteps=T_total, paths=cfg["paths"], horizon=H,
                                demo_timesteps=cfg.get("demos", 0) * H, cg_iters=CG_ITERS,
-                               parallelism="dp%d" % world),
+                               parallelism="dp%d" % world,
+                               comm=type(eng.comm).__name__ + (" (one rank, sharded code path)"
+                                                               if args.sharded_path and world == 1 else "")),
                    commit=_commit(),
                    hipgraph=bool(graphed), eager_ms_per_step=None if eager_ms is None else round(eager_ms, 3),
                    f32_ms_per_step=None if f32_ms is None else round(f32_ms, 3),
@@ -601,7 +631,7 @@ def main():
             rows = T_total if (args.cpu_full or args.config != "c4") else min(args.cpu_rows, T_total)
             reps = args.cpu_reps or (3 if args.config == "c4" else 10)
             out["cpu_baseline"] = cpu_baseline(rows, base, reps=reps, cfg=cfg)
-        print(json.dumps(out))
+        print(json.dumps(out), file=json_out, flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
 

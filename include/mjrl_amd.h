@@ -105,6 +105,13 @@ int mjrl_obs_colscale(const double* obs, int64_t T, const mjrl_shape* s, const f
                       const float* in_scale, float* xc, void* stream);
 int mjrl_obs_colscale_f32(const float* obs, int64_t T, const mjrl_shape* s, const float* in_shift,
                           const float* in_scale, float* xc, void* stream);
+/* The same xc from per-column ranges of the f32 observations, cmin[n] / cmax[n]
+ * (device), as the host staging pass takes them (mjrl_host_stage_*): the
+ * normalisation is monotone in x, so the column max of |xhat| sits at one end of
+ * the range and xc equals mjrl_obs_colscale's bit for bit, without a pass over
+ * the batch.  cmin[k] > cmax[k] marks an empty range (scale 1). */
+int mjrl_obs_colscale_range(const float* cmin, const float* cmax, const mjrl_shape* s, const float* in_shift,
+                            const float* in_scale, float* xc, void* stream);
 /* Same batch assembly into the split-f16 form of mjrl_rows.xs / xu, given the
  * column scales xc of mjrl_obs_colscale (one wave per row: the row's max
  * |xhat / xc| picks xu[t], then hi / lo as described at mjrl_rows).  Only for
@@ -206,6 +213,17 @@ int mjrl_moments2(const double* x1, int64_t N1, const double* c1, const double* 
 int mjrl_whiten_moments(const double* adv, int64_t T, const double* m1, const double* m2, double eps,
                         float* adv32, double* w64, double* rpart, double* out, void* stream);
 
+/* Sharded moments in ONE collective (npg_cg.py:91, 97-102 over the union of the
+ * shards): each rank runs pass 1 (center null) and pass 2 centred on its OWN mean
+ * into a record of `rec` doubles — group j's pass-1 out[6] at 16 j, its pass-2
+ * out[6] at 16 j + 8 — the records are all-gathered (gathered[world][rec], rank
+ * order), and this folds them: global pass-1 moments to out[16 j ..], pass-2
+ * moments about the GLOBAL mean to out[16 j + 8 ..], M2 = sum_r [M2_r + 2 (m_r -
+ * mean) D_r + n_r (m_r - mean)^2].  With world = 1 the outputs equal the
+ * unsharded two passes bit for bit.  One workgroup, ngroups <= 64. */
+int mjrl_moments_combine(const double* gathered, int32_t world, int32_t rec, int32_t ngroups, double* out,
+                         void* stream);
+
 /* w = (adv[t] - mean) / (std + eps), mean = m1[0]/m1[2], std = sqrt(m2[1]/m1[2]);
  * adv32[t] = float(w) (eps = 1e-6: npg_cg.py:91 then the .float() of
  * batch_reinforce.py:38) and/or w64[t] = w (eps = 1e-8: the `normalize` option of
@@ -306,6 +324,13 @@ int mjrl_cg_step_xr_p(const mjrl_shape* s, float* x, const float* r, float* r_ou
                       const float* z, float* packed_p, float* cg, int32_t* done, float residual_tol,
                       void* stream);
 
+/* The z step of that iteration from an all-reduced gradient sum (the sharded
+ * path: gather, all-reduce of gsum, then this, then mjrl_cg_step_xr_p): z and the
+ * per-64-parameter p.z partials exactly as mjrl_gather_cg_z writes them, so one
+ * rank reproduces the one-process iteration bit for bit. */
+int mjrl_cg_z(const mjrl_shape* s, const float* gsum, double inv_T, float damping, const float* packed_theta,
+              const float* p, float* z, float* cg, const int32_t* done, void* stream);
+
 /* The whole iteration of mjrl_cg_step in one launch (the sharded path: gsum is
  * the all-reduced sum): every workgroup forms z for all of d on the fly and folds
  * p.z and the new r.r itself, then updates x, r and p of its own chunk; r and p
@@ -349,6 +374,17 @@ int mjrl_npg_step(const mjrl_shape* s, const float* g, const float* x, const flo
 int mjrl_policy_mean(const mjrl_shape* s, const float* obs, int64_t N, const float* packed_theta,
                      const float* in_shift, const float* in_scale, const float* out_shift,
                      const float* out_scale, float* mean, void* stream);
+
+/* ---- host staging of sampler paths (base_sampler.py:76-83,
+ * npg_cg.py:87-89 concatenate) — HOST memory, runs on the calling CPU thread ----
+ * dst[rows][n] = float(src) (round to nearest, as torch .float()), and when cmin /
+ * cmax (n floats each) are given, cmin[k] = min(cmin[k], column k), cmax likewise
+ * (NaN skipped, as the device column max skips it) in the same pass, so the
+ * column scales of the split rows (mjrl_obs_colscale_range) cost no pass over the
+ * batch.  Callers initialise cmin = +inf, cmax = -inf.  Thread-safe for disjoint
+ * dst / cmin / cmax. */
+int mjrl_host_stage_f64(const double* src, int64_t rows, int32_t n, float* dst, float* cmin, float* cmax);
+int mjrl_host_stage_f32(const float* src, int64_t rows, int32_t n, float* dst, float* cmin, float* cmax);
 
 #ifdef __cplusplus
 }

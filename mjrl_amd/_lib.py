@@ -53,6 +53,7 @@ SIGNATURES = {
     "mjrl_pack_batch": [P, P, I64, SP, P, P, P, P, P],
     "mjrl_obs_colscale": [P, I64, SP, P, P, P, P],
     "mjrl_obs_colscale_f32": [P, I64, SP, P, P, P, P],
+    "mjrl_obs_colscale_range": [P, P, SP, P, P, P, P],
     "mjrl_pack_batch_split": [P, P, I64, SP, P, P, P, P, P, P, P],
     "mjrl_pack_batch_f32": [P, P, I64, SP, P, P, P, P, P],
     "mjrl_pack_batch_split_f32": [P, P, I64, SP, P, P, P, P, P, P, P],
@@ -65,6 +66,7 @@ SIGNATURES = {
     "mjrl_moments_f32": [P, I64, P, P, P, P],
     "mjrl_moments2": [P, I64, P, P, I64, P, P, P, P, P],
     "mjrl_whiten_moments": [P, I64, P, P, F64, P, P, P, P, P],
+    "mjrl_moments_combine": [P, I32, I32, I32, P, P],
     "mjrl_whiten": [P, I64, P, P, F64, P, P, P],
     "mjrl_dapg_adv": [P, I64, P, P, I64, F64, P, P],
     "mjrl_pack_params": [SP, P, P, I32, F32, P],
@@ -79,6 +81,7 @@ SIGNATURES = {
     "mjrl_cg_step": [SP, P, F64, F32, P, P, P, P, P, P, P, P, F32, P],
     "mjrl_gather_cg_z": [SP, C.POINTER(Rows), I64, C.POINTER(Scratch), P, P, F64, F32, P, P, P, P, P],
     "mjrl_cg_step_xr_p": [SP, P, P, P, P, P, P, P, P, F32, P],
+    "mjrl_cg_z": [SP, P, F64, F32, P, P, P, P, P, P],
     "mjrl_cg_step1": [SP, P, F64, F32, P, P, P, P, P, P, P, P, P, F32, P],
     "mjrl_cg_init_vec": [I32, P, P, P, P, P, P, P],
     "mjrl_cg_update": [I32, P, P, P, P, P, P, F32, P],
@@ -91,6 +94,8 @@ SIGNATURES = {
     "mjrl_linear_baseline_residual_f32": [P, P, I64, I32, P, I64, P, P, P, P],
     "mjrl_npg_step": [SP, P, P, P, I32, F32, F32, I32, F32, P, P, P, P],
     "mjrl_policy_mean": [SP, P, I64, P, P, P, P, P, P, P],
+    "mjrl_host_stage_f64": [P, I64, I32, P, P, P],
+    "mjrl_host_stage_f32": [P, I64, I32, P, P, P],
 }
 
 _LIB = None

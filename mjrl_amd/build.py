@@ -23,6 +23,9 @@ FLAGS = [
     "-Wall", "-Wno-unused-function", "-Wno-unused-variable",
 ]
 SOURCES = ["batch.hip", "policy.hip", "cg.hip", "baseline.hip", "rollout.hip"]
+# host-only C++ (the staging conversion of csrc/stage.cpp), built with g++
+HOST_SOURCES = ["stage.cpp"]
+HOST_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-mavx2", "-Wall"]
 
 
 def _deps():
@@ -33,10 +36,14 @@ def _deps():
 
 def _compile(src, force, prof=False, tag="", extra=()):
     s = os.path.join(CSRC, src)
-    o = os.path.join(OUTDIR, src.replace(".hip", ("_prof" if prof else "") + tag + ".o"))
+    host = src.endswith(".cpp")
+    o = os.path.join(OUTDIR, src.replace(".hip", "").replace(".cpp", "") + ("_prof" if prof else "") + tag + ".o")
     if not force and os.path.exists(o) and os.path.getmtime(o) >= max(os.path.getmtime(s), _deps()):
         return o
-    cmd = [HIPCC] + FLAGS + list(extra) + (["-DMJRL_KX_PROF"] if prof else []) + ["-c", s, "-o", o]
+    if host:
+        cmd = [os.environ.get("CXX", "g++")] + HOST_FLAGS + ["-c", s, "-o", o]
+    else:
+        cmd = [HIPCC] + FLAGS + list(extra) + (["-DMJRL_KX_PROF"] if prof else []) + ["-c", s, "-o", o]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError("hipcc failed for %s:\n%s\n%s" % (src, " ".join(cmd), r.stderr[-8000:]))
@@ -51,7 +58,7 @@ def build(force=False, jobs=None, prof=False, tag="", extra=()):
     jobs = jobs or min(len(SOURCES), os.cpu_count() or 1, 16)
     lib = LIB.replace(".so", ("_prof" if prof else "") + tag + ".so")
     with cf.ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, force, prof, tag, extra), SOURCES))
+        objs = list(ex.map(lambda s: _compile(s, force, prof, tag, extra), SOURCES + HOST_SOURCES))
     if force or not os.path.exists(lib) or os.path.getmtime(lib) < max(os.path.getmtime(o) for o in objs):
         cmd = [HIPCC, "-shared", "--offload-arch=" + ARCH, "-fPIC"] + objs + ["-o", lib]
         r = subprocess.run(cmd, capture_output=True, text=True)

@@ -981,6 +981,71 @@ __global__ void k_colscale(float* xc, int np) {
     for (int k = threadIdx.x; k < np; k += blockDim.x) xc[k] = col_scale(xc[k]);
 }
 
+// The same scales from per-column ranges [cmin, cmax] of the f32 observations
+// (taken by the host staging pass, mjrl_host_stage_*): x -> (x - shift) / (scale
+// + 1e-8) is the pack's f32 expression, monotone in x (each rounding is), so the
+// column max of |xhat| over the batch is attained at cmin or cmax: the result is
+// bit for bit k_colmax's.  An empty column range (cmin > cmax: no rows) gives 1.
+__global__ void k_colscale_range(const float* __restrict__ cmin, const float* __restrict__ cmax, int n, int np,
+                                 const float* __restrict__ in_shift, const float* __restrict__ in_scale,
+                                 float* __restrict__ xc) {
+    for (int k = threadIdx.x; k < np; k += blockDim.x) {
+        float m = 0.f;
+        if (k < n) {
+            float lo = cmin[k], hi = cmax[k];
+            if (lo <= hi) {
+                if (in_shift) {
+                    const float den = in_scale[k] + 1e-8f;
+                    lo = (lo - in_shift[k]) / den;   // MuNet.forward:177, as the pack
+                    hi = (hi - in_shift[k]) / den;
+                }
+                m = fmaxf(fabsf(lo), fabsf(hi));
+            }
+        } else if (k == n) {
+            m = 1.f;   // the bias column
+        }
+        xc[k] = col_scale(m);
+    }
+}
+
+// Sharded moments (the all-gather form of npg_cg.py:91, 97-102 over shards):
+// g[world][rec] holds every rank's local pass-1 moments (mjrl_moments format, at
+// 16 j + 0..5 for group j) and its pass-2 moments centred on the rank's OWN mean
+// (16 j + 8..13).  Thread j folds group j over the ranks in rank order: N = sum
+// n_r, S = sum S_r, mean = S / N, and the centred sum of squares about the global
+// mean, M2 = sum_r [M2_r + 2 (m_r - mean) D_r + n_r (m_r - mean)^2] (m_r = S_r /
+// n_r, D_r = sum (x - m_r): exact algebra, only rounding differs from one pass
+// about the global mean; with one rank m_0 == mean and M2 = M2_0 bit for bit).
+// out[16 j + 0..5] / out[16 j + 8..13] receive the global pass-1 / pass-2 moments.
+__global__ void k_moments_combine(const double* __restrict__ g, int world, int rec, int ngroups,
+                                  double* __restrict__ out) {
+    const int j = threadIdx.x;
+    if (j >= ngroups) return;
+    double N = 0.0, S = 0.0, SS = 0.0, mn = __builtin_inf(), mx = -__builtin_inf();
+    for (int r = 0; r < world; ++r) {
+        const double* p = g + (int64_t)r * rec + 16 * j;
+        S += p[0];
+        SS += p[1];
+        N += p[2];
+        mn = fmin(mn, p[3]);
+        mx = fmax(mx, p[4]);
+    }
+    const double mean = S / N;
+    double D = 0.0, M2 = 0.0;
+    for (int r = 0; r < world; ++r) {
+        const double* p = g + (int64_t)r * rec + 16 * j;
+        const double nr = p[2];
+        if (!(nr > 0.0)) continue;
+        const double dm = p[0] / nr - mean;
+        M2 += p[9] + 2.0 * dm * p[8] + nr * dm * dm;
+        D += p[8] + nr * dm;
+    }
+    double* o1 = out + 16 * j;
+    double* o2 = o1 + 8;
+    o1[0] = S; o1[1] = SS; o1[2] = N; o1[3] = mn; o1[4] = mx; o1[5] = -mn;
+    o2[0] = D; o2[1] = M2; o2[2] = N; o2[3] = mn; o2[4] = mx; o2[5] = -mn;
+}
+
 template <typename TO>
 static int obs_colscale(const TO* obs, int64_t T, const mjrl_shape* s, const float* in_shift, const float* in_scale,
                         float* xc, void* stream) {
@@ -1026,6 +1091,24 @@ int mjrl_obs_colscale(const double* obs, int64_t T, const mjrl_shape* s, const f
 int mjrl_obs_colscale_f32(const float* obs, int64_t T, const mjrl_shape* s, const float* in_shift,
                           const float* in_scale, float* xc, void* stream) {
     return obs_colscale(obs, T, s, in_shift, in_scale, xc, stream);
+}
+
+int mjrl_obs_colscale_range(const float* cmin, const float* cmax, const mjrl_shape* s, const float* in_shift,
+                            const float* in_scale, float* xc, void* stream) {
+    if (!s || !cmin || !cmax || !xc) return MJRL_EINVAL;
+    if ((in_shift == nullptr) != (in_scale == nullptr)) return MJRL_EINVAL;
+    if (s->np > 512 || s->n >= s->np) return MJRL_ESHAPE;
+    hipLaunchKernelGGL(k_colscale_range, dim3(1), dim3(512), 0, (hipStream_t)stream, cmin, cmax, s->n, s->np, in_shift,
+                       in_scale, xc);
+    return err(hipGetLastError());
+}
+
+int mjrl_moments_combine(const double* gathered, int32_t world, int32_t rec, int32_t ngroups, double* out,
+                         void* stream) {
+    if (!gathered || !out || world < 1 || ngroups < 1 || ngroups > 64 || rec < 16 * ngroups) return MJRL_EINVAL;
+    hipLaunchKernelGGL(k_moments_combine, dim3(1), dim3(64), 0, (hipStream_t)stream, gathered, world, rec, ngroups,
+                       out);
+    return err(hipGetLastError());
 }
 
 int mjrl_pack_batch_split(const double* obs, const double* act, int64_t T, const mjrl_shape* s,

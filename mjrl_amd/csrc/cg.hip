@@ -361,6 +361,18 @@ __global__ void __launch_bounds__(CGX_T) k_cgm_xrp_f(mjrl_shape s, float* __rest
     }
 }
 
+// The z step of a CG iteration from an all-reduced gradient sum (the sharded path):
+// z = gsum inv_T + c(sigma) p_ls + damping p and one p.z partial per 64 parameters,
+// exactly as the fused gather's epilogue writes them from its own fold
+// (cgz_epilogue), so k_cgm_xrp_f finishes the iteration as in one process (with
+// one rank the two schedules are bit-identical).
+__global__ void __launch_bounds__(64) k_cg_zpart(int d, const float* __restrict__ gsum,
+                                                 const int32_t* __restrict__ done, CgZ cz) {
+    if (*done) return;
+    const int f = blockIdx.x * 64 + threadIdx.x;
+    cgz_epilogue(cz, f, d, f < d ? gsum[f] : 0.f);
+}
+
 // A whole CG iteration after an all-reduced gradient sum (the sharded path) in ONE
 // launch: every workgroup forms z = gsum inv_T + c(sigma) p_ls + damping p on the
 // fly for all of d, folds p.z and then the new r.r in the same fixed order as
@@ -657,6 +669,17 @@ int mjrl_cg_step_xr_p(const mjrl_shape* s, float* x, const float* r, float* r_ou
     if (ng > CG_PZ_MAX) return MJRL_EINVAL;
     hipLaunchKernelGGL(k_cgm_xrp_f, dim3((s->d + CGX_T - 1) / CGX_T), dim3(CGX_T), 0, (hipStream_t)stream, *s, p, z,
                        x, r, r_out, packed_p, cg, done, residual_tol, ng);
+    return err(hipGetLastError());
+}
+
+int mjrl_cg_z(const mjrl_shape* s, const float* gsum, double inv_T, float damping, const float* packed_theta,
+              const float* p, float* z, float* cg, const int32_t* done, void* stream) {
+    if (!s || !gsum || !packed_theta || !p || !z || !cg || !done) return MJRL_EINVAL;
+    const int ng = (s->d + 63) / 64;
+    if (ng > CG_PZ_MAX) return MJRL_EINVAL;
+    const Packed pk(s->h0, s->h1, s->np, s->mp);
+    CgZ cz{p, z, cg, packed_theta + pk.ls, inv_T, damping, s->d - s->m};
+    hipLaunchKernelGGL(k_cg_zpart, dim3(ng), dim3(64), 0, (hipStream_t)stream, s->d, gsum, done, cz);
     return err(hipGetLastError());
 }
 

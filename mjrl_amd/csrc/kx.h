@@ -237,6 +237,40 @@ __device__ __forceinline__ void wscale_cols(float* inv, const float* red, int ti
     }
 }
 
+// Row-scaled images, one 16-byte chunk per thread: thread t owns image row t >> 3
+// and its columns 8 (t & 7) .. + 7, so a row's maximum is a 3-step shuffle over 8
+// neighbouring lanes (the per-column lane mapping of wload needed a 6-step wave
+// reduction per row, 12 rows per wave in one serial chain: most of the launch
+// preamble), and each thread stores one swizzled 16-byte hi / lo chunk.  Rows >=
+// nrows (and threads past the image) read as zero.  NR = image rows (64 or 32).
+template <int NR>
+__device__ __forceinline__ float8v wload_rows(const float* __restrict__ W, int nrows, int tid) {
+    const int j = tid >> 3;
+    float8v v = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (j < NR && j < nrows) v = load8(W + j * 64 + 8 * (tid & 7));
+    return v;
+}
+// split row j's chunk into the image at the row's power-of-two scale; its inverse
+// to inv[j] (lane 0 of the row's 8)
+template <int NR>
+__device__ __forceinline__ void wrows_store(const float8v& v, char* img, int imgbytes, float* inv, int tid) {
+    float mx = absmax8(v);
+    mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 2, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 4, 64));
+    const int j = tid >> 3;
+    if (j < NR) {
+        float iv;
+        const float sc = pow2_scale(mx, iv);
+        half8 h, l;
+        split8(v, sc, h, l);   // the bits of wstore's v / inv -> (hi, f16(y - hi)): sc = 1 / iv exactly
+        const int off = j * 128 + 16 * ((tid & 7) ^ swz128(j));
+        *reinterpret_cast<half8*>(img + off) = h;
+        *reinterpret_cast<half8*>(img + imgbytes + off) = l;
+        if ((tid & 7) == 0) inv[j] = iv;
+    }
+}
+
 template <bool COLS, int IR>
 __device__ __forceinline__ void wstore(const float (&v)[IR], char* img, int imgbytes, const float* inv, int tid) {
     const int lane = tid & 63, w = tid >> 6;
@@ -304,13 +338,20 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
     // every global load of the preamble is issued before the first wait
     constexpr int KS = KH / 32;   // k32 steps per observation half
     static_assert(KT == 512 && MP <= 32, "preamble layout: 8 waves, output-layer images of 32 rows");
-    float w1v[8], w3v[4], w2v[8], w4v[4];
-    wload(P + pk.W1, H, w1v, tid);
-    wload(P + pk.W2, MP, w3v, tid);
-    if (MODE != EVAL) {
+    // column-scaled images (FVP / FWD: W1c, W2c) with the per-column lane mapping;
+    // row-scaled images (FVP: dW1r / dW2r, FWD: W1r / W2r, EVAL: W1r / W2r) one
+    // 16-byte chunk per thread (wload_rows)
+    float w1v[8], w3v[4];
+    float8v rv1, rv2;
+    if (MODE == EVAL) {
+        rv1 = wload_rows<64>(P + pk.W1, H, tid);
+        rv2 = wload_rows<32>(P + pk.W2, MP, tid);
+    } else {
+        wload(P + pk.W1, H, w1v, tid);
+        wload(P + pk.W2, MP, w3v, tid);
         const float* src = MODE == FVP ? a.V : P;   // FVP: dW1r / dW2r;  FWD: W1r / W2r
-        wload(src + pk.W1, H, w2v, tid);
-        wload(src + pk.W2, MP, w4v, tid);
+        rv1 = wload_rows<64>(src + pk.W1, H, tid);
+        rv2 = wload_rows<32>(src + pk.W2, MP, tid);
     }
     const float* BV = MODE == FVP ? a.V : P;
     const float bias1 = BV[pk.b1 + cb * 16 + r16];
@@ -350,31 +391,27 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
     {
         float* red1 = D0;          // [8][64] column-max partials (D0 / D0B are free until P1)
         float* red3 = D0 + 512;
+        // the row-scaled images first: their scales need no barrier
         if (MODE == EVAL) {
-            wscale<false>(w1v, sc1, nullptr, tid);
-            wscale<false>(w3v, sc3, nullptr, tid);
+            wrows_store<64>(rv1, S1, L::WIMG, sc1, tid);
+            wrows_store<32>(rv2, S3, L::WIMG2, sc3, tid);
         } else {
+            wrows_store<64>(rv1, S2, L::WIMG, sc2, tid);
+            wrows_store<32>(rv2, S4, L::WIMG2, sc4v, tid);
             wscale<true>(w1v, sc1, red1, tid);
             wscale<true>(w3v, sc3, red3, tid);
-            wscale<false>(w2v, sc2, nullptr, tid);
-            wscale<false>(w4v, sc4v, nullptr, tid);
         }
-        __syncthreads();
         KX_PRE(2);
         if (MODE != EVAL) {
+            __syncthreads();
             wscale_cols(sc1, red1, tid);
             wscale_cols(sc3, red3, tid);
             __syncthreads();
         }
         KX_PRE(3);
-        if (MODE == EVAL) {
-            wstore<false>(w1v, S1, L::WIMG, sc1, tid);
-            wstore<false>(w3v, S3, L::WIMG2, sc3, tid);
-        } else {
+        if (MODE != EVAL) {
             wstore<true>(w1v, S1, L::WIMG, sc1, tid);
             wstore<true>(w3v, S3, L::WIMG2, sc3, tid);
-            wstore<false>(w2v, S2, L::WIMG, sc2, tid);
-            wstore<false>(w4v, S4, L::WIMG2, sc4v, tid);
         }
     }
     KX_PRE(4);

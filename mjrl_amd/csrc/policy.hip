@@ -1128,7 +1128,6 @@ __global__ void __launch_bounds__(64) k_eval_final(const double* __restrict__ rp
 #include "fused.h"
 #include "ks.h"
 #include "kx.h"
-#include "kv.h"
 
 namespace {
 
@@ -1328,42 +1327,10 @@ int launch_kx_t(const RowArgs& ra, const FOut& fo, int grid, hipStream_t st) {
     return (int)hipGetLastError();
 }
 
-template <int MP, int KG>
-int launch_kv_t(const RowArgs& ra, const FOut& fo, int grid, hipStream_t st) {
-    using L = VLayout<MP, KG>;
-    auto fn = k_kv<MP, KG>;
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, L::bytes);
-        if (e != hipSuccess) return (int)e;
-        attr = true;
-    }
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(VT), L::bytes, st, ra, fo);
-    return (int)hipGetLastError();
-}
-
-// the FVP kernel of split rows: k_kx's FVP mode, or with MJRL_AMD_FVP=kv (read once per
-// process) the pipelined 4-wave k_kv (kv.h; NP = 384, the Humanoid width)
-inline bool fvp_kv() {
-    static const bool v = [] {
-        const char* e = getenv("MJRL_AMD_FVP");
-        return e && e[0] == 'k' && e[1] == 'v' && e[2] == 0;
-    }();
-    return v;
-}
-
-// rows given as split-f16 (ra.xs) run the all-split kernels (FVP: k_kv, FWD / EVAL:
-// k_kx); f32 xhat the exact-f32 k_ks
+// rows given as split-f16 (ra.xs) run the all-split k_kx; f32 xhat the exact-f32 k_ks
 template <int MODE>
 int launch_ks(const mjrl_shape* s, const RowArgs& ra, const FOut& fo, int grid, hipStream_t st) {
     const int kg = s->np / 32;
-    if (ra.xs && MODE == FVP && fvp_kv()) {
-#define MJRL_K(MP_, KG_) \
-    if (s->mp == MP_ && kg == KG_) return launch_kv_t<MP_, KG_>(ra, fo, grid, st);
-        MJRL_K(16, 12)
-        MJRL_K(32, 12)
-#undef MJRL_K
-    }
     if (ra.xs) {
 #define MJRL_K(MP_, KG_) \
     if (s->mp == MP_ && kg == KG_) return launch_kx_t<MP_, KG_, MODE>(ra, fo, grid, st);

@@ -22,8 +22,12 @@ import torch
 from . import _lib
 from .comm import LocalComm
 
-# slots (doubles) in the per-update stats buffer; each moments result takes 8
-S_M1, S_M2, S_PM1, S_PM2, S_MS, S_MW1, S_MW2, S_EVAL = 0, 8, 16, 24, 32, 40, 48, 56
+# slots (doubles) in the per-update stats buffer; each moments result takes 8 (6
+# used).  Layout for the sharded collectives: [0, 32) the advantage / path-return
+# moment records all-gathered as one block (mjrl_moments_combine), [32, 40) the
+# surr_before moments then the two eval sums (one contiguous all-reduce),
+# [40, 56) DAPG's w moments (one all-gathered record).
+S_M1, S_M2, S_PM1, S_PM2, S_MS, S_EVAL, S_MW1, S_MW2 = 0, 8, 16, 24, 32, 38, 40, 48
 N_STATS = 64
 
 
@@ -68,6 +72,33 @@ def _host_threads():
     if quota:
         n = min(n, max(1, int(quota)))
     return max(1, min(16, n))
+
+
+def host_stage(arrs, view, offs, a0, a1, lo=None, hi=None):
+    """Arrays a0 .. a1 - 1 of `arrs` into their rows offs[i]:offs[i+1] of `view`
+    (a pinned host array), converted to view's dtype; with lo / hi (float32 [n])
+    the column ranges of what was written are folded in.  f64 / f32 arrays go
+    through the native one-pass convert-and-range loop (mjrl_host_stage_*, ctypes
+    releases the GIL), anything else through numpy."""
+    fns = None
+    if view.dtype == np.float32 and view.ndim == 2:
+        L = _lib.load()
+        fns = {np.dtype(np.float64): L.mjrl_host_stage_f64, np.dtype(np.float32): L.mjrl_host_stage_f32}
+    for i in range(a0, a1):
+        dst = view[offs[i]:offs[i + 1]]
+        if dst.shape[0] == 0:
+            continue
+        src = np.asarray(arrs[i])
+        fn = fns.get(src.dtype) if fns is not None else None
+        if fn is not None and src.ndim == 2 and src.shape == dst.shape and src.flags.c_contiguous:
+            rc = fn(src.ctypes.data, dst.shape[0], dst.shape[1], dst.ctypes.data,
+                    None if lo is None else lo.ctypes.data, None if hi is None else hi.ctypes.data)
+            _lib.check(rc, "mjrl_host_stage")
+            continue
+        np.copyto(dst, src.reshape(dst.shape), casting="unsafe")
+        if lo is not None:
+            np.fmin(lo, np.nanmin(dst, axis=0) if dst.shape[0] else lo, out=lo)
+            np.fmax(hi, np.nanmax(dst, axis=0) if dst.shape[0] else hi, out=hi)
 
 
 class _PinnedStaging:
@@ -116,10 +147,12 @@ class _PinnedStaging:
             self._dev[slot] = d
         return d[:nbytes].view(tdt)
 
-    def stage(self, slot, arrs, ncols, dtype, device, reuse=False):
+    def stage(self, slot, arrs, ncols, dtype, device, reuse=False, ranges=False):
         """Concatenation of `arrs` (each [rows] or [rows, ncols]) as a device
         tensor [R] / [R, ncols] of `dtype` (np.float32 / np.float64 / np.int64 /
-        np.uint8)."""
+        np.uint8).  ranges=True (float32 [R, ncols] slots): also the per-column
+        (min, max) of the staged values, taken in the same conversion pass, as
+        self.last_range (two float32 [ncols] arrays)."""
         dtype = np.dtype(dtype)
         rows = [int(a.shape[0]) for a in arrs]
         R = sum(rows)
@@ -145,6 +178,8 @@ class _PinnedStaging:
             out = torch.empty(shape, dtype=tdt, device=device)
         view = h[:nbytes].numpy().view(dtype).reshape(shape)
         if R == 0:
+            if ranges and ncols:
+                self.last_range = (np.full(width, np.inf, np.float32), np.full(width, -np.inf, np.float32))
             return out
         cur = torch.cuda.current_stream(device)
         cs = self._copy_stream(device)
@@ -160,13 +195,18 @@ class _PinnedStaging:
             bounds.append(len(rows))
         offs = np.concatenate([[0], np.cumsum(rows)])
 
-        def fill(a0, a1):
-            for i in range(a0, a1):
-                np.copyto(view[offs[i]:offs[i + 1]], np.asarray(arrs[i]).reshape(view[offs[i]:offs[i + 1]].shape),
-                          casting="unsafe")
+        ranges = ranges and dtype == np.float32 and bool(ncols)
+        nchunk = len(bounds) - 1
+        rng = np.empty((nchunk, 2, width), dtype=np.float32) if ranges else None
+        if ranges:
+            rng[:, 0] = np.inf
+            rng[:, 1] = -np.inf
+
+        def fill(k):
+            host_stage(arrs, view, offs, bounds[k], bounds[k + 1], *((rng[k, 0], rng[k, 1]) if ranges else ()))
 
         ex = self.pool()
-        futs = [ex.submit(fill, bounds[k], bounds[k + 1]) for k in range(len(bounds) - 1)]
+        futs = [ex.submit(fill, k) for k in range(nchunk)]
         hflat = h[:nbytes]
         oflat = out.view(-1).view(torch.uint8)
         row_bytes = width * dtype.itemsize
@@ -180,6 +220,8 @@ class _PinnedStaging:
         ev.record(cs)
         self._ev[slot] = ev
         cur.wait_stream(cs)
+        if ranges:
+            self.last_range = (rng[:, 0].min(axis=0), rng[:, 1].max(axis=0))
         return out
 
 
@@ -214,8 +256,13 @@ class DeviceBatch:
     i64 [P+1] row offsets; terminated: u8 [P].  advantages (optional, f64 [T]):
     when given, the GAE scan is skipped (train_from_paths semantics)."""
 
-    def __init__(self, obs, act, rewards, baseline, path_off, terminated, advantages=None, T_demo=0):
+    def __init__(self, obs, act, rewards, baseline, path_off, terminated, advantages=None, T_demo=0, obs_range=None):
         self.obs, self.act = obs, act
+        # f32 [2][n] per-column (min, max) of the staged observations, taken by the
+        # host staging pass (mjrl_host_stage_*): the split rows' column scales come
+        # from it (mjrl_obs_colscale_range) instead of a device pass over obs
+        self.obs_range = obs_range
+        self.T_global = None   # all-rank row count, cached by a sharded update
         self.rewards, self.baseline = rewards, baseline
         self.path_off, self.terminated = path_off, terminated
         self.advantages = advantages
@@ -252,15 +299,18 @@ class DeviceBatch:
         dlen = [len(p["observations"]) for p in (demo_paths or [])]
         T_demo = int(sum(dlen))
 
-        def stage(slot, arrs, ncols, dtype=np.float64):
-            return _STAGING.stage(slot, arrs, ncols, dtype, device, reuse)
+        def stage(slot, arrs, ncols, dtype=np.float64, ranges=False):
+            return _STAGING.stage(slot, arrs, ncols, dtype, device, reuse, ranges=ranges)
 
         # slot after slot: each stage() returns once its copies are issued, so the
         # next slot's conversion overlaps the previous slot's H2D tail (one chunked
         # pipeline for all three slots measured 52 ms against 32.5 ms this way,
         # tools/staging_ab.py, profiles/r03f/staging_ab.txt)
         obs = stage("obs", [p["observations"] for p in paths] + [p["observations"] for p in demo_paths or []], n,
-                    obs_dtype)
+                    obs_dtype, ranges=obs_dtype == np.float32)
+        orange = None
+        if obs_dtype == np.float32:
+            orange = stage("orange", [np.stack(_STAGING.last_range)], n, np.float32)
         act = stage("act", [p["actions"] for p in paths] + [p["actions"] for p in demo_paths or []], m, obs_dtype)
         rew = stage("rew", [p["rewards"] for p in paths], 0)
         off = stage("off", [np.concatenate([[0], np.cumsum(lengths)]).astype(np.int64)], 0, np.int64)
@@ -293,7 +343,7 @@ class DeviceBatch:
                 [baseline.predict(p) if baseline is not None else np.zeros(len(p["rewards"])) for p in paths]
             base = stage("base", preds, 0)
             adv = None
-        b = cls(obs, act, rew, base, off, term, advantages=adv, T_demo=T_demo)
+        b = cls(obs, act, rew, base, off, term, advantages=adv, T_demo=T_demo, obs_range=orange)
         b.lengths = lengths
         return b
 
@@ -384,6 +434,11 @@ class UpdateEngine:
         self.mom_part = torch.zeros(4 * 256 + 16, dtype=torch.float64, device=dev)
         self.mom2_part = torch.zeros(_lib.MOM_SCRATCH, dtype=torch.float64, device=dev)   # one-launch moments
         self.transforms = (None, None, None, None)
+        # sharded schedule (one rank of several, or a one-rank communicator forced
+        # onto it): moments through one all-gather + mjrl_moments_combine, an
+        # all-reduce between every FVP's gather and its CG step
+        self.sharded = bool(getattr(self.comm, "sharded", self.comm.world_size > 1))
+        self.gbuf = torch.zeros(max(self.comm.world_size, 1) * 32, dtype=torch.float64, device=dev)
         self.kernel_timing = None   # list -> (start, accumulate done, gather done) events per FVP
         # capture / replay whole updates as hipGraphs (one process): True, False, or
         # "auto" = only for batches of at most GRAPH_AUTO_ROWS rows, where launch
@@ -533,20 +588,26 @@ class UpdateEngine:
         if reduce:
             self.comm.allreduce_sum(self._stat(out_slot))
 
-    def _allreduce_slots(self, slots):
-        """One SUM all-reduce over several (start, length) slices of the stats buffer
-        (gathered into one small tensor): fewer latency-bound collectives per update."""
-        if self.comm.world_size <= 1:
-            return
-        buf = torch.cat([self.stats[a:a + n] for a, n in slots])
-        self.comm.allreduce_sum(buf)
-        o = 0
-        for a, n in slots:
-            self.stats[a:a + n].copy_(buf[o:o + n])
-            o += n
+    def _reduce_stats(self, a, b):
+        """SUM all-reduce of the contiguous stats slots [a, b) (sharded only)."""
+        if self.sharded:
+            self.comm.allreduce_sum(self.stats[a:b])
 
-    def _pack(self, obs, act, T, st):
-        """a5 batch assembly: f64 obs / act -> the row format the policy passes read."""
+    def _sharded_moments(self, base, rec, ngroups, st):
+        """The local pass-1 / pass-2 records at stats[base:base+rec] of every rank
+        all-gathered in ONE collective and folded into the global moments in place
+        (mjrl_moments_combine)."""
+        W = self.comm.world_size
+        g = self.gbuf[:W * rec]
+        self.comm.allgather(self.stats[base:base + rec], g)
+        _lib.check(self.lib.mjrl_moments_combine(_lib.ptr(g), W, rec, ngroups,
+                                                 C.c_void_p(self.stats[base:].data_ptr()), st),
+                   "mjrl_moments_combine")
+
+    def _pack(self, obs, act, T, st, obs_range=None):
+        """a5 batch assembly: f64 obs / act -> the row format the policy passes read.
+        obs_range: the staged batch's per-column (min, max) (DeviceBatch.obs_range),
+        from which the split rows' column scales follow without a pass over obs."""
         w = self.ws
         ins, isc, _, _ = self.transforms
         sp = C.byref(self.shape)
@@ -554,10 +615,15 @@ class UpdateEngine:
         if f32 != (act.dtype == torch.float32):
             raise ValueError("observations and actions must be staged in the same dtype")
         if self.split:
-            # column scales of this batch (one read pass), then the split rows
-            cs = self.lib.mjrl_obs_colscale_f32 if f32 else self.lib.mjrl_obs_colscale
-            _lib.check(cs(_lib.ptr(obs), T, sp, _lib.ptr(ins), _lib.ptr(isc), _lib.ptr(w["xc"]), st),
-                       "mjrl_obs_colscale")
+            # column scales of this batch, then the split rows
+            if obs_range is not None:
+                _lib.check(self.lib.mjrl_obs_colscale_range(_lib.ptr(obs_range[0]), _lib.ptr(obs_range[1]), sp,
+                                                            _lib.ptr(ins), _lib.ptr(isc), _lib.ptr(w["xc"]), st),
+                           "mjrl_obs_colscale_range")
+            else:
+                cs = self.lib.mjrl_obs_colscale_f32 if f32 else self.lib.mjrl_obs_colscale
+                _lib.check(cs(_lib.ptr(obs), T, sp, _lib.ptr(ins), _lib.ptr(isc), _lib.ptr(w["xc"]), st),
+                           "mjrl_obs_colscale")
             fn = self.lib.mjrl_pack_batch_split_f32 if f32 else self.lib.mjrl_pack_batch_split
             _lib.check(fn(_lib.ptr(obs), _lib.ptr(act), T, sp, _lib.ptr(ins), _lib.ptr(isc), _lib.ptr(w["xc"]),
                           _lib.ptr(w["xs"]), _lib.ptr(w["xu"]), _lib.ptr(w["act32"]), st), "mjrl_pack_batch_split")
@@ -639,13 +705,17 @@ class UpdateEngine:
         theta = self._pad(theta, "theta")
         T, T_demo, P = batch.T, batch.T_demo, batch.P
         T_all = T + T_demo
-        # global row count (all ranks): scales every mean
+        # global row count (all ranks): scales every mean; one host round trip per
+        # staged batch, cached on it (outside any captured graph)
         if T_global is None and self.comm.world_size > 1:
-            tg = torch.tensor([float(T)], dtype=torch.float64, device=self.device)
-            self.comm.allreduce_sum(tg)
-            T_global = float(tg.item())
+            T_global = batch.T_global
+            if T_global is None:
+                tg = torch.tensor([float(T)], dtype=torch.float64, device=self.device)
+                self.comm.allreduce_sum(tg)
+                T_global = batch.T_global = float(tg.item())
         elif T_global is None:
             T_global = float(T)
+        sharded = self.sharded
         sub = None
         if hvp_sample_frac is not None and hvp_sample_frac < 0.99 and algo != "vpg":
             sub = self._hvp_draws(float(hvp_sample_frac), int(round(T_global)), T, int(cg_iters))
@@ -658,9 +728,11 @@ class UpdateEngine:
         ins, isc, osh, osc = self.transforms
         want = self.graphs if graph is None else graph
         if want == "auto":
-            want = T_all <= GRAPH_AUTO_ROWS
-        use_graph = (bool(want) and self.comm.world_size == 1 and sub is None
-                     and algo in ("npg", "vpg", "dapg"))
+            # sharded: always (the graph holds the collectives too, no host launch
+            # or collective-call overhead between the latency-bound steps)
+            want = T_all <= GRAPH_AUTO_ROWS or sharded
+        use_graph = (bool(want) and (self.comm.world_size == 1 or getattr(self.comm, "capturable", False))
+                     and sub is None and algo in ("npg", "vpg", "dapg"))
         if use_graph:
             key = self._graph_key(batch, T_global, (algo, gamma, gae_lambda, n_step_size, const_lr, kl_dist, cg_iters,
                                                     damping, residual_tol, learn_rate, skip_gae, demo_coef))
@@ -696,21 +768,22 @@ class UpdateEngine:
             elif not skip_gae:
                 self.returns_advantages(batch, gamma, gae_lambda, stream=C.c_void_p(side.cuda_stream))
             # a5: batch assembly (f64 -> f32, input normalisation, bias column)
-            self._pack(batch.obs, batch.act, T_all, st)
+            self._pack(batch.obs, batch.act, T_all, st, batch.obs_range)
             main.wait_stream(side)
             # whitening (npg_cg.py:91) and path-return statistics (npg_cg.py:97-102):
             # two-pass fp64 moments, both quantities in one launch per pass; when
             # sharded, each pass's sums share one all-reduce (plus one MAX for the
             # path-return extrema)
+            # (sharded: both passes local — pass 2 about this rank's own mean — then
+            # one all-gather of the four records and mjrl_moments_combine)
             sp_ = lambda slot: C.c_void_p(self.stats[slot:].data_ptr())
             mp2 = _lib.ptr(self.mom2_part)
             _lib.check(L.mjrl_moments2(_lib.ptr(adv64), T, None, _lib.ptr(w["path_ret"]), P, None, mp2, sp_(S_M1),
                                        sp_(S_PM1), st), "mjrl_moments2")
-            self._allreduce_slots([(S_M1, 3), (S_PM1, 3)])
-            self.comm.allreduce_max(self.stats[S_PM1 + 4:S_PM1 + 6])
             _lib.check(L.mjrl_moments2(_lib.ptr(adv64), T, sp_(S_M1), _lib.ptr(w["path_ret"]), P, sp_(S_PM1), mp2,
                                        sp_(S_M2), sp_(S_PM2), st), "mjrl_moments2")
-            self._allreduce_slots([(S_M2, 3), (S_PM2, 3)])
+            if sharded:
+                self._sharded_moments(S_M1, 32, 2, st)
             dapg = algo == "dapg" and demo_coef is not None
             # whitening + surr_before = mean(LR * adv) with LR == 1 (npg_cg.py:113) in one
             # launch; the surr_before all-reduce rides with the first post-step evaluation's
@@ -721,10 +794,10 @@ class UpdateEngine:
             if dapg:
                 _lib.check(L.mjrl_moments2(_lib.ptr(w["w64"]), T, None, None, 0, None, mp2, sp_(S_MW1), None, st),
                            "mjrl_moments2")
-                self._allreduce_slots([(S_MW1, 3)])
                 _lib.check(L.mjrl_moments2(_lib.ptr(w["w64"]), T, sp_(S_MW1), None, 0, None, mp2, sp_(S_MW2), None, st),
                            "mjrl_moments2")
-                self._allreduce_slots([(S_MW2, 3)])
+                if sharded:
+                    self._sharded_moments(S_MW1, 16, 1, st)
                 _lib.check(L.mjrl_dapg_adv(_lib.ptr(w["w64"]), T, C.c_void_p(self.stats[S_MW1:].data_ptr()),
                                            C.c_void_p(self.stats[S_MW2:].data_ptr()), T_demo, float(demo_coef),
                                            _lib.ptr(w["adv_vpg"]), st), "mjrl_dapg_adv")
@@ -762,7 +835,11 @@ class UpdateEngine:
                 inv_T_fvp = inv_T if sub is None else 1.0 / max(sub["Ts"], 1)
                 # gather + CG z fused when no all-reduce sits between them and the CG
                 # state holds one p.z partial per 64 parameters
-                fuse_cg = self.comm.world_size == 1 and (s.d + 63) // 64 <= (_lib.CG_STATE - _lib.CG_PZ_PARTS) // 2
+                cg_zx = (s.d + 63) // 64 <= (_lib.CG_STATE - _lib.CG_PZ_PARTS) // 2
+                fuse_cg = not sharded and cg_zx
+                # sharded: gather -> all-reduce -> mjrl_cg_z -> mjrl_cg_step_xr_p (the one-launch
+                # mjrl_cg_step1, which forms z over all of d in every workgroup, only past the
+                # CG state's p.z partial capacity)
                 for k in range(int(cg_iters)):
                     rows_k, sc_k, T_k = rows_fvp, sc_fvp, T
                     if sub is not None:
@@ -796,6 +873,17 @@ class UpdateEngine:
                                    "mjrl_cg_step_xr_p")
                         continue
                     self.comm.allreduce_sum(v["gsum"])
+                    if cg_zx:
+                        # z + p.z partials from the reduced sum, then the one-process iteration tail
+                        _lib.check(L.mjrl_cg_z(sp, _lib.ptr(v["gsum"]), inv_T_fvp, float(damping),
+                                               _lib.ptr(self.packed_theta), _lib.ptr(v["p"]), _lib.ptr(v["z"]),
+                                               _lib.ptr(self.cg), _lib.ptr(self.done), st), "mjrl_cg_z")
+                        r_in, r_out = (v["r"], v["r2"]) if k % 2 == 0 else (v["r2"], v["r"])
+                        _lib.check(L.mjrl_cg_step_xr_p(sp, _lib.ptr(v["x"]), _lib.ptr(r_in), _lib.ptr(r_out),
+                                                       _lib.ptr(v["p"]), _lib.ptr(v["z"]), _lib.ptr(self.packed_p),
+                                                       _lib.ptr(self.cg), _lib.ptr(self.done), float(residual_tol),
+                                                       st), "mjrl_cg_step_xr_p")
+                        continue
                     # the rest of the iteration in one launch; r and p alternate between two buffers each
                     (r_in, r_out), (p_in, p_out) = ((v["r"], v["r2"]), (v["p"], v["p2"])) if k % 2 == 0 else \
                         ((v["r2"], v["r"]), (v["p2"], v["p"]))
@@ -820,10 +908,10 @@ class UpdateEngine:
                                               C.byref(sc_fvp), C.c_void_p(self.stats[S_EVAL:].data_ptr()), st),
                            "mjrl_policy_eval")
                 if ms_pending[0]:
-                    self._allreduce_slots([(S_MS, 3), (S_EVAL, 2)])
+                    self._reduce_stats(S_MS, S_EVAL + 2)   # surr_before's moments + the eval sums
                     ms_pending[0] = False
                 else:
-                    self._allreduce_slots([(S_EVAL, 2)])
+                    self._reduce_stats(S_EVAL, S_EVAL + 2)
 
             if algo == "vpg":
                 step(1, 0.0, np.float32(learn_rate), 0)
@@ -882,8 +970,8 @@ class UpdateEngine:
     # the engine workspace, whose addresses are part of the key.
     def _graph_key(self, batch, T_global, args):
         ptrs = tuple(0 if t is None else t.data_ptr() for t in (
-            batch.obs, batch.act, batch.rewards, batch.baseline, batch.path_off, batch.terminated, batch.advantages)
-            + tuple(self.transforms))
+            batch.obs, batch.act, batch.rewards, batch.baseline, batch.path_off, batch.terminated, batch.advantages,
+            batch.obs_range) + tuple(self.transforms))
         return (ptrs, batch.T, batch.T_demo, batch.P, float(T_global), self._ws_gen, self.kernel_timing is not None,
                 tuple(args))
 

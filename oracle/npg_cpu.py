@@ -85,6 +85,44 @@ def path_return_stats(rewards, lengths):
     return [np.mean(pr), np.std(pr), np.amin(pr), np.amax(pr)]
 
 
+def moments_record(x):
+    """One shard's 16-double moment record of the sharded update (the layout
+    mjrl_moments_combine folds): pass 1 [sum, sum^2, n, min, max, -min] at 0..5,
+    pass 2 about the shard's own mean [sum(x - m_r), sum((x - m_r)^2), n, ...] at
+    8..13.  The mean / std of npg_cg.py:91, 97-102 over the union of the shards
+    follow from the records alone (moments_combine)."""
+    x = np.asarray(x, dtype=np.float64)
+    r = np.zeros(16)
+    n = float(len(x))
+    mn, mx = (x.min(), x.max()) if len(x) else (np.inf, -np.inf)
+    r[0:6] = [x.sum(), (x * x).sum(), n, mn, mx, -mn]
+    c = x.sum() / n if len(x) else 0.0
+    r[8:14] = [(x - c).sum(), ((x - c) ** 2).sum(), n, mn, mx, -mn]
+    return r
+
+
+def moments_combine(records):
+    """The fold of every shard's record (rank order): global [S, SS, N, min, max,
+    -min] and [sum(x - mean), M2 about the global mean, N, ...], with M2 =
+    sum_r [M2_r + 2 (m_r - mean) D_r + n_r (m_r - mean)^2] — exact algebra, so
+    mean = out[0] / out[2] and std = sqrt(out[9] / out[2]) are np.mean / np.std of
+    the concatenation up to rounding."""
+    R = np.asarray(records, dtype=np.float64).reshape(len(records), 16)
+    S, SS, N = R[:, 0].sum(), R[:, 1].sum(), R[:, 2].sum()
+    mn, mx = R[:, 3].min(), R[:, 4].max()
+    mean = S / N
+    D = M2 = 0.0
+    for r in R:
+        if r[2] > 0:
+            dm = r[0] / r[2] - mean
+            M2 += r[9] + 2.0 * dm * r[8] + r[2] * dm * dm
+            D += r[8] + r[2] * dm
+    out = np.zeros(16)
+    out[0:6] = [S, SS, N, mn, mx, -mn]
+    out[8:14] = [D, M2, N, mn, mx, -mn]
+    return out
+
+
 def linear_baseline_features(obs_path):
     """LinearBaseline._features (baselines/linear_baseline.py:10-18)."""
     o = np.clip(obs_path, -10, 10)

@@ -1,11 +1,12 @@
 """world_size-2 gloo test of the sharded update's collective schedule (CPU).
 
 Every rank takes its shard of a golden batch (mjrl_amd.comm.partition_paths),
-computes the per-shard SUMS the device kernels produce (whitening moments,
-path-return moments + extrema, VPG sum, FVP sums) — here with the oracle as the
-stand-in compute, since this container has no GPU — all-reduces them through
-mjrl_amd.comm.DistComm exactly as mjrl_amd.engine.UpdateEngine.update does, and
-finishes with the replicated CG.  The result must equal the unsharded update.
+computes the per-shard quantities the device kernels produce (the local moment
+records of the advantages and path returns, VPG sum, FVP sums) — here with the
+oracle as the stand-in compute, since this container has no GPU — exchanges them
+through mjrl_amd.comm.DistComm exactly as mjrl_amd.engine.UpdateEngine.update
+does (one all-gather of the moment records folded as mjrl_moments_combine does,
+one all-reduce per VPG / FVP sum), and finishes with the replicated CG.  The result must equal the unsharded update.
 The same schedule runs over RCCL on the GPU box (tests/test_gpu_dist.py)."""
 import os
 import socket
@@ -43,25 +44,21 @@ def _worker(rank, world, port, name, q):
         r0, r1 = offs[p0], offs[p1]
         adv = c["advantages"][r0:r1]
         T = float(r1 - r0)
-        # whitening: two-pass moments, all-reduced (engine.update S_M1 / S_M2)
-        m1 = torch.tensor([adv.sum(), 0.0, T], dtype=torch.float64)
-        comm.allreduce_sum(m1)
-        mean = m1[0].item() / m1[2].item()
-        m2 = torch.tensor([(adv - mean).sum(), ((adv - mean) ** 2).sum(), T], dtype=torch.float64)
-        comm.allreduce_sum(m2)
-        w = (adv - mean) / (np.sqrt(m2[1].item() / m1[2].item()) + 1e-6)
-        # path-return stats: sums + MAX over [max, -min]
+        # whitening + path-return stats (engine.update, sharded): each rank's two
+        # local passes as moment records, ONE all-gather, the fixed-order fold of
+        # mjrl_moments_combine (restated by O.moments_combine)
         pr = np.array([np.sum(c["rewards"][offs[i]:offs[i + 1]]) for i in range(p0, p1)])
-        pm1 = torch.tensor([pr.sum(), 0.0, float(len(pr))], dtype=torch.float64)
-        comm.allreduce_sum(pm1)
-        mx = torch.tensor([pr.max() if len(pr) else -np.inf, -pr.min() if len(pr) else -np.inf],
-                          dtype=torch.float64)
-        comm.allreduce_max(mx)
-        pmean = pm1[0].item() / pm1[2].item()
-        pm2 = torch.tensor([((pr - pmean) ** 2).sum()], dtype=torch.float64)
-        comm.allreduce_sum(pm2)
-        stats = [pmean, np.sqrt(pm2[0].item() / pm1[2].item()), -mx[1].item(), mx[0].item()]
-        Tg = m1[2].item()
+        rec = torch.from_numpy(np.concatenate([O.moments_record(adv), O.moments_record(pr)]))
+        g = torch.zeros(world * 32, dtype=torch.float64)
+        comm.allgather(rec, g)
+        g = g.numpy().reshape(world, 32)
+        ma = O.moments_combine(g[:, :16])
+        mp_ = O.moments_combine(g[:, 16:])
+        mean = ma[0] / ma[2]
+        w = (adv - mean) / (np.sqrt(ma[9] / ma[2]) + 1e-6)
+        pmean = mp_[0] / mp_[2]
+        stats = [pmean, np.sqrt(mp_[9] / mp_[2]), -mp_[5], mp_[4]]
+        Tg = ma[2]
         # VPG: per-shard sum, all-reduced, divided by the global row count
         pol = O.Policy(int(c["n"]), int(c["m"]), c["hidden_t"], c["theta0"], c["transforms"])
         obs, act = c["obs64"][r0:r1], c["act64"][r0:r1]

@@ -74,6 +74,9 @@ class BatchREINFORCE:
     # policy's own input precision, half the PCIe bytes) or float64 (the device
     # LinearBaseline then predicts / fits from the sampler's exact values)
     staging_dtype = np.float32
+    # whether MJRL_AMD_DEVICES / devices= may hand the update to the GPU worker pool
+    # (an algorithm whose update does not shard, PPO, runs in this process)
+    _poolable = True
 
     def __init__(self, env, policy, baseline, learn_rate=0.01, seed=None, save_logs=False, device=None,
                  comm=None, devices=None):
@@ -97,6 +100,7 @@ class BatchREINFORCE:
         d = dict(self.__dict__)
         d["_engine"] = None
         d["_last_batch"] = None   # device tensors
+        d.pop("_pre", None)       # views of a pool worker's shared segment
         if not isinstance(d.get("_comm"), (LocalComm, type(None))):
             d["_comm"] = None     # a process group does not pickle; re-resolved on use
         return d
@@ -123,7 +127,7 @@ class BatchREINFORCE:
         several devices from one controller process, else None."""
         from ..comm import launched_world
         from ..pool import resolve_devices, get_pool
-        if self._comm is not None or launched_world() is not None:
+        if not self._poolable or self._comm is not None or launched_world() is not None:
             return None
         devices = resolve_devices(getattr(self, "_devices", None))
         return None if devices is None else get_pool(devices)
@@ -243,12 +247,21 @@ class BatchREINFORCE:
     def _sample_shard(self, trajectory_sampler, batch_sampler, comm, N, sample_mode, env_name, T, num_cpu):
         """This rank's share of the sampling.  'trajectories': shard_count(N) paths
         with pegasus seed `seed + first` (the offset trajectory_sampler.py:40-44
-        gives worker i); 'samples': n_r = ceil(N / world) timesteps with seed
-        `seed + r n_r`, rank r's slot of the iteration's N-seed window (the
-        reference itself advances the seed by N per iteration, batch_reinforce.py:84;
-        an offset of r N would hand rank r - 1 of the next iteration exactly rank
-        r's starting seed of this one).  num_cpu='max' becomes this rank's share of
-        the host cores."""
+        gives worker i).  'samples': n_r = ceil(N / world) timesteps.  On one core
+        (batch_sampler.sample_paths_one_core: one seed per path, and a path has at
+        least one step, so at most n_r seeds) the rank's seed is `seed + r n_r`,
+        rank r's slot of the iteration's N-seed window (the reference itself
+        advances the seed by N per iteration, batch_reinforce.py:84; an offset of
+        r N would hand rank r - 1 of the next iteration exactly rank r's starting
+        seed of this one).  On several cores the reference's loop
+        (batch_sampler.py:39-51) advances its seed cumulatively
+        (`pegasus_seed += paths_so_far`), far past n_r, so rank slots of any fixed
+        width could overlap and two ranks would replay the same env resets in one
+        batch: _sample_calls keeps that loop (paths_per_call paths per call until
+        more than n_r steps) with the calls of all ranks interleaved instead, call
+        k of rank r seeded at `seed + (k world + r) w`, w the seeds one call uses —
+        disjoint across ranks and calls within the iteration.  num_cpu='max'
+        becomes this rank's share of the host cores."""
         if num_cpu is None or num_cpu == "max":
             num_cpu = max(1, mp.cpu_count() // comm.world_size)
         if sample_mode == "trajectories":
@@ -259,9 +272,29 @@ class BatchREINFORCE:
             seed = self.seed + first if self.seed is not None else None
             return trajectory_sampler.sample_paths_parallel(n_r, self.policy, T, env_name, seed, num_cpu)
         n_r = int(np.ceil(N / comm.world_size))
+        if num_cpu != 1:
+            return self._sample_calls(trajectory_sampler, comm, n_r, env_name, T, num_cpu)
         seed = self.seed + comm.rank * n_r if self.seed is not None else None
         return batch_sampler.sample_paths(n_r, self.policy, T, env_name=env_name, pegasus_seed=seed,
                                           num_cpu=num_cpu)
+
+    def _sample_calls(self, trajectory_sampler, comm, n_r, env_name, T, num_cpu, paths_per_call=5):
+        """batch_sampler.sample_paths' multi-core loop (batch_sampler.py:39-51) for
+        rank r of a sharded samples-mode step, seeds interleaved over the ranks
+        (see _sample_shard).  One call of trajectory_sampler.sample_paths_parallel
+        seeds worker i at base + i ceil(P / c) (trajectory_sampler.py:37-44), so it
+        uses w = c ceil(P / c) seeds, c = min(cpu_count, num_cpu)."""
+        c = min(mp.cpu_count(), int(num_cpu))
+        w = c * int(np.ceil(paths_per_call / c))
+        paths, so_far, k = [], 0, 0
+        while so_far <= n_r:
+            seed = self.seed + (k * comm.world_size + comm.rank) * w if self.seed is not None else None
+            new = trajectory_sampler.sample_paths_parallel(paths_per_call, self.policy, T, env_name, seed, num_cpu,
+                                                           suppress_print=True, mode="sample")
+            paths += new
+            so_far += int(np.sum([len(p["rewards"]) for p in new]))
+            k += 1
+        return paths
 
     def _fit_baseline(self, paths, return_errors=False):
         """baseline.fit(paths) (batch_reinforce.py:93-101).  A LinearBaseline is
@@ -290,7 +323,7 @@ class BatchREINFORCE:
         advantages into the path dicts like the reference does."""
         eng = self.engine()
         batch = DeviceBatch.from_paths(paths, eng.device, baseline=self.baseline, demo_paths=self._demo_paths(),
-                                       obs_dtype=self.staging_dtype, reuse=True)
+                                       obs_dtype=self.staging_dtype, reuse=True, pre=self.__dict__.pop("_pre", None))
         ret, adv = eng.returns_advantages(batch, gamma, gae_lambda)
         ret, adv = ret.cpu().numpy(), adv.cpu().numpy()
         base = batch.baseline.cpu().numpy()
@@ -309,7 +342,7 @@ class BatchREINFORCE:
             return self._apply_pool(pool.step(self, paths, "paths"), paths)
         eng = self.engine()
         batch = DeviceBatch.from_paths(paths, eng.device, use_advantages=True, demo_paths=self._demo_paths(),
-                                       obs_dtype=self.staging_dtype, reuse=True)
+                                       obs_dtype=self.staging_dtype, reuse=True, pre=self.__dict__.pop("_pre", None))
         return self._update(batch, paths)
 
     # ---- hooks for subclasses ---------------------------------------------------

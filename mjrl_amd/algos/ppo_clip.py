@@ -28,6 +28,7 @@ from ..utils.logger import DataLog
 
 
 class PPO(BatchREINFORCE):
+    _poolable = False   # the minibatch order is global: one process, even with MJRL_AMD_DEVICES set
     def __init__(self, env, policy, baseline, clip_coef=0.2, epochs=10, mb_size=64, learn_rate=3e-4, seed=0,
                  save_logs=False, device=None, comm=None):
         super().__init__(env, policy, baseline, learn_rate=learn_rate, seed=seed, save_logs=save_logs,

@@ -147,6 +147,45 @@ class _PinnedStaging:
             self._dev[slot] = d
         return d[:nbytes].view(tdt)
 
+    def stage_host(self, slot, src, device, reuse=False):
+        """A host array that is already the concatenation, in its final dtype (a
+        pool worker's shared-memory view, registered as pinned memory with
+        register_host), copied to a device tensor of the same shape in chunks on
+        the copy stream: no conversion pass and no pinned staging copy."""
+        tdt = {np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64}[src.dtype]
+        nbytes = src.nbytes
+        if reuse:
+            d = self._dev.get(slot)
+            if d is None or d.numel() < max(nbytes, 1) or d.device != torch.device(device):
+                d = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
+                self._dev[slot] = d
+            out = d[:nbytes].view(tdt).view(src.shape)
+        else:
+            out = torch.empty(src.shape, dtype=tdt, device=device)
+        if nbytes == 0:
+            return out
+        cur = torch.cuda.current_stream(device)
+        cs = self._copy_stream(device)
+        cs.wait_stream(cur)
+        hflat = torch.from_numpy(src.reshape(-1).view(np.uint8))
+        oflat = out.view(-1).view(torch.uint8)
+        with torch.cuda.stream(cs):
+            for b0 in range(0, nbytes, self.CHUNK_BYTES):
+                b1 = min(nbytes, b0 + self.CHUNK_BYTES)
+                oflat[b0:b1].copy_(hflat[b0:b1], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(cs)
+        self._ev["pre:" + slot] = ev   # the host array may be rewritten only after this
+        cur.wait_stream(cs)
+        return out
+
+    def wait_host(self, slot):
+        """Blocks until the last copies out of the host array stage_host(slot)
+        was given completed."""
+        ev = self._ev.get("pre:" + slot)
+        if ev is not None:
+            ev.synchronize()
+
     def stage(self, slot, arrs, ncols, dtype, device, reuse=False, ranges=False):
         """Concatenation of `arrs` (each [rows] or [rows, ncols]) as a device
         tensor [R] / [R, ncols] of `dtype` (np.float32 / np.float64 / np.int64 /
@@ -228,6 +267,36 @@ class _PinnedStaging:
 _STAGING = _PinnedStaging()
 
 
+def register_host(arr):
+    """hipHostRegister of a host array's memory (a pool worker's shared-memory
+    segment): H2D copies out of it then run as DMA at full PCIe rate.  Returns
+    an unregister callable (None when the runtime refuses: the copies stay
+    correct, only staged by the driver)."""
+    import ctypes as C
+    lib = _hip_runtime()
+    ptr = C.c_void_p(arr.ctypes.data)
+    if lib.hipHostRegister(ptr, C.c_size_t(arr.nbytes), C.c_uint(0)) != 0:
+        return None
+    return lambda: lib.hipHostUnregister(ptr)
+
+
+_HIP = None
+
+
+def _hip_runtime():
+    """The HIP runtime torch loaded (torch/lib/libamdhip64.so)."""
+    global _HIP
+    if _HIP is None:
+        import ctypes as C
+        path = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
+        _HIP = C.CDLL(path if os.path.exists(path) else "libamdhip64.so")
+        _HIP.hipHostRegister.argtypes = [C.c_void_p, C.c_size_t, C.c_uint]
+        _HIP.hipHostRegister.restype = C.c_int
+        _HIP.hipHostUnregister.argtypes = [C.c_void_p]
+        _HIP.hipHostUnregister.restype = C.c_int
+    return _HIP
+
+
 class _NoEvent:
     """Stand-in timing event for graph captures that cannot hold event records."""
     def record(self, stream=None):
@@ -273,7 +342,7 @@ class DeviceBatch:
 
     @classmethod
     def from_paths(cls, paths, device, baseline=None, use_advantages=False, demo_paths=None, obs_dtype=np.float32,
-                   reuse=False):
+                   reuse=False, pre=None):
         """Stages sampler-format paths (mjrl/samplers/base_sampler.py:76-83) into HBM.
 
         The concatenation (npg_cg.py:87-89) goes straight into pinned host
@@ -285,13 +354,17 @@ class DeviceBatch:
         A device LinearBaseline predict / fit reads the staged observations.
         reuse: stage into the engine-wide grow-only device buffers (one batch
         alive at a time; stable addresses, so hipGraph replay applies).
+        pre: dict(obs=, act=, obs_range=) — the observations / actions of `paths`
+        already concatenated in obs_dtype in (registered) host memory, with their
+        column ranges: copied as they are (a pool worker's shared segment).
         Baseline predictions of other baselines come from the caller's baseline
         object, per path, as compute_advantages does (process_samples.py:23)."""
         with torch.cuda.device(device):
-            return cls._from_paths(paths, device, baseline, use_advantages, demo_paths, np.dtype(obs_dtype), reuse)
+            return cls._from_paths(paths, device, baseline, use_advantages, demo_paths, np.dtype(obs_dtype), reuse,
+                                   pre)
 
     @classmethod
-    def _from_paths(cls, paths, device, baseline, use_advantages, demo_paths, obs_dtype, reuse):
+    def _from_paths(cls, paths, device, baseline, use_advantages, demo_paths, obs_dtype, reuse, pre=None):
         lengths = np.array([len(p["rewards"]) for p in paths], dtype=np.int64)
         T = int(lengths.sum())
         n = paths[0]["observations"].shape[1]
@@ -306,12 +379,19 @@ class DeviceBatch:
         # next slot's conversion overlaps the previous slot's H2D tail (one chunked
         # pipeline for all three slots measured 52 ms against 32.5 ms this way,
         # tools/staging_ab.py, profiles/r03f/staging_ab.txt)
-        obs = stage("obs", [p["observations"] for p in paths] + [p["observations"] for p in demo_paths or []], n,
-                    obs_dtype, ranges=obs_dtype == np.float32)
         orange = None
-        if obs_dtype == np.float32:
-            orange = stage("orange", [np.stack(_STAGING.last_range)], n, np.float32)
-        act = stage("act", [p["actions"] for p in paths] + [p["actions"] for p in demo_paths or []], m, obs_dtype)
+        if pre is not None and not demo_paths and pre["obs"].dtype == obs_dtype and pre["obs"].shape == (T, n):
+            obs = _STAGING.stage_host("obs", pre["obs"], device, reuse)
+            act = _STAGING.stage_host("act", pre["act"], device, reuse)
+            if obs_dtype == np.float32 and pre.get("obs_range") is not None:
+                orange = stage("orange", [np.stack(pre["obs_range"]).astype(np.float32)], n, np.float32)
+        else:
+            obs = stage("obs", [p["observations"] for p in paths] + [p["observations"] for p in demo_paths or []], n,
+                        obs_dtype, ranges=obs_dtype == np.float32)
+            if obs_dtype == np.float32:
+                orange = stage("orange", [np.stack(_STAGING.last_range)], n, np.float32)
+            act = stage("act", [p["actions"] for p in paths] + [p["actions"] for p in demo_paths or []], m,
+                        obs_dtype)
         rew = stage("rew", [p["rewards"] for p in paths], 0)
         off = stage("off", [np.concatenate([[0], np.cumsum(lengths)]).astype(np.int64)], 0, np.int64)
         term = stage("term", [np.array([bool(p.get("terminated", False)) for p in paths], dtype=np.uint8)], 0,

@@ -50,7 +50,7 @@ from multiprocessing import connection, shared_memory
 import numpy as np
 
 # agent attributes that stay with the controller / are rebuilt in a worker
-_LOCAL = ("env", "logger", "_engine", "_comm", "_last_batch", "_pool", "_devices", "_device", "_backend")
+_LOCAL = ("env", "logger", "_engine", "_comm", "_last_batch", "_pool", "_devices", "_device", "_backend", "_pre")
 # agent attributes a worker's update changes and the controller takes back
 _SYNC = ("running_score", "iter_count", "last_update")
 
@@ -79,75 +79,157 @@ def _free_port():
 
 
 class _Layout:
-    """Byte offsets of one shard in its shared-memory segment (8-byte aligned)."""
+    """Byte offsets of one shard in its shared-memory segment (64-byte aligned
+    fields).  obs / act are in `dtype`: float32 when the agent stages in float32
+    (half the bytes; the controller's fill converts them with their column
+    ranges, which go in 'orange', so the worker copies the segment to HBM as it
+    is), float64 otherwise; the rest float64 / int64."""
 
-    def __init__(self, T, P, n, m, with_adv):
+    def __init__(self, T, P, n, m, with_adv, dtype=np.float64):
         self.T, self.P, self.n, self.m = T, P, n, m
+        self.dtype = dt = np.dtype(dtype)
+        f32, f64, i64 = np.dtype(np.float32), np.dtype(np.float64), np.dtype(np.int64)
         off = 0
         self.fields = {}
-        for name, count in (("obs", T * n), ("act", T * m), ("rew", T), ("lengths", P), ("term", P),
-                            ("adv_in", T if with_adv else 0), ("ret", T), ("base", T), ("adv", T)):
-            self.fields[name] = (off, count)
-            off += 8 * count
-        self.nbytes = max(off, 8)
+        for name, count, ft in (("obs", T * n, dt), ("act", T * m, dt), ("orange", 2 * n if dt == f32 else 0, f32),
+                                ("rew", T, f64), ("lengths", P, i64), ("term", P, i64),
+                                ("adv_in", T if with_adv else 0, f64), ("ret", T, f64), ("base", T, f64),
+                                ("adv", T, f64)):
+            self.fields[name] = (off, count, ft)
+            off += -(-count * ft.itemsize // 64) * 64
+        self.nbytes = max(off, 64)
 
     def view(self, buf, name):
-        off, count = self.fields[name]
-        dt = np.int64 if name in ("lengths", "term") else np.float64
-        return np.ndarray((count,), dtype=dt, buffer=buf, offset=off)
+        off, count, ft = self.fields[name]
+        return np.ndarray((count,), dtype=ft, buffer=buf, offset=off)
+
+
+def _segment_dtype(agent):
+    """float32 segments when the agent stages its observations in float32 and
+    fits its baseline from the batch in HBM (device LinearBaseline / MLPBaseline):
+    nothing in the worker then reads the float64 values; otherwise float64."""
+    f32 = np.dtype(getattr(agent, "staging_dtype", np.float64)) == np.float32
+    dev_fit = type(getattr(agent, "baseline", None)).__name__ in ("LinearBaseline", "MLPBaseline")
+    return np.float32 if (f32 and dev_fit) else np.float64
+
+
+def _fill_shard(buf, L, sh, lengths):
+    """The shard's paths `sh` into its segment.  float32 layouts: the native
+    convert-and-range pass (engine.host_stage, the staging path's own) writes
+    obs / act and the per-column (min, max) of obs into 'orange'."""
+    if sh:
+        if L.dtype == np.float32:
+            from .engine import host_stage
+            offs = np.concatenate([[0], np.cumsum(lengths)])
+            rng = L.view(buf, "orange").reshape(2, L.n)
+            rng[0], rng[1] = np.inf, -np.inf
+            host_stage([p["observations"] for p in sh], L.view(buf, "obs").reshape(L.T, L.n), offs, 0, len(sh),
+                       rng[0], rng[1])
+            host_stage([p["actions"] for p in sh], L.view(buf, "act").reshape(L.T, L.m), offs, 0, len(sh))
+        else:
+            np.concatenate([np.asarray(p["observations"], np.float64).reshape(-1) for p in sh],
+                           out=L.view(buf, "obs"))
+            np.concatenate([np.asarray(p["actions"], np.float64).reshape(-1) for p in sh], out=L.view(buf, "act"))
+        np.concatenate([np.asarray(p["rewards"], np.float64) for p in sh], out=L.view(buf, "rew"))
+        if L.fields["adv_in"][1]:
+            np.concatenate([np.asarray(p["advantages"], np.float64) for p in sh], out=L.view(buf, "adv_in"))
+    L.view(buf, "lengths")[:] = lengths
+    L.view(buf, "term")[:] = [int(bool(p.get("terminated", False))) for p in sh]
 
 
 class DevicePool:
     """N worker processes, one per GPU of `devices`, driven from this process."""
 
-    def __init__(self, devices, backend="nccl", timeout=900.0):
+    def __init__(self, devices, backend="nccl", timeout=900.0, connect_timeout=600.0):
         self.devices = list(devices)
         self.world = len(self.devices)
         self.backend = backend
         self.timeout = timeout
         self._shm = [None] * self.world
+        self._digests = {}
+        self._procs = []
+        self._conns = [None] * self.world
         authkey = secrets.token_bytes(16)
         self._listener = connection.Listener(("127.0.0.1", 0), authkey=authkey)
         host, port = self._listener.address
         dist_port = _free_port()
         env = dict(os.environ)
         env["MJRL_AMD_DEVICES"] = ""          # a worker never starts a pool of its own
-        env["PYTHONPATH"] = os.pathsep.join([p for p in sys.path if p and os.path.isdir(p)])
-        self._procs = []
-        for r, d in enumerate(self.devices):
-            cmd = [sys.executable, "-u", "-m", "mjrl_amd.pool", "--address", "%s:%d" % (host, port),
-                   "--authkey", authkey.hex(), "--rank", str(r), "--world", str(self.world), "--device", str(d),
-                   "--backend", backend, "--dist-port", str(dist_port)]
-            self._procs.append(subprocess.Popen(cmd, env=env))
-        self._conns = [None] * self.world
-        # a worker that dies before it connects would leave accept() waiting: a
-        # watchdog closes the listener then
-        import threading
-        done = threading.Event()
-
-        def watch():
-            while not done.wait(0.5):
-                if any(p.poll() is not None for p in self._procs):
-                    self._listener.close()
-                    return
-        threading.Thread(target=watch, daemon=True).start()
+        # the package's own root first: an import through '' (the caller's cwd)
+        # does not survive train_agent's chdir into the job directory
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        env["PYTHONPATH"] = os.pathsep.join([root] + [os.path.abspath(p) for p in sys.path if p and os.path.isdir(p)])
         try:
-            for _ in range(self.world):
-                c = self._listener.accept()
-                rank = c.recv()
-                self._conns[rank] = c
-        except OSError:
-            for p in self._procs:
-                if p.poll() is None:
-                    p.kill()
-            raise RuntimeError("mjrl_amd pool: a worker exited before connecting (codes %s)"
-                               % [p.poll() for p in self._procs]) from None
-        finally:
-            done.set()
-        for r, c in enumerate(self._conns):
-            msg = self._recv(r)
-            if msg[0] != "ready":
-                raise RuntimeError("mjrl_amd pool worker %d failed to start: %s" % (r, msg[1]))
+            for r, d in enumerate(self.devices):
+                cmd = [sys.executable, "-u", "-m", "mjrl_amd.pool", "--address", "%s:%d" % (host, port),
+                       "--authkey", authkey.hex(), "--rank", str(r), "--world", str(self.world), "--device", str(d),
+                       "--backend", backend, "--dist-port", str(dist_port)]
+                self._procs.append(subprocess.Popen(cmd, env=env))
+            self._accept_all(connect_timeout)
+            for r in range(self.world):
+                msg = self._recv(r)
+                if msg[0] != "ready":
+                    raise RuntimeError("mjrl_amd pool worker %d failed to start: %s" % (r, msg[1]))
+        except BaseException:
+            self._abort()
+            raise
+
+    def _accept_all(self, connect_timeout):
+        """Accepts the workers' connections, polling: a worker that exits before
+        it connects ends the wait with a RuntimeError (a blocked accept() is not
+        woken by closing its socket from another thread)."""
+        import select
+        sock = self._listener._listener._socket
+        t0 = time.time()
+        for _ in range(self.world):
+            while not select.select([sock], [], [], 0.25)[0]:
+                dead = [r for r, p in enumerate(self._procs) if p.poll() is not None]
+                if dead:
+                    raise RuntimeError("mjrl_amd pool: worker(s) %s exited before connecting (codes %s)"
+                                       % (dead, [self._procs[r].returncode for r in dead]))
+                if time.time() - t0 > connect_timeout:
+                    raise TimeoutError("mjrl_amd pool: workers did not connect within %.0f s" % connect_timeout)
+            c = self._listener.accept()
+            rank = c.recv()
+            self._conns[rank] = c
+
+    def _abort(self):
+        """After any failure: kill every worker (the others may be blocked in a
+        collective, or hold a stale reply), unlink the segments, and forget the
+        pool, so the next use starts a fresh one."""
+        for p in self._procs:
+            if p.poll() is None:
+                p.kill()
+        for p in self._procs:
+            try:
+                p.wait(timeout=30)
+            except Exception:
+                pass
+        for c in self._conns:
+            if c is not None:
+                try:
+                    c.close()
+                except Exception:
+                    pass
+        self._conns = [None] * self.world
+        self._free_segments()
+        try:
+            self._listener.close()
+        except Exception:
+            pass
+        for k, v in list(_POOLS.items()):
+            if v is self:
+                del _POOLS[k]
+
+    def _free_segments(self):
+        for s in self._shm:
+            if s is not None:
+                try:
+                    s.close()
+                    s.unlink()
+                except Exception:
+                    pass
+        self._shm = [None] * self.world
 
     # ---- plumbing -------------------------------------------------------------
     def _recv(self, r):
@@ -159,6 +241,30 @@ class DevicePool:
             if time.time() - t0 > self.timeout:
                 raise TimeoutError("mjrl_amd pool worker %d did not answer within %.0f s" % (r, self.timeout))
         return c.recv()
+
+    def _recv_all(self):
+        """Every worker's reply to a step, in any order: the first error reply or
+        dead worker ends the wait at once (the other ranks are then typically
+        blocked in a collective with the failed one; the caller aborts them)."""
+        replies = [None] * self.world
+        pending = set(range(self.world))
+        t0 = time.time()
+        while pending:
+            ready = connection.wait([self._conns[r] for r in pending], timeout=1.0)
+            for c in ready:
+                r = self._conns.index(c)
+                msg = c.recv()
+                if msg[0] != "ok":
+                    raise RuntimeError("mjrl_amd pool worker %d failed:\n%s" % (r, msg[1]))
+                replies[r] = msg
+                pending.discard(r)
+            for r in pending:
+                if self._procs[r].poll() is not None:
+                    raise RuntimeError("mjrl_amd pool worker %d exited with code %s" % (r, self._procs[r].returncode))
+            if pending and time.time() - t0 > self.timeout:
+                raise TimeoutError("mjrl_amd pool workers %s did not answer within %.0f s" % (sorted(pending),
+                                                                                            self.timeout))
+        return replies
 
     def _segment(self, r, nbytes):
         s = self._shm[r]
@@ -180,12 +286,25 @@ class DevicePool:
                 p.wait(timeout=60)
             except Exception:
                 p.kill()
-        for s in self._shm:
-            if s is not None:
-                s.close()
-                s.unlink()
-        self._shm = [None] * self.world
+        self._free_segments()
         self._listener.close()
+
+    def _state(self, agent, commit=True):
+        """The agent as the workers rebuild it: its __getstate__ (the device
+        engine, batch and trainer dropped) minus the controller-local attributes,
+        pickled per attribute; only the attributes whose pickle changed since the
+        last step travel (DAPG's demo_paths and the hyperparameters once, the
+        policy / baseline / running statistics every step).  commit=False: the
+        delta without recording it as sent."""
+        import hashlib
+        d = agent.__getstate__() if hasattr(type(agent), "__getstate__") else dict(agent.__dict__)
+        blobs = {k: pickle.dumps(v, protocol=pickle.HIGHEST_PROTOCOL) for k, v in d.items() if k not in _LOCAL}
+        digests = {k: hashlib.blake2b(b, digest_size=16).digest() for k, b in blobs.items()}
+        changed = {k: b for k, b in blobs.items() if self._digests.get(k) != digests[k]}
+        dropped = [k for k in self._digests if k not in blobs]
+        if commit:
+            self._digests = digests
+        return dict(cls=type(agent), changed=changed, dropped=dropped)
 
     # ---- one update -------------------------------------------------------------
     def step(self, agent, paths, mode, gamma=0.995, gae_lambda=0.98, fit=False, return_errors=False):
@@ -201,40 +320,31 @@ class DevicePool:
         if any(p1 <= p0 for p0, p1 in parts):
             raise ValueError("%d paths over %d GPU workers: every worker needs at least one path"
                              % (len(paths), self.world))
-        state = pickle.dumps(dict(cls=type(agent), d={k: v for k, v in agent.__dict__.items() if k not in _LOCAL}))
         with_adv = mode == "paths"
-        layouts = []
+        dtype = _segment_dtype(agent)
         import concurrent.futures as cf
 
         def fill(r):
             p0, p1 = parts[r]
-            sh = paths[p0:p1]
-            L = _Layout(int(lengths[p0:p1].sum()), p1 - p0, n, m, with_adv)
-            seg = self._segment(r, L.nbytes)
-            if sh:
-                np.concatenate([np.asarray(p["observations"], np.float64).reshape(-1) for p in sh],
-                               out=L.view(seg.buf, "obs"))
-                np.concatenate([np.asarray(p["actions"], np.float64).reshape(-1) for p in sh],
-                               out=L.view(seg.buf, "act"))
-                np.concatenate([np.asarray(p["rewards"], np.float64) for p in sh], out=L.view(seg.buf, "rew"))
-                if with_adv:
-                    np.concatenate([np.asarray(p["advantages"], np.float64) for p in sh], out=L.view(seg.buf, "adv_in"))
-            L.view(seg.buf, "lengths")[:] = lengths[p0:p1]
-            L.view(seg.buf, "term")[:] = [int(bool(p.get("terminated", False))) for p in sh]
+            L = _Layout(int(lengths[p0:p1].sum()), p1 - p0, n, m, with_adv, dtype)
+            _fill_shard(self._segment(r, L.nbytes).buf, L, paths[p0:p1], lengths[p0:p1])
             return L
 
-        with cf.ThreadPoolExecutor(self.world) as ex:
-            layouts = list(ex.map(fill, range(self.world)))
-        rng = np.random.get_state()
-        for r in range(self.world):
-            L = layouts[r]
-            self._conns[r].send(("step", dict(state=state, shm=self._shm[r].name, T=L.T, P=L.P, n=n, m=m,
-                                              mode=mode, gamma=gamma, gae_lambda=gae_lambda, fit=fit,
-                                              return_errors=return_errors, rng=rng, with_adv=with_adv)))
-        replies = [self._recv(r) for r in range(self.world)]
-        for r, msg in enumerate(replies):
-            if msg[0] != "ok":
-                raise RuntimeError("mjrl_amd pool worker %d failed:\n%s" % (r, msg[1]))
+        try:
+            state = self._state(agent)
+            with cf.ThreadPoolExecutor(self.world) as ex:
+                layouts = list(ex.map(fill, range(self.world)))
+            rng = np.random.get_state()
+            for r in range(self.world):
+                L = layouts[r]
+                self._conns[r].send(("step", dict(state=state, shm=self._shm[r].name, T=L.T, P=L.P, n=n, m=m,
+                                                  dtype=L.dtype.str, mode=mode, gamma=gamma, gae_lambda=gae_lambda,
+                                                  fit=fit, return_errors=return_errors, rng=rng,
+                                                  with_adv=with_adv)))
+            replies = self._recv_all()
+        except BaseException:
+            self._abort()
+            raise
         if mode == "samples":
             for r in range(self.world):
                 p0, p1 = parts[r]
@@ -321,28 +431,36 @@ def _worker_main(args):
         return 1
     conn.send(("ready",))
     engines = {}
-    shm = None
+    blobs = {}          # the agent's attributes as last sent (pickles)
+    shm = unreg = None
     while True:
         msg = conn.recv()
         if msg[0] == "close":
             break
+        paths = agent = None
         try:
             a = msg[1]
             if shm is None or shm.name != a["shm"]:
-                if shm is not None:
-                    shm.close()
-                shm = shared_memory.SharedMemory(name=a["shm"])
-                _untrack(shm)
-            L = _Layout(a["T"], a["P"], a["n"], a["m"], a["with_adv"])
+                shm, unreg = _attach(shm, unreg, a["shm"])
+            L = _Layout(a["T"], a["P"], a["n"], a["m"], a["with_adv"], np.dtype(a["dtype"]))
             paths = _worker_paths(L, shm.buf)
-            st = pickle.loads(a["state"])
+            st = a["state"]
+            for k in st["dropped"]:
+                blobs.pop(k, None)
+            blobs.update(st["changed"])
             agent = st["cls"].__new__(st["cls"])
-            agent.__dict__.update(st["d"])
+            # unpickled afresh every step: the update mutates the policy / baseline
+            agent.__dict__.update({k: pickle.loads(b) for k, b in blobs.items()})
             agent.env = None
             agent.logger = DataLog()
             agent._comm = comm
             agent._device = None
             agent._devices = None
+            if L.dtype == np.float32 and L.T:
+                rng = L.view(shm.buf, "orange").reshape(2, L.n)
+                # the segment is the staged batch: copied to HBM as it is
+                agent._pre = dict(obs=L.view(shm.buf, "obs").reshape(L.T, L.n),
+                                  act=L.view(shm.buf, "act").reshape(L.T, L.m), obs_range=(rng[0], rng[1]))
             key = (agent.policy.n, agent.policy.m, agent.policy.hidden)
             agent._engine = engines.get(key)
             np.random.set_state(a["rng"])
@@ -370,10 +488,36 @@ def _worker_main(args):
             conn.send(("ok", out))
         except Exception:
             conn.send(("error", traceback.format_exc()))
-    if shm is not None:
-        shm.close()
+    paths = agent = None
+    _attach(shm, unreg, None)
     dist.destroy_process_group()
     return 0
+
+
+def _attach(shm, unreg, name):
+    """Detaches from the current segment (unregistering it as pinned memory) and
+    attaches to segment `name`, registered with hipHostRegister when this worker
+    has a GPU, so the H2D copies of its batch run as DMA straight out of it."""
+    import gc
+    import torch
+    if shm is not None:
+        if unreg is not None:
+            torch.cuda.synchronize()
+            unreg()
+        gc.collect()             # views of the old segment (the last step's paths)
+        try:
+            shm.close()
+        except BufferError:
+            pass                 # still viewed: the mapping goes with the process
+    if name is None:
+        return None, None
+    shm = shared_memory.SharedMemory(name=name)
+    _untrack(shm)
+    unreg = None
+    if torch.cuda.is_available():
+        from .engine import register_host
+        unreg = register_host(np.ndarray((shm.size,), np.uint8, buffer=shm.buf))
+    return shm, unreg
 
 
 def _untrack(shm):

@@ -108,6 +108,129 @@ def test_pool_train_from_paths(pool_env):
     np.testing.assert_allclose(out[1][1], out[0][1], rtol=1e-6)
 
 
+def _adv_paths(seed=3):
+    rs = np.random.RandomState(seed)
+    return [dict(observations=rs.randn(h, N_OBS) * 10 ** rs.uniform(-3, 3, N_OBS), actions=rs.randn(h, N_ACT),
+                 rewards=rs.randn(h), advantages=rs.randn(h)) for h in (7, 30, 12, 3, 25)]
+
+
+def _agent(cls, devices, **kw):
+    from mjrl_amd.baselines.linear_baseline import LinearBaseline
+    from mjrl_amd.policies.gaussian_mlp import MLP
+    from mjrl_amd.utils.gym_env import EnvSpec
+    spec = EnvSpec(N_OBS, N_ACT, 100, 1)
+    return cls(_Env(), MLP(spec, hidden_sizes=(32, 32), seed=0), LinearBaseline(spec), devices=devices, **kw)
+
+
+def test_pool_f32_segments(pool_env):
+    """float32 staging: the workers get the batch already converted, with its
+    column ranges (the worker-side checks are in StubNPG32), and the update equals
+    the one-process one."""
+    from stub_pool_agent import StubNPG32
+    paths = _adv_paths()
+    out = []
+    for devices in (None, [0, 0]):
+        ag = _agent(StubNPG32, devices)
+        if devices is None:
+            ag._pre = dict(obs=np.concatenate([p["observations"] for p in paths]).astype(np.float32),
+                           act=np.concatenate([p["actions"] for p in paths]).astype(np.float32))
+            ag._pre["obs_range"] = (ag._pre["obs"].min(0), ag._pre["obs"].max(0))
+        out.append((ag.train_from_paths(paths), ag.policy.get_param_values()))
+    np.testing.assert_allclose(out[1][0], out[0][0], rtol=1e-12)
+    np.testing.assert_allclose(out[1][1], out[0][1], rtol=1e-6)
+
+
+def test_fill_shard_layouts():
+    """The controller's fill of a segment, read back as the worker reads it."""
+    from mjrl_amd.pool import _Layout, _fill_shard, _worker_paths
+    paths = _adv_paths(5)
+    lengths = np.array([len(p["rewards"]) for p in paths])
+    for dt in (np.float64, np.float32):
+        L = _Layout(int(lengths.sum()), len(paths), N_OBS, N_ACT, True, dt)
+        buf = bytearray(L.nbytes)
+        _fill_shard(buf, L, paths, lengths)
+        got = _worker_paths(L, buf)
+        for p, q in zip(paths, got):
+            assert q["observations"].dtype == dt
+            np.testing.assert_array_equal(q["observations"], p["observations"].astype(dt))
+            np.testing.assert_array_equal(q["actions"], p["actions"].astype(dt))
+            np.testing.assert_array_equal(q["rewards"], p["rewards"])
+            np.testing.assert_array_equal(q["advantages"], p["advantages"])
+        if dt == np.float32:
+            rng = L.view(buf, "orange").reshape(2, N_OBS)
+            allo = np.concatenate([p["observations"] for p in paths]).astype(np.float32)
+            np.testing.assert_array_equal(rng[0], allo.min(0))
+            np.testing.assert_array_equal(rng[1], allo.max(0))
+        assert all(off % 64 == 0 for off, _, _ in L.fields.values())
+
+
+def test_pool_state_travels_once(pool_env):
+    """Attributes whose pickle did not change since the last step stay with the
+    workers (hyperparameters, DAPG demos); the policy travels every step."""
+    from stub_pool_agent import StubNPG
+    from mjrl_amd import pool
+    ag = _agent(StubNPG, [0, 0])
+    ag.demo_like = np.arange(1000.0)
+    paths = _adv_paths()
+    ag.train_from_paths(paths)
+    p = next(iter(pool._POOLS.values()))
+    st = p._state(ag, commit=False)                 # what the next step sends: the update's results
+    assert "policy" in st["changed"] and "demo_like" not in st["changed"] and "n_step_size" not in st["changed"]
+    p._state(ag)                      # as if sent
+    st = p._state(ag, commit=False)   # nothing changed since
+    assert not st["changed"] and not st["dropped"]
+    ag.policy.set_param_values(ag.policy.get_param_values() + 1.0, set_new=True, set_old=True)
+    del ag.demo_like
+    st = p._state(ag, commit=False)
+    assert set(st["changed"]) == {"policy"} and st["dropped"] == ["demo_like"]
+    th = ag.policy.get_param_values()
+    ref = _agent(StubNPG, None)
+    ref.policy.set_param_values(th, set_new=True, set_old=True)
+    ref.running_score = ag.running_score
+    # the workers rebuild the agent from their cache + the delta
+    np.testing.assert_allclose(ag.train_from_paths(paths), ref.train_from_paths(paths), rtol=1e-12)
+    np.testing.assert_allclose(ag.policy.get_param_values(), ref.policy.get_param_values(), rtol=1e-6)
+
+
+def test_pool_worker_exits_before_connecting(pool_env, monkeypatch):
+    """A worker that dies before it connects (e.g. an import error) ends the pool
+    start with a RuntimeError instead of an accept() that never returns."""
+    import sys
+    import time
+    from mjrl_amd import pool
+    monkeypatch.setattr(sys, "executable", "/bin/false")
+    t0 = time.time()
+    with pytest.raises(RuntimeError, match="exited before connecting"):
+        pool.DevicePool([0, 0], "gloo")
+    assert time.time() - t0 < 30
+
+
+def test_pool_failed_update_is_cleaned_up(pool_env):
+    """One rank's update raises while the other waits in the all-reduce: the step
+    raises at once, every worker is killed, the segments are unlinked and the
+    pool is forgotten; the next step starts a fresh pool."""
+    import time
+    from multiprocessing import shared_memory
+    from stub_pool_agent import FailingNPG, StubNPG
+    from mjrl_amd import pool
+    paths = _adv_paths()
+    ag = _agent(FailingNPG, [0, 0])
+    t0 = time.time()
+    with pytest.raises(RuntimeError, match="update failed on rank 1"):
+        ag.train_from_paths(paths)
+    assert time.time() - t0 < 60
+    assert not pool._POOLS
+    ag2 = _agent(StubNPG, [0, 0])
+    ag2.train_from_paths(paths)
+    p = next(iter(pool._POOLS.values()))
+    assert all(q.poll() is None for q in p._procs)
+    names = [s.name for s in p._shm]
+    pool.close_pools()
+    for nm in names:
+        with pytest.raises(FileNotFoundError):
+            shared_memory.SharedMemory(name=nm)
+
+
 def test_resolve_devices(monkeypatch):
     from mjrl_amd.pool import resolve_devices
     monkeypatch.delenv("MJRL_AMD_DEVICES", raising=False)

@@ -80,11 +80,11 @@ def _agent(baseline_kind, comm=None):
     return agent
 
 
-def _run_steps(agent, N, mode):
+def _run_steps(agent, N, mode, num_cpu=1):
     stub_samplers.install()
     out = []
     for _ in range(2):
-        stats = agent.train_step(N, sample_mode=mode, gamma=0.99, gae_lambda=0.95, num_cpu=1)
+        stats = agent.train_step(N, sample_mode=mode, gamma=0.99, gae_lambda=0.95, num_cpu=num_cpu)
         seeds = [round(float(p["rewards"][0]), 12) for p in agent._stub_paths]
         coeffs = getattr(agent.baseline, "_coeffs", None)
         out.append(dict(stats=stats, seed=agent.seed, first=seeds, coeffs=None if coeffs is None else coeffs.copy(),
@@ -94,23 +94,23 @@ def _run_steps(agent, N, mode):
     return out
 
 
-def _worker(rank, world, port, kind, N, mode, q):
+def _worker(rank, world, port, kind, N, mode, q, num_cpu=1):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from mjrl_amd.comm import DistComm
-        q.put((rank, _run_steps(_agent(kind, DistComm()), N, mode)))
+        q.put((rank, _run_steps(_agent(kind, DistComm()), N, mode, num_cpu)))
     finally:
         dist.destroy_process_group()
 
 
-def _sharded(kind, N, mode, world=2):
+def _sharded(kind, N, mode, world=2, num_cpu=1):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, kind, N, mode, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, kind, N, mode, q, num_cpu)) for r in range(world)]
     for p in procs:
         p.start()
     out = {}
@@ -174,6 +174,47 @@ def test_train_step_sharded_samples_mode():
     # no rank starts where any rank started before (the next iteration's rank 0 vs
     # this one's rank 1 included): no two shards replay the same env resets
     assert len(set(starts)) == len(starts), starts
+
+
+def test_train_step_sharded_samples_mode_multicore():
+    """num_cpu > 1: the reference's multi-core loop advances its seed cumulatively
+    (batch_sampler.py:45), so the ranks' calls are interleaved instead
+    (BatchREINFORCE._sample_calls): call k of rank r at seed + (2k + r) w, w = 2 x
+    ceil(5 / 2) = 6 seeds per call on two cores; every rank draws more than its
+    n_r = 125 steps, and no env reset is replayed by two ranks in one batch."""
+    N = 250
+    out = _sharded("linear", N, "samples", num_cpu=2)
+    for it in range(2):
+        base = 1000 + N * it
+        seeds = {}
+        for r in range(2):
+            calls = out[r][it]["calls"]
+            assert all(c[0] == "trajectories" and c[1] == 5 and c[3] == 2 for c in calls)
+            assert [c[2] for c in calls] == [base + (2 * k + r) * 6 for k in range(len(calls))]
+            seeds[r] = {c[2] + i for c in calls for i in range(5)}
+            # the loop stops on the first call that takes the rank past n_r steps
+            h = [min(stub_samplers.HORIZON - (s % 7), 1e6) for s in sorted(seeds[r])]
+            assert sum(h) > 125 and sum(h[:-5]) <= 125
+        assert not seeds[0] & seeds[1]
+        assert out[0][it]["seed"] == out[1][it]["seed"] == base + N
+        assert out[0][it]["stats"] == out[1][it]["stats"]
+
+
+def test_ppo_stays_in_process_with_devices_set(monkeypatch):
+    """MJRL_AMD_DEVICES hands NPG / TRPO / DAPG updates to the worker pool; PPO's
+    update does not shard (one global minibatch order) and stays in this process."""
+    from mjrl_amd.algos.npg_cg import NPG
+    from mjrl_amd.algos.ppo_clip import PPO
+    from mjrl_amd import pool
+    monkeypatch.setenv("MJRL_AMD_DEVICES", "0,1")
+    started = []
+    monkeypatch.setattr(pool, "get_pool", lambda devices, backend=None: started.append(devices) or "pool")
+    ppo = PPO.__new__(PPO)
+    ppo._comm, ppo._devices = None, None
+    assert ppo._pool() is None and not started
+    npg = NPG.__new__(NPG)
+    npg._comm, npg._devices = None, None
+    assert npg._pool() == "pool" and started == [[0, 1]]
 
 
 def test_dapg_demo_share():

@@ -41,6 +41,14 @@ sys.path.insert(0, ROOT)
 
 METRIC = "NPG train_step timesteps/sec, Humanoid 1M-step batch @ 1/2/4/8 MI355X"
 GAMMA, LAM, CG_ITERS, DAMPING = 0.995, 0.97, 10, 1e-4
+# the reference's own update measured on CPU (8 vCPU Xeon, torch
+# CPU, synthetic inputs of the same shapes; BASELINE.json publishes no number), in
+# timesteps/s: vs_baseline = value / this, on the config's full batch
+REF_CPU = {"c4": (1e6 / 42.08, "BASELINE.md: reference update 42.08 s per 1M timesteps, 8 vCPU Xeon"),
+           "c3": (1e5 / 3.084, "BASELINE.md: reference TRPO update 3.084 s per 100k timesteps, 8 vCPU Xeon"),
+           "c5": (4e4 / 3.126, "BASELINE.md: reference DAPG update 3.126 s per 40k RL timesteps, 8 vCPU Xeon"),
+           "c2": (12500 / 0.180, "BASELINE.md: reference NPG update 0.180 s per 12.5k timesteps, 8 vCPU Xeon")}
+
 CONFIGS = {
     "c4": dict(workload="humanoid_npg_1M", metric=METRIC, n=376, m=17, hidden=(64, 64), paths=1000, horizon=1000,
                algo="npg", step=dict(n_step_size=0.01)),
@@ -384,11 +392,57 @@ def e2e_from_host(paths_range, eng, th0, base, upd, device, cfg, reps=3):
         one()
         ts.append(time.perf_counter() - t0)
     dt = float(np.median(ts))
+    tl = e2e_timeline(paths, eng, th, base, upd, device)
     return dict(value=round(T / dt, 1), unit="timesteps/s", ms_per_step=round(dt * 1e3, 2),
-                staging_ms=round(float(np.median(stage_ms)), 2),
+                staging_ms=round(float(np.median(stage_ms)), 2), timeline=tl,
                 note="numpy f64 paths -> f32 into reused pinned slabs on %d host threads, chunked H2D "
                      "overlapping the conversion -> device LinearBaseline.predict -> update -> readback; "
                      "median of %d (staging_ms: the staging alone, synchronised)" % (host_threads(), reps))
+
+
+def e2e_timeline(paths, eng, th, base, upd, device):
+    """One more end-to-end update with the staging traced (engine._PinnedStaging
+    .trace): host conversion spans per chunk, each chunk's H2D copy timed with
+    events on the copy stream, and the device update after the staging, all in
+    ms from the update's start.  Summarised: conversion span, H2D span and busy
+    time, bytes and GB/s, and the update's tail after the last copy."""
+    from mjrl_amd import engine as E
+    torch.cuda.synchronize()
+    E._STAGING.trace = tr = []
+    ref = torch.cuda.Event(enable_timing=True)
+    ref.record()
+    h0 = time.perf_counter()
+    try:
+        b = E.DeviceBatch.from_paths(paths, device, baseline=base, reuse=True)
+    finally:
+        E._STAGING.trace = None
+    u0 = torch.cuda.Event(enable_timing=True)
+    u0.record()
+    eng.update(b, th, **upd)
+    u1 = torch.cuda.Event(enable_timing=True)
+    u1.record()
+    torch.cuda.synchronize()
+    h1 = time.perf_counter()
+    fills = [c["fill"] for c in tr if c["fill"]]
+    cp = [(ref.elapsed_time(c["ev"][0]), ref.elapsed_time(c["ev"][1]), c["bytes"], c["slot"]) for c in tr]
+    nbytes = sum(c[2] for c in cp)
+    busy = sum(c[1] - c[0] for c in cp)
+    by_slot = {}
+    for c in cp:
+        d = by_slot.setdefault(c[3], [0, 0.0])
+        d[0] += c[2]
+        d[1] += c[1] - c[0]
+    return dict(
+        chunks=len(cp), h2d_bytes=nbytes,
+        convert_ms=[round((min(f[0] for f in fills) - h0) * 1e3, 2), round((max(f[1] for f in fills) - h0) * 1e3, 2)]
+        if fills else None,
+        h2d_ms=[round(min(c[0] for c in cp), 2), round(max(c[1] for c in cp), 2)] if cp else None,
+        h2d_busy_ms=round(busy, 2), h2d_GBps=round(nbytes / busy / 1e6, 1) if busy else None,
+        h2d_by_slot={k: dict(bytes=v[0], busy_ms=round(v[1], 3)) for k, v in by_slot.items()},
+        update_ms=[round(ref.elapsed_time(u0), 2), round(ref.elapsed_time(u1), 2)],
+        wall_ms=round((h1 - h0) * 1e3, 2),
+        note="ms from the update's start: host f64 -> f32 conversion span (first chunk start, last chunk end), "
+             "device H2D span and summed copy time, the update after the staging (device events)")
 
 
 def kernel_names(eng, cfg):
@@ -421,9 +475,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--paths", type=int, default=None, help="paths per update (default: the config's)")
-    ap.add_argument("--cpu-rows", type=int, default=200000,
-                    help="timesteps of the bounded CPU-baseline sample (c4; the other configs use their full batch)")
-    ap.add_argument("--cpu-full", action="store_true", help="CPU baseline on the full batch of the config")
+    ap.add_argument("--cpu-rows", type=int, default=None,
+                    help="timesteps of a bounded CPU-baseline sample (default: the config's full batch; about "
+                         "40 s per update at Humanoid 1M on 16 cores)")
+    ap.add_argument("--cpu-full", action="store_true", help="(the default) CPU baseline on the full batch")
     ap.add_argument("--cpu-reps", type=int, default=None,
                     help="timed CPU-baseline updates (default: 3 at c4, 10 for the smaller configs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -610,7 +665,10 @@ def main():
         ms = elapsed / args.steps * 1e3
         out = dict(metric=cfg["metric"], value=round(T_total * args.steps / elapsed, 1), unit="timesteps/s",
                    n_gpus=world, steps=args.steps, warmup=args.warmup, ms_per_step=round(ms, 3),
-                   higher_is_better=True, scaling="strong", vs_baseline=None,
+                   higher_is_better=True, scaling="strong",
+                   vs_baseline=round(T_total * args.steps / elapsed / REF_CPU[args.config][0], 1)
+                   if args.config in REF_CPU and not args.paths else None,
+                   vs_baseline_source=REF_CPU[args.config][1] if args.config in REF_CPU and not args.paths else None,
                    dtype="f32" if not eng.split else "f32 (split-f16 MFMA, f32 accumulate)",
                    data="synthetic (seeded N(0,1) obs/act/rewards, LinearBaseline fitted on 20 paths)",
                    config=dict(workload=cfg["workload"], obs_dim=n, act_dim=m, hidden=list(hidden),
@@ -628,9 +686,12 @@ def main():
             log("end-to-end from host paths")
             out["e2e_from_host"] = e2e_from_host((p0, p1), eng, th, base, upd, device, cfg)
         if world == 1 and not args.no_cpu_baseline:
-            rows = T_total if (args.cpu_full or args.config != "c4") else min(args.cpu_rows, T_total)
+            rows = T_total if (args.cpu_full or not args.cpu_rows) else min(args.cpu_rows, T_total)
             reps = args.cpu_reps or (3 if args.config == "c4" else 10)
             out["cpu_baseline"] = cpu_baseline(rows, base, reps=reps, cfg=cfg)
+            # BASELINE.md holds no published number (vs_baseline stays null); the
+            # ratio to the CPU restatement timed beside it on this host:
+            out["vs_cpu_baseline"] = round(out["value"] / out["cpu_baseline"]["value"], 2)
         print(json.dumps(out), file=json_out, flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

@@ -112,6 +112,10 @@ def load(path=None):
     if _LIB is not None:
         return _LIB
     path = path or os.environ.get("MJRL_AMD_LIB") or LIB_PATH
+    if not os.path.isabs(path) and not os.path.exists(path):
+        # a relative MJRL_AMD_LIB names a file under the repository root (pool
+        # workers and train_agent run from other working directories)
+        path = os.path.join(os.path.dirname(HERE), path)
     if not os.path.exists(path):
         raise MjrlError("mjrl_amd HIP library not built: %s (run `python -m mjrl_amd.build`)" % path)
     lib = C.CDLL(path)

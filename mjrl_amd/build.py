@@ -74,5 +74,10 @@ if __name__ == "__main__":
     ap.add_argument("--prof", action="store_true", help="phase-profiling variant (libmjrl_amd_prof.so)")
     ap.add_argument("--tag", default="", help="variant suffix: lib/libmjrl_amd<tag>.so")
     ap.add_argument("--extra", default="", help="extra hipcc flags of the variant (space separated)")
+    ap.add_argument("--debug", action="store_true",
+                    help="device-checked variant lib/libmjrl_amd_dbg.so (-DMJRL_DEVICE_CHECKS: slab indices "
+                         "against the scratch; select it with MJRL_AMD_LIB=<path>)")
     args = ap.parse_args()
+    if args.debug:
+        args.tag, args.extra = args.tag or "_dbg", args.extra + " -DMJRL_DEVICE_CHECKS"
     print(build(args.force, args.j, args.prof, args.tag, args.extra.split()))

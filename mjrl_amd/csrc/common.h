@@ -290,6 +290,27 @@ __device__ __forceinline__ double block_sum(double v, double* red /* LDS, >= NT/
 __host__ __device__ __forceinline__ int round_up(int x, int m) { return (x + m - 1) / m * m; }
 
 // ---------------------------------------------------------------------------
+// Debug build only (-DMJRL_DEVICE_CHECKS: python -m mjrl_amd.build --debug ->
+// lib/libmjrl_amd_dbg.so): every weight-gradient slab index is checked against
+// the scratch the caller sized with mjrl_scratch_size (wcap floats, passed in the
+// kernel arguments), and a bad one prints the kernel's file:line, workgroup,
+// index and bound, then traps.  Release builds compile the checks out.
+// ---------------------------------------------------------------------------
+#ifdef MJRL_DEVICE_CHECKS
+#define MJRL_SLAB_CHECK(idx, cap)                                                                          \
+    do {                                                                                                 \
+        const int64_t i_ = (int64_t)(idx), c_ = (int64_t)(cap);                                          \
+        if (i_ < 0 || i_ >= c_) {                                                                        \
+            printf("MJRL_SLAB_CHECK %s:%d wg %d thread %d: slab index %lld outside [0, %lld)\n", __FILE__, \
+                   __LINE__, (int)blockIdx.x, (int)threadIdx.x, (long long)i_, (long long)c_);            \
+            __builtin_trap();                                                                            \
+        }                                                                                                \
+    } while (0)
+#else
+#define MJRL_SLAB_CHECK(idx, cap) ((void)0)
+#endif
+
+// ---------------------------------------------------------------------------
 // Grid-wide fixed-order fold without a grid barrier: every workgroup stores its
 // (already block-reduced) partial, and the LAST workgroup to take a ticket folds
 // all nwg partials in index order (lane l: partials l, l + 64, ... then a fixed

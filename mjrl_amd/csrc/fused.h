@@ -54,6 +54,7 @@ struct FOut {
     float* wpart;
     int64_t off0, off1, boff1, off2, boff2;   // per-job slab offsets (make_jobs; unused by the flat writers)
     int n, m;                                 // k_kx / k_ks / k_fused: flat layout wpart[f / 64][S][64] (k_gather_flat)
+    int64_t wcap;                             // floats of the scratch's slabs (MJRL_SLAB_CHECK)
 };
 
 // acc[i][j] += sum_{t<64} G[t][n-block] * A[t][k-block], both row-major in LDS.
@@ -399,7 +400,10 @@ __global__ void __launch_bounds__(FT, 1) k_fused(RowArgs a, FOut o) {
     const int fb0 = H0 * nobs, fW1 = fb0 + H0, fb1 = fW1 + H1 * H0, fW2 = fb1 + H1, fb2 = fW2 + mact * H1;
     float* wp = o.wpart + blk * 64;
     const int64_t cs = (int64_t)gridDim.x * 64;
-    auto put = [&](int f, float v) { wp[(int64_t)(f >> 6) * cs + (f & 63)] = v; };
+    auto put = [&](int f, float v) {
+        MJRL_SLAB_CHECK(blk * 64 + (int64_t)(f >> 6) * cs + (f & 63), o.wcap);
+        wp[(int64_t)(f >> 6) * cs + (f & 63)] = v;
+    };
 #pragma unroll
     for (int c = 0; c < NCH; ++c)
 #pragma unroll

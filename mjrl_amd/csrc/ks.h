@@ -406,7 +406,10 @@ __global__ void __launch_bounds__(KT, 1) k_ks(RowArgs a, FOut o) {
         const int fb0 = H * nobs, fW1 = fb0 + H, fb1 = fW1 + H * H, fW2 = fb1 + H, fb2 = fW2 + mact * H;
         float* wp = o.wpart + blk * 64;
         const int64_t cs = (int64_t)gridDim.x * 64;
-        auto put = [&](int f, float v) { wp[(int64_t)(f >> 6) * cs + (f & 63)] = v; };
+        auto put = [&](int f, float v) {
+            MJRL_SLAB_CHECK(blk * 64 + (int64_t)(f >> 6) * cs + (f & 63), o.wcap);
+            wp[(int64_t)(f >> 6) * cs + (f & 63)] = v;
+        };
 #pragma unroll
         for (int g = 0; g < KG; ++g)
 #pragma unroll

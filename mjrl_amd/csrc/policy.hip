@@ -570,6 +570,7 @@ struct WArgs {
     int64_t rows_per_slice;
     float* wpart;
     const int32_t* done;
+    int64_t wcap;   // floats of the scratch's slabs (MJRL_SLAB_CHECK)
 };
 
 constexpr int WB = 64;        // output block edge
@@ -654,10 +655,16 @@ __global__ void __launch_bounds__(NTHREADS, 2) k_wgrad(WArgs a) {
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
             const int n = n0 + 16 * w + 4 * q + rr;
-            if (n < J.N && k < J.K) out[(int64_t)n * J.K + k] = acc[i][rr];
+            if (n < J.N && k < J.K) {
+                MJRL_SLAB_CHECK(J.off + (int64_t)s * J.N * J.K + (int64_t)n * J.K + k, a.wcap);
+                out[(int64_t)n * J.K + k] = acc[i][rr];
+            }
         }
     }
-    if (do_bias && tid < WB && n0 + tid < J.N) a.wpart[J.boff + (int64_t)s * J.N + n0 + tid] = (float)bsum;
+    if (do_bias && tid < WB && n0 + tid < J.N) {
+        MJRL_SLAB_CHECK(J.boff + (int64_t)s * J.N + n0 + tid, a.wcap);
+        a.wpart[J.boff + (int64_t)s * J.N + n0 + tid] = (float)bsum;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -701,6 +708,7 @@ struct WallArgs {
     int64_t T, rows_per_slice;
     float* wpart;   // flat slab layout (k_gather_flat)
     const int32_t* done;
+    int64_t wcap;   // floats of the scratch's slabs (MJRL_SLAB_CHECK)
 };
 
 // PART 0: all three products (the kernel below); 1: gW1 + gb1 only, 2: gW0, gW2 + gb2
@@ -911,7 +919,10 @@ __device__ __forceinline__ void wall_body(const WallArgs& a, int s, float* sm) {
     const int fb0 = H * n, fW1 = fb0 + H, fb1 = fW1 + H * H, fW2 = fb1 + H, fb2 = fW2 + m * H;
     float* wp = a.wpart + (int64_t)s * 64;
     const int64_t cs = (int64_t)a.S * 64;
-    auto put = [&](int f, float v) { wp[(int64_t)(f >> 6) * cs + (f & 63)] = v; };
+    auto put = [&](int f, float v) {
+        MJRL_SLAB_CHECK((int64_t)s * 64 + (int64_t)(f >> 6) * cs + (f & 63), a.wcap);
+        wp[(int64_t)(f >> 6) * cs + (f & 63)] = v;
+    };
     if constexpr (J1) {
 #pragma unroll
         for (int t = 0; t < S1; ++t) {
@@ -925,7 +936,10 @@ __device__ __forceinline__ void wall_body(const WallArgs& a, int s, float* sm) {
                     // address per row, immediate offsets for the 16-column steps)
                     float* rowp = wp + (int64_t)((fW1 >> 6) + j * (H / 64)) * cs + r16;
 #pragma unroll
-                    for (int kb = 0; kb < HB; ++kb) rowp[(kb >> 2) * cs + 16 * (kb & 3)] = acc1[t][kb][rr];
+                    for (int kb = 0; kb < HB; ++kb) {
+                        MJRL_SLAB_CHECK((rowp - a.wpart) + (kb >> 2) * cs + 16 * (kb & 3), a.wcap);
+                        rowp[(kb >> 2) * cs + 16 * (kb & 3)] = acc1[t][kb][rr];
+                    }
                 } else {
 #pragma unroll
                     for (int kb = 0; kb < HB; ++kb) put(fW1 + j * H + 16 * kb + r16, acc1[t][kb][rr]);
@@ -975,6 +989,7 @@ struct GArgs {
     int n, m, h0, h1, np, mp, d, S;
     int64_t off0, off1, off2, boff1, boff2;
     const float* wpart;
+    int64_t wcap;           // floats of the scratch's slabs (MJRL_SLAB_CHECK)
     const double* lspart;   // FWD: per-row-kernel-WG log-std partials [G][mp]; null for FVP
     int G;
     float* gsum;
@@ -1037,6 +1052,7 @@ __global__ void __launch_bounds__(64 * GATHER_WAVES) k_gather(GArgs a) {
         const int per = (a.S + GATHER_WAVES - 1) / GATHER_WAVES;
         const int s0 = w * per, s1 = min(a.S, s0 + per);
         const float* p = a.wpart + src;
+        if (s1 > s0) MJRL_SLAB_CHECK(src + (int64_t)(s1 - 1) * stride, a.wcap);
         for (int sb = s0; sb < s1; sb += GATHER_PER) {
             float v[GATHER_PER];
 #pragma unroll
@@ -1070,7 +1086,8 @@ __global__ void __launch_bounds__(64 * GATHER_WAVES) k_gather(GArgs a) {
 __global__ void __launch_bounds__(64 * GATHER_WAVES) k_gather_flat(const float* __restrict__ wpart, int S, int d_mu,
                                                                    int d, const double* __restrict__ lspart, int G,
                                                                    int mp, float* __restrict__ gsum,
-                                                                   const int32_t* __restrict__ done, CgZ cz) {
+                                                                   const int32_t* __restrict__ done, CgZ cz,
+                                                                   int64_t wcap) {
     if (done && *done) return;
     __shared__ double part[GATHER_WAVES][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1080,6 +1097,7 @@ __global__ void __launch_bounds__(64 * GATHER_WAVES) k_gather_flat(const float* 
         const int per = (S + GATHER_WAVES - 1) / GATHER_WAVES;
         const int s0 = w * per, s1 = min(S, s0 + per);
         const float* p = wpart + (int64_t)blockIdx.x * S * 64 + lane;
+        if (s1 > s0) MJRL_SLAB_CHECK((int64_t)blockIdx.x * S * 64 + lane + (int64_t)(s1 - 1) * 64, wcap);
         for (int sb = s0; sb < s1; sb += GATHER_PER) {
             float v[GATHER_PER];
 #pragma unroll
@@ -1128,6 +1146,7 @@ __global__ void __launch_bounds__(64) k_eval_final(const double* __restrict__ rp
 #include "fused.h"
 #include "ks.h"
 #include "kx.h"
+#include "kz.h"
 
 namespace {
 
@@ -1157,6 +1176,8 @@ struct JobSet {
     WJob job[3];
     int64_t floats;   // per full set (all slices)
 };
+
+int64_t slab_floats(const mjrl_shape* s, int S);
 
 JobSet make_jobs(const mjrl_shape* s, const mjrl_rows* r, int S) {
     JobSet js{};
@@ -1327,10 +1348,50 @@ int launch_kx_t(const RowArgs& ra, const FOut& fo, int grid, hipStream_t st) {
     return (int)hipGetLastError();
 }
 
-// rows given as split-f16 (ra.xs) run the all-split k_kx; f32 xhat the exact-f32 k_ks
+template <int MP, int KG>
+int launch_kz_t(const RowArgs& ra, const FOut& fo, int grid, hipStream_t st) {
+    using L = ZLayout<MP, KG>;
+    auto fn = k_kz<MP, KG>;
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, L::bytes);
+        if (e != hipSuccess) return (int)e;
+        attr = true;
+    }
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(ZT), L::bytes, st, ra, fo);
+    return (int)hipGetLastError();
+}
+
+#ifdef MJRL_KZ_ROLES_PROBE
+void kz_roles_probe() {   // -Rpass-analysis register counts of each role alone
+    hipLaunchKernelGGL((k_kz<32, 12, 1>), dim3(1), dim3(ZT), 0, 0, RowArgs{}, FOut{});
+    hipLaunchKernelGGL((k_kz<32, 12, 2>), dim3(1), dim3(ZT), 0, 0, RowArgs{}, FOut{});
+    hipLaunchKernelGGL((k_kz<32, 12, 4>), dim3(1), dim3(ZT), 0, 0, RowArgs{}, FOut{});
+}
+#endif
+
+// the FVP of split rows: k_kx's FVP mode, or the three-role pipeline k_kz (kz.h) with
+// MJRL_AMD_FVP=kz (read once per process; A/B runs)
+inline bool fvp_kx() {
+    static const bool v = [] {
+        const char* e = getenv("MJRL_AMD_FVP");
+        return !(e && e[0] == 'k' && e[1] == 'z' && e[2] == 0);
+    }();
+    return v;
+}
+
+// rows given as split-f16 (ra.xs) run the all-split kernel k_kx (FVP optionally
+// k_kz); f32 xhat the exact-f32 k_ks
 template <int MODE>
 int launch_ks(const mjrl_shape* s, const RowArgs& ra, const FOut& fo, int grid, hipStream_t st) {
     const int kg = s->np / 32;
+    if (ra.xs && MODE == FVP && !fvp_kx()) {
+#define MJRL_K(MP_, KG_) \
+    if (s->mp == MP_ && kg == KG_) return launch_kz_t<MP_, KG_>(ra, fo, grid, st);
+        MJRL_K(16, 4) MJRL_K(16, 8) MJRL_K(16, 12)
+        MJRL_K(32, 4) MJRL_K(32, 8) MJRL_K(32, 12)
+#undef MJRL_K
+    }
     if (ra.xs) {
 #define MJRL_K(MP_, KG_) \
     if (s->mp == MP_ && kg == KG_) return launch_kx_t<MP_, KG_, MODE>(ra, fo, grid, st);
@@ -1388,6 +1449,7 @@ int run_fused(int mode, const mjrl_shape* s, const mjrl_rows* r, int64_t T, cons
     JobSet js = make_jobs(s, r, G);
     FOut fo{};
     fo.wpart = sc->wpart;
+    fo.wcap = slab_floats(s, sc->slices);
     fo.off0 = js.job[0].off;
     fo.off1 = js.job[1].off;
     fo.boff1 = js.job[1].boff;
@@ -1410,7 +1472,7 @@ int run_gather(const mjrl_shape* s, const mjrl_rows* r, int64_t T, const mjrl_sc
         const int d_mu = s->d - s->m;
         const int G = p == 2 ? ks_grid(T) : (p == 1 ? fused_grid(T) : row_grid(s, T));   // log-std partial rows
         hipLaunchKernelGGL(k_gather_flat, dim3((s->d + 63) / 64), dim3(64 * GATHER_WAVES), 0, st, sc->wpart, S, d_mu,
-                           s->d, lspart, G, s->mp, gsum, done, cz);
+                           s->d, lspart, G, s->mp, gsum, done, cz, slab_floats(s, sc->slices));
         return (int)hipGetLastError();
     }
     JobSet js = make_jobs(s, r, S);
@@ -1422,6 +1484,7 @@ int run_gather(const mjrl_shape* s, const mjrl_rows* r, int64_t T, const mjrl_sc
         ga.off2 = js.job[2].off; ga.boff2 = js.job[2].boff;
     }
     ga.wpart = sc->wpart;
+    ga.wcap = slab_floats(s, sc->slices);
     ga.lspart = lspart;
     {
         const int p = acc_path(s, T);
@@ -1471,6 +1534,7 @@ int run_wgrad_all(const mjrl_shape* s, const mjrl_rows* r, int64_t T, const mjrl
     const int64_t tiles = (T + bt - 1) / bt;
     wa.rows_per_slice = ((tiles + S - 1) / S) * bt;
     wa.wpart = sc->wpart;
+    wa.wcap = slab_floats(s, sc->slices);
     wa.done = done;
     const int nb = wall_npbm(s);
 #define MJRL_W(H_, MP_, NB_) \
@@ -1502,6 +1566,7 @@ int run_wgrad_only(const mjrl_shape* s, const mjrl_rows* r, int64_t T, const mjr
     const int64_t tiles = (T + WT - 1) / WT;
     wa.rows_per_slice = ((tiles + S - 1) / S) * WT;
     wa.wpart = sc->wpart;
+    wa.wcap = slab_floats(s, sc->slices);
     wa.done = done;
     if (T > 0) {
         hipLaunchKernelGGL(k_wgrad, dim3(tot * S), dim3(NTHREADS), 0, st, wa);
@@ -1530,6 +1595,13 @@ int mjrl_debug_kx_prof(unsigned long long* out) {
     if (e != hipSuccess) return (int)e;
     unsigned long long z[KX_NPROF] = {0};
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_kx_prof), z, sizeof(z));
+}
+
+int mjrl_debug_kz_prof(unsigned long long* out) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_kz_prof), sizeof(unsigned long long) * KZ_NPROF);
+    if (e != hipSuccess) return (int)e;
+    unsigned long long z[KZ_NPROF] = {0};
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_kz_prof), z, sizeof(z));
 }
 #endif
 

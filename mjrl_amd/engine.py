@@ -16,6 +16,8 @@ import functools
 import math
 import os
 
+import time
+
 import numpy as np
 import torch
 
@@ -124,6 +126,9 @@ class _PinnedStaging:
         self._ev = {}
         self._pool = None
         self._copy = {}
+        # a list to record per-chunk host fill times and device copy events into
+        # (bench.py's e2e timeline), or None
+        self.trace = None
 
     def pool(self):
         if self._pool is None:
@@ -241,8 +246,14 @@ class _PinnedStaging:
             rng[:, 0] = np.inf
             rng[:, 1] = -np.inf
 
+        tr = self.trace
+        fill_t = [None] * nchunk
+
         def fill(k):
+            t0 = time.perf_counter() if tr is not None else 0.0
             host_stage(arrs, view, offs, bounds[k], bounds[k + 1], *((rng[k, 0], rng[k, 1]) if ranges else ()))
+            if tr is not None:
+                fill_t[k] = (t0, time.perf_counter())
 
         ex = self.pool()
         futs = [ex.submit(fill, k) for k in range(nchunk)]
@@ -254,7 +265,14 @@ class _PinnedStaging:
                 f.result()
                 b0, b1 = offs[bounds[k]] * row_bytes, offs[bounds[k + 1]] * row_bytes
                 if b1 > b0:
+                    if tr is not None:
+                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        e0.record(cs)
                     oflat[b0:b1].copy_(hflat[b0:b1], non_blocking=True)
+                    if tr is not None:
+                        e1.record(cs)
+                        tr.append(dict(slot=slot, bytes=int(b1 - b0), fill=fill_t[k], issue=time.perf_counter(),
+                                       ev=(e0, e1)))
         ev = torch.cuda.Event()
         ev.record(cs)
         self._ev[slot] = ev

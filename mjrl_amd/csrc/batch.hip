@@ -330,6 +330,7 @@ __global__ void __launch_bounds__(64 * GAE_WAVES) k_gae(const double* __restrict
     __shared__ double sr[GAE_WAVES][GW];
     __shared__ double sb[GAE_WAVES][GW];
     __shared__ double stt[GAE_WAVES][GW];
+    __shared__ double sjunk[GAE_WAVES][GW];   // the stores of chains whose outputs are not kept
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     double* R = sr[w];
     double* B = sb[w];
@@ -378,24 +379,41 @@ __global__ void __launch_bounds__(64 * GAE_WAVES) k_gae(const double* __restrict
                 const bool fwd = lane == 0;
                 const double c = lane == 0 ? 1.0 : (lane == 1 ? gamma : gl);
                 const double* src = lane == 2 ? TD : R;
-                double* dst = lane == 1 ? B : TD;             // returns over B (free now), advantages in place
+                // returns over B (free now), advantages in place; the path-return sum's
+                // (and plain advantages') chain stores into a junk window, so every step's
+                // store is unconditional (an exec-masked store per step cost a branch
+                // with its exec save / restore on the serial chain)
                 const bool put = lane == 1 || (lane == 2 && use_gae);
+                double* dst = lane == 1 ? B : (put ? TD : sjunk[w]);
                 double acc = 0.0;
                 int j = 0;
-                for (; j + GU <= cnt; j += GU) {
-                    double xv[GU];
+                // software-pipelined: the LDS reads of batch j + GU are issued (in program
+                // order, before this batch's stores: legal even in place) ahead of batch
+                // j's serial steps, so only the dependent fp64 multiply-add chain is on
+                // the critical path, not a ~50-cycle LDS round trip per batch
+                const int nfull = cnt / GU * GU;
+                double xv[GU];
+                if (nfull > 0) {
 #pragma unroll
-                    for (int u = 0; u < GU; ++u) xv[u] = src[fwd ? j + u : cnt - 1 - j - u];
+                    for (int u = 0; u < GU; ++u) xv[u] = src[fwd ? u : cnt - 1 - u];
+                }
+                for (; j < nfull; j += GU) {
+                    double xn[GU];
+                    const int jn = j + GU < nfull ? j + GU : j;   // clamped: the last batch re-reads itself
+#pragma unroll
+                    for (int u = 0; u < GU; ++u) xn[u] = src[fwd ? jn + u : cnt - 1 - jn - u];
 #pragma unroll
                     for (int u = 0; u < GU; ++u) {
                         acc = __dadd_rn(xv[u], __dmul_rn(c, acc));
-                        if (put) dst[cnt - 1 - j - u] = acc;
+                        dst[cnt - 1 - j - u] = acc;
                     }
+#pragma unroll
+                    for (int u = 0; u < GU; ++u) xv[u] = xn[u];
                 }
                 for (; j < cnt; ++j) {
                     const int idx = fwd ? j : cnt - 1 - j;
                     acc = __dadd_rn(src[idx], __dmul_rn(c, acc));
-                    if (put) dst[idx] = acc;
+                    dst[idx] = acc;
                 }
                 if (lane == 0) path_ret[p] = acc;
             }

@@ -44,20 +44,9 @@ __device__ unsigned long long g_kx_prof[KX_NPROF];
     } while (0)
 #endif
 
-#ifndef MJRL_KX_P1PIPE
-#define MJRL_KX_P1PIPE 0
-#endif
-
 namespace {
 
 constexpr int AIMG_BYTES = 64 * 64;   // one [64 feature][32 row] f16 activation image
-
-// FVP first-layer pipeline (MJRL_KX_P1PIPE): the next tile's first layer runs in
-// four parts beside this tile's P2 .. P5; part i covers k32 steps
-// [p1_part(i), p1_part(i + 1)) of the wave's observation half (KS = 2, 4, 6)
-__host__ __device__ constexpr int p1_part(int ks, int i) {
-    return ks == 6 ? (i <= 4 ? i : 6) : (i * ks + 3) / 4;   // KS = 6: one step per chain phase, two in P6
-}
 
 template <int MP, int KG>
 struct XLayout {
@@ -519,50 +508,6 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
     }
     auto g0off_at = [&](int g, int) { return g0off[g]; };
 #endif
-    // FVP pipeline (MJRL_KX_P1PIPE): P1 of tile t + G runs in parts beside P2 .. P5 of
-    // tile t, reading its split rows straight from global memory (L2: touched one tile
-    // ahead), and its partials go to D0 / D0B in P6; only the first tile has a P1 phase.
-    // The partials then carry wsc1 only: P2 applies the tile's row scale (a power of
-    // two, so (D0 + D0B) Us is bit-identical to D0 Us + D0B Us)
-    constexpr bool PIPE = MODE == FVP && MJRL_KX_P1PIPE;
-    // the observation-half-0 partial of P1: D0, or (PIPE, written in P5 while D0 holds
-    // G1) the GPf / GPT region, free from P4 to the next P3
-    float* P1A = PIPE ? GPf : D0;
-    static_assert(L::oG1T - L::oGP >= BT * L::LD * 4, "P1A in the GPf / GPT region");
-    const char* xsb = reinterpret_cast<const char*>(a.xs);
-    floatx4 acc1n[2] = {zero4(), zero4()};
-    float pa0[4], pa1[4];   // FVP: cached a0 / a1 at (rows kh*16 + 4q + rr, unit cb*16 + r)
-    auto load_pa = [&](int64_t t_, int lq_, int lr16_) {
-        const int64_t rb_ = t_ * BT;
-        const int nr_ = (int)(T - rb_ < BT ? T - rb_ : BT);
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-            const int row = kh * 16 + 4 * lq_ + rr;
-            // rows past T read row 0 of the tile instead of zero: finite values whose
-            // output-layer weights are masked to zero (gp), so they add nothing, and
-            // no select pulls the wait for these L2 loads to the top of P1
-            const int64_t gi = (rb_ + (row < nr_ ? row : 0)) * H + cb * 16 + lr16_;
-            pa0[rr] = a.a0[gi];
-            pa1[rr] = a.a1[gi];
-        }
-    };
-    // the next tile's split rows of k32 step s (rows clamped into the batch: rows past
-    // T are finite and masked at the output layer); loads only, MFMAs in p1n_mfma
-    auto p1n_load = [&](int64_t tile_, int s, int lq_, int lr16_, half8 (&xh)[2], half8 (&xl)[2]) {
-        const int64_t tn = tile_ + gridDim.x < ntiles ? tile_ + gridDim.x : ntiles - 1;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            int64_t row = tn * BT + i * 16 + lr16_;
-            row = row < T ? row : T - 1;
-            const char* src = xsb + row * (4 * NP) + 2 * (kh * KH + 32 * s + 8 * lq_);
-            xh[i] = *reinterpret_cast<const half8*>(src);
-            xl[i] = *reinterpret_cast<const half8*>(src + 2 * NP);
-        }
-    };
-    auto p1n_mfma = [&](int s, const half8 (&xh)[2], const half8 (&xl)[2]) __attribute__((always_inline)) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i) acc1n[i] = mfma_x3(xh[i], xl[i], wh[s], wl[s], acc1n[i]);
-    };
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         KX_STAMP(9);   // loop top (the wait on the previous tile's last barrier)
         // per-lane indices through an opaque zero: recomputed per tile rather than
@@ -593,7 +538,19 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
         // EVAL has no weight-gradient phase: the next tile's xhat loads go right
         // after the publish, before this tile's unconditional row-pass loads
         if (MODE == EVAL) xload(tile + gridDim.x, ltid);
-        if (MODE == FVP) load_pa(tile, lq, lr16);   // PIPE: pa1 for P2 / P4 (pa0's image came from P6)
+        float pa0[4], pa1[4];   // FVP: cached a0 / a1 at (rows kh*16 + 4q + rr, unit cb*16 + r)
+        if (MODE == FVP) {
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int row = kh * 16 + 4 * lq + rr;
+                // rows past T read row 0 of the tile instead of zero: finite values whose
+                // output-layer weights are masked to zero (gp), so they add nothing, and
+                // no select pulls the wait for these L2 loads to the top of P1
+                const int64_t gi = (row_base + (row < nrow ? row : 0)) * H + cb * 16 + lr16;
+                pa0[rr] = a.a0[gi];
+                pa1[rr] = a.a1[gi];
+            }
+        }
         __syncthreads();
         KX_STAMP(0);
         // EVAL: this tile's row-pass inputs into registers now (L2 hits since the
@@ -630,20 +587,9 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
             } else {
                 touch[0] = *reinterpret_cast<const float*>(a.xs);
             }
-            if constexpr (PIPE) {
-                // the split rows of tile t + 2G (the next P1-in-parts reads them): one
-                // dword per 128-byte line, 12 lines per row
-                const int64_t t2 = tile + 2 * (int64_t)gridDim.x;
-                const int64_t tc = t2 < ntiles ? t2 : ntiles - 1;
-                int64_t row = tc * BT + (ltid < 12 * BT ? ltid / 12 : 0);
-                row = row < T ? row : T - 1;
-                touch[1] = *reinterpret_cast<const float*>(xsb + row * (4 * NP) + 128 * (ltid % 12));
-            }
         }
 
-        // ---- P1: first layer, partial over this wave's observation half (PIPE: the
-        // first tile only; later tiles' P1 runs beside the previous tile's P2 .. P5) ----
-        if (!PIPE || tile == blockIdx.x) {
+        // ---- P1: first layer, partial over this wave's observation half ----
         floatx4 acc1[2] = {zero4(), zero4()};
         {
 #pragma unroll
@@ -660,13 +606,13 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
-                for (int rr = 0; rr < 4; ++rr) acc1[i][rr] *= (PIPE ? 1.f : Us[i * 16 + 4 * lq + rr]) * wsc1;
+                for (int rr = 0; rr < 4; ++rr) acc1[i][rr] *= Us[i * 16 + 4 * lq + rr] * wsc1;
         }
         if (MODE == FVP) {
             // FVP: both observation-half partials go to LDS whole (kh = 0 -> D0, kh = 1 ->
             // D0B) and P2 folds them while it loads its operand: no fold phase.  The
             // cached activations of this wave's rows go into the a0 / a1 images.
-            float* dst = kh ? D0B : P1A;
+            float* dst = kh ? D0B : D0;
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -698,16 +644,9 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
             __syncthreads();
             KX_STAMP(2);
         }
-        }
 
         // ---- P2: layer 1, wave -> (rb = kh, cb) ----
         {
-            half8 nxh[PIPE ? p1_part(KS, 1) - p1_part(KS, 0) : 1][2], nxl[PIPE ? p1_part(KS, 1) - p1_part(KS, 0) : 1][2];
-            if constexpr (PIPE) {
-#pragma unroll
-                for (int s = p1_part(KS, 0); s < p1_part(KS, 1); ++s)
-                    p1n_load(tile, s, lq, lr16, nxh[s - p1_part(KS, 0)], nxl[s - p1_part(KS, 0)]);
-            }
             const int j = cb * 16 + lr16;
             floatx4 acc = zero4();
             float rinv = 1.f;
@@ -717,13 +656,12 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
                 half8 xh[2], xl[2], ah[2], al[2];
                 float8v dv[2];
                 float mx = 0.f;
-                const float us = PIPE ? Us[kh * 16 + lr16] : 1.f;   // PIPE: the row scale here
 #pragma unroll
                 for (int s = 0; s < 2; ++s) {
                     arow(A0i, kh, s, lq, lr16, xh[s], xl[s]);
                     const int o = (kh * 16 + lr16) * L::LD + 32 * s + 8 * lq;
                     const float8v av = hilo8(xh[s], xl[s]) * AHR_INV;
-                    dv[s] = (load8(P1A + o) + load8(D0B + o)) * us * (1.f - av * av);   // W1c column scale folded in P1
+                    dv[s] = (load8(D0 + o) + load8(D0B + o)) * (1.f - av * av);   // W1c column scale folded in P1
                     mx = fmaxf(mx, absmax8(dv[s]));
                 }
                 const float sc = pow2_scale(max_over_groups(mx), rinv);
@@ -770,24 +708,11 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
                 }
             }
             if (MODE != FVP) astore4(A1i, j, kh * 16 + 4 * lq, av);
-            if constexpr (PIPE) {
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int s = p1_part(KS, 0); s < p1_part(KS, 1); ++s)
-                    p1n_mfma(s, nxh[s - p1_part(KS, 0)], nxl[s - p1_part(KS, 0)]);
-            }
         }
         __syncthreads();
         KX_STAMP(3);
 
         // ---- P3: output layer [32 x MP], waves < 2 * MP/16 -> (rb3, cbo3) ----
-        constexpr int NP3 = PIPE ? p1_part(KS, 2) - p1_part(KS, 1) : 1;
-        half8 nxh3[NP3 > 0 ? NP3 : 1][2], nxl3[NP3 > 0 ? NP3 : 1][2];
-        if constexpr (PIPE) {
-#pragma unroll
-            for (int s = p1_part(KS, 1); s < p1_part(KS, 2); ++s)
-                p1n_load(tile, s, lq, lr16, nxh3[s - p1_part(KS, 1)], nxl3[s - p1_part(KS, 1)]);
-        }
         if (w < 2 * (MP / 16)) {
             floatx4 acc = zero4();
             if (MODE == FVP) {
@@ -841,12 +766,6 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
         if (MP == 16) {   // the padded k16..31 of the P4 operand
             for (int i = ltid; i < BT * 16; i += KT) GPf[(i >> 4) * L::LDG + 16 + (i & 15)] = 0.f;
         }
-        if constexpr (PIPE) {
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int s = p1_part(KS, 1); s < p1_part(KS, 2); ++s)
-                p1n_mfma(s, nxh3[s - p1_part(KS, 1)], nxl3[s - p1_part(KS, 1)]);
-        }
         __syncthreads();
         KX_STAMP(4);
 
@@ -873,13 +792,6 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
         if (MODE == EVAL) continue;
 
         xload(tile + gridDim.x, ltid, 0, L::XPER / 2);   // first half of the next tile's xhat
-        constexpr int NP4 = PIPE ? p1_part(KS, 3) - p1_part(KS, 2) : 1;
-        half8 nxh4[NP4 > 0 ? NP4 : 1][2], nxl4[NP4 > 0 ? NP4 : 1][2];
-        if constexpr (PIPE) {
-#pragma unroll
-            for (int s = p1_part(KS, 2); s < p1_part(KS, 3); ++s)
-                p1n_load(tile, s, lq, lr16, nxh4[s - p1_part(KS, 2)], nxl4[s - p1_part(KS, 2)]);
-        }
         // ---- P4: gu1 = (1 - a1^2) (gp W2), wave -> (rb = kh, cb) ----
         {
             const int hcol = cb * 16 + lr16;
@@ -927,25 +839,12 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
             }
         };
         if (MODE == FVP) gw2_sum();
-        if constexpr (PIPE) {
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int s = p1_part(KS, 2); s < p1_part(KS, 3); ++s)
-                p1n_mfma(s, nxh4[s - p1_part(KS, 2)], nxl4[s - p1_part(KS, 2)]);
-        }
         __syncthreads();
         KX_STAMP(6);
         // ---- P5: gu0 = (1 - a0^2) (gu1 W1), times the xhat row scale; beside it the
         // gW1 / gW2 sums (their operands are complete since P4) and the next tile's
         // xhat loads (consumed at the next publish) ----
         xload(tile + gridDim.x, ltid, L::XPER / 2, L::XPER);
-        constexpr int NP5 = PIPE ? p1_part(KS, 4) - p1_part(KS, 3) : 1;
-        half8 nxh5[NP5 > 0 ? NP5 : 1][2], nxl5[NP5 > 0 ? NP5 : 1][2];
-        if constexpr (PIPE) {
-#pragma unroll
-            for (int s = p1_part(KS, 3); s < p1_part(KS, 4); ++s)
-                p1n_load(tile, s, lq, lr16, nxh5[s - p1_part(KS, 3)], nxl5[s - p1_part(KS, 3)]);
-        }
         auto p5_gu0 = [&]() __attribute__((always_inline)) {
             const int hcol = cb * 16 + lr16;
             half8 ah[2], al[2];
@@ -1000,18 +899,11 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
         p5_gu0();
         p5_gw();
         if (MODE != FVP) gw2_sum();
-        if constexpr (PIPE) {
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int s = p1_part(KS, 3); s < p1_part(KS, 4); ++s)
-                p1n_mfma(s, nxh5[s - p1_part(KS, 3)], nxl5[s - p1_part(KS, 3)]);
-        }
         __syncthreads();
         KX_STAMP(7);
 
         // ---- P6: the gW0 sums ----
         KX_STAMP(10);
-        if constexpr (PIPE) load_pa(tile + gridDim.x < ntiles ? tile + gridDim.x : tile, lq, lr16);
         {
             // gW0 (xhat transposed reads)
             half8 gh, gl;
@@ -1035,29 +927,6 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
                 if (g & 1) __builtin_amdgcn_sched_barrier(0);
             }
             KX_STAMP(12);
-        }
-        if constexpr (PIPE) {
-            // the last steps of the next tile's first layer, then its two observation-half
-            // partials (times wsc1; its row scale is applied in its P2) -> P1A (the GPf /
-            // GPT region, free since P4) and D0B
-#pragma unroll
-            for (int s = p1_part(KS, 4); s < KS; ++s) {
-                half8 nxh6[2], nxl6[2];
-                p1n_load(tile, s, lq, lr16, nxh6, nxl6);
-                p1n_mfma(s, nxh6, nxl6);
-            }
-            float* dst = kh ? D0B : P1A;
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-#pragma unroll
-                for (int rr = 0; rr < 4; ++rr)
-                    dst[(i * 16 + 4 * lq + rr) * L::LD + cb * 16 + lr16] = acc1n[i][rr] * wsc1;
-                acc1n[i] = zero4();
-            }
-            // the next tile's cached activations -> the a0 / a1 images (free since P5;
-            // loaded at the top of P6)
-            astore4(A0i, cb * 16 + lr16, kh * 16 + 4 * lq, pa0);
-            astore4(A1i, cb * 16 + lr16, kh * 16 + 4 * lq, pa1);
         }
         KX_STAMP(14);
         __syncthreads();

@@ -1146,7 +1146,6 @@ __global__ void __launch_bounds__(64) k_eval_final(const double* __restrict__ rp
 #include "fused.h"
 #include "ks.h"
 #include "kx.h"
-#include "kz.h"
 
 namespace {
 
@@ -1348,50 +1347,11 @@ int launch_kx_t(const RowArgs& ra, const FOut& fo, int grid, hipStream_t st) {
     return (int)hipGetLastError();
 }
 
-template <int MP, int KG>
-int launch_kz_t(const RowArgs& ra, const FOut& fo, int grid, hipStream_t st) {
-    using L = ZLayout<MP, KG>;
-    auto fn = k_kz<MP, KG>;
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, L::bytes);
-        if (e != hipSuccess) return (int)e;
-        attr = true;
-    }
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(ZT), L::bytes, st, ra, fo);
-    return (int)hipGetLastError();
-}
-
-#ifdef MJRL_KZ_ROLES_PROBE
-void kz_roles_probe() {   // -Rpass-analysis register counts of each role alone
-    hipLaunchKernelGGL((k_kz<32, 12, 1>), dim3(1), dim3(ZT), 0, 0, RowArgs{}, FOut{});
-    hipLaunchKernelGGL((k_kz<32, 12, 2>), dim3(1), dim3(ZT), 0, 0, RowArgs{}, FOut{});
-    hipLaunchKernelGGL((k_kz<32, 12, 4>), dim3(1), dim3(ZT), 0, 0, RowArgs{}, FOut{});
-}
-#endif
-
-// the FVP of split rows: k_kx's FVP mode, or the three-role pipeline k_kz (kz.h) with
-// MJRL_AMD_FVP=kz (read once per process; A/B runs)
-inline bool fvp_kx() {
-    static const bool v = [] {
-        const char* e = getenv("MJRL_AMD_FVP");
-        return !(e && e[0] == 'k' && e[1] == 'z' && e[2] == 0);
-    }();
-    return v;
-}
-
-// rows given as split-f16 (ra.xs) run the all-split kernel k_kx (FVP optionally
-// k_kz); f32 xhat the exact-f32 k_ks
+// rows given as split-f16 (ra.xs) run the all-split kernel k_kx; f32 xhat the
+// exact-f32 k_ks
 template <int MODE>
 int launch_ks(const mjrl_shape* s, const RowArgs& ra, const FOut& fo, int grid, hipStream_t st) {
     const int kg = s->np / 32;
-    if (ra.xs && MODE == FVP && !fvp_kx()) {
-#define MJRL_K(MP_, KG_) \
-    if (s->mp == MP_ && kg == KG_) return launch_kz_t<MP_, KG_>(ra, fo, grid, st);
-        MJRL_K(16, 4) MJRL_K(16, 8) MJRL_K(16, 12)
-        MJRL_K(32, 4) MJRL_K(32, 8) MJRL_K(32, 12)
-#undef MJRL_K
-    }
     if (ra.xs) {
 #define MJRL_K(MP_, KG_) \
     if (s->mp == MP_ && kg == KG_) return launch_kx_t<MP_, KG_, MODE>(ra, fo, grid, st);
@@ -1595,13 +1555,6 @@ int mjrl_debug_kx_prof(unsigned long long* out) {
     if (e != hipSuccess) return (int)e;
     unsigned long long z[KX_NPROF] = {0};
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_kx_prof), z, sizeof(z));
-}
-
-int mjrl_debug_kz_prof(unsigned long long* out) {
-    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_kz_prof), sizeof(unsigned long long) * KZ_NPROF);
-    if (e != hipSuccess) return (int)e;
-    unsigned long long z[KZ_NPROF] = {0};
-    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_kz_prof), z, sizeof(z));
 }
 #endif
 

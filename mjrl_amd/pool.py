@@ -113,23 +113,47 @@ def _segment_dtype(agent):
     return np.float32 if (f32 and dev_fit) else np.float64
 
 
-def _fill_shard(buf, L, sh, lengths):
+def _fill_shard(buf, L, sh, lengths, ex=None, chunk_rows=1 << 16):
     """The shard's paths `sh` into its segment.  float32 layouts: the native
     convert-and-range pass (engine.host_stage, the staging path's own) writes
-    obs / act and the per-column (min, max) of obs into 'orange'."""
-    if sh:
-        if L.dtype == np.float32:
-            from .engine import host_stage
-            offs = np.concatenate([[0], np.cumsum(lengths)])
-            rng = L.view(buf, "orange").reshape(2, L.n)
-            rng[0], rng[1] = np.inf, -np.inf
-            host_stage([p["observations"] for p in sh], L.view(buf, "obs").reshape(L.T, L.n), offs, 0, len(sh),
-                       rng[0], rng[1])
-            host_stage([p["actions"] for p in sh], L.view(buf, "act").reshape(L.T, L.m), offs, 0, len(sh))
+    obs / act and the per-column (min, max) of obs into 'orange'.  ex: a thread
+    pool; the paths are then cut into chunks of about chunk_rows timesteps,
+    converted in parallel (ctypes / numpy release the GIL), their ranges folded."""
+    lengths = np.asarray(lengths, dtype=np.int64)
+    offs = np.concatenate([[0], np.cumsum(lengths)])
+    bounds = [0]
+    for i in range(len(sh)):
+        if offs[i + 1] - offs[bounds[-1]] >= chunk_rows:
+            bounds.append(i + 1)
+    if bounds[-1] != len(sh):
+        bounds.append(len(sh))
+    nchunk = len(bounds) - 1
+    f32 = L.dtype == np.float32
+    rng = np.empty((max(nchunk, 1), 2, L.n), np.float32)
+    rng[:, 0], rng[:, 1] = np.inf, -np.inf
+    obs_v, act_v = L.view(buf, "obs").reshape(L.T, L.n), L.view(buf, "act").reshape(L.T, L.m)
+    if f32:
+        from .engine import host_stage
+
+    def conv(k):
+        a0, a1 = bounds[k], bounds[k + 1]
+        if f32:
+            host_stage([p["observations"] for p in sh], obs_v, offs, a0, a1, rng[k, 0], rng[k, 1])
+            host_stage([p["actions"] for p in sh], act_v, offs, a0, a1)
         else:
-            np.concatenate([np.asarray(p["observations"], np.float64).reshape(-1) for p in sh],
-                           out=L.view(buf, "obs"))
-            np.concatenate([np.asarray(p["actions"], np.float64).reshape(-1) for p in sh], out=L.view(buf, "act"))
+            for i in range(a0, a1):
+                obs_v[offs[i]:offs[i + 1]] = np.asarray(sh[i]["observations"], np.float64).reshape(-1, L.n)
+                act_v[offs[i]:offs[i + 1]] = np.asarray(sh[i]["actions"], np.float64).reshape(-1, L.m)
+
+    if ex is not None and nchunk > 1:
+        list(ex.map(conv, range(nchunk)))
+    else:
+        for k in range(nchunk):
+            conv(k)
+    if sh:
+        if f32:
+            o = L.view(buf, "orange").reshape(2, L.n)
+            o[0], o[1] = rng[:, 0].min(axis=0), rng[:, 1].max(axis=0)
         np.concatenate([np.asarray(p["rewards"], np.float64) for p in sh], out=L.view(buf, "rew"))
         if L.fields["adv_in"][1]:
             np.concatenate([np.asarray(p["advantages"], np.float64) for p in sh], out=L.view(buf, "adv_in"))
@@ -322,18 +346,20 @@ class DevicePool:
                              % (len(paths), self.world))
         with_adv = mode == "paths"
         dtype = _segment_dtype(agent)
-        import concurrent.futures as cf
-
-        def fill(r):
-            p0, p1 = parts[r]
-            L = _Layout(int(lengths[p0:p1].sum()), p1 - p0, n, m, with_adv, dtype)
-            _fill_shard(self._segment(r, L.nbytes).buf, L, paths[p0:p1], lengths[p0:p1])
-            return L
+        from .engine import _STAGING
 
         try:
+            t0 = time.perf_counter()
             state = self._state(agent)
-            with cf.ThreadPoolExecutor(self.world) as ex:
-                layouts = list(ex.map(fill, range(self.world)))
+            t1 = time.perf_counter()
+            layouts = []
+            for r in range(self.world):
+                # every shard's conversion spread over the staging thread pool
+                p0, p1 = parts[r]
+                L = _Layout(int(lengths[p0:p1].sum()), p1 - p0, n, m, with_adv, dtype)
+                _fill_shard(self._segment(r, L.nbytes).buf, L, paths[p0:p1], lengths[p0:p1], _STAGING.pool())
+                layouts.append(L)
+            t2 = time.perf_counter()
             rng = np.random.get_state()
             for r in range(self.world):
                 L = layouts[r]
@@ -342,9 +368,12 @@ class DevicePool:
                                                   fit=fit, return_errors=return_errors, rng=rng,
                                                   with_adv=with_adv)))
             replies = self._recv_all()
+            t3 = time.perf_counter()
         except BaseException:
             self._abort()
             raise
+        self.last_timing = dict(state_ms=(t1 - t0) * 1e3, fill_ms=(t2 - t1) * 1e3, workers_ms=(t3 - t2) * 1e3,
+                                worker_train_ms=[msg[1].get("train_ms") for msg in replies])
         if mode == "samples":
             for r in range(self.world):
                 p0, p1 = parts[r]
@@ -465,6 +494,7 @@ def _worker_main(args):
             agent._engine = engines.get(key)
             np.random.set_state(a["rng"])
             out = {}
+            tw = time.perf_counter()
             if a["mode"] == "samples":
                 stats = agent.train_from_samples(paths, a["gamma"], a["gae_lambda"])
                 for name, k in (("ret", "returns"), ("base", "baseline"), ("adv", "advantages")):
@@ -479,6 +509,7 @@ def _worker_main(args):
                     out["baseline"] = pickle.dumps(agent.baseline) if args.rank == 0 else None
             else:
                 stats = agent.train_from_paths(paths)
+            out["train_ms"] = (time.perf_counter() - tw) * 1e3
             engines[key] = agent._engine
             if args.rank == 0:
                 out.update(stats=[float(s) for s in stats], theta=agent.policy.get_param_values(),

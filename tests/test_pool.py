@@ -145,10 +145,13 @@ def test_fill_shard_layouts():
     from mjrl_amd.pool import _Layout, _fill_shard, _worker_paths
     paths = _adv_paths(5)
     lengths = np.array([len(p["rewards"]) for p in paths])
-    for dt in (np.float64, np.float32):
+    import concurrent.futures as cf
+    ex = cf.ThreadPoolExecutor(4)
+    for dt, kw in ((np.float64, {}), (np.float32, {}), (np.float64, dict(ex=ex, chunk_rows=20)),
+                   (np.float32, dict(ex=ex, chunk_rows=20))):   # one chunk / several chunks in parallel
         L = _Layout(int(lengths.sum()), len(paths), N_OBS, N_ACT, True, dt)
         buf = bytearray(L.nbytes)
-        _fill_shard(buf, L, paths, lengths)
+        _fill_shard(buf, L, paths, lengths, **kw)
         got = _worker_paths(L, buf)
         for p, q in zip(paths, got):
             assert q["observations"].dtype == dt

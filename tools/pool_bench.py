@@ -42,17 +42,23 @@ def main():
     agent.train_from_paths(paths)                    # pool start + first update
     first = time.perf_counter() - t0
     agent.train_from_paths(paths)                    # warm
-    ts = []
+    ts, timing = [], []
     for _ in range(args.reps):
         t0 = time.perf_counter()
         agent.train_from_paths(paths)
         ts.append(time.perf_counter() - t0)
+        if devices:
+            from mjrl_amd import pool
+            p = next(iter(pool._POOLS.values()))
+            timing.append({k: (round(v, 1) if isinstance(v, float) else [round(x, 1) for x in v])
+                           for k, v in p.last_timing.items()})
     T = args.paths * H
     dt = float(np.median(ts))
     print(json.dumps(dict(mode=args.mode, workers=len(devices) if devices else 1,
                           backend=os.environ.get("MJRL_AMD_POOL_BACKEND", "nccl") if devices else None,
                           timesteps=T, ms_per_update=round(dt * 1e3, 1), all_ms=[round(t * 1e3, 1) for t in ts],
-                          first_ms=round(first * 1e3, 1), timesteps_per_s=round(T / dt, 1))), flush=True)
+                          first_ms=round(first * 1e3, 1), timesteps_per_s=round(T / dt, 1),
+                          pool_timing=timing or None)), flush=True)
     if devices:
         from mjrl_amd import pool
         pool.close_pools()

@@ -17,53 +17,6 @@ namespace {
 constexpr int CG_THREADS = 1024;
 constexpr int CG_U = 8;   // elements per thread per chunk of a pass
 
-struct PackMap {
-    int n, m, h0, h1, np, mp;
-    Packed pk;
-    __host__ __device__ PackMap(const mjrl_shape& s)
-        : n(s.n), m(s.m), h0(s.h0), h1(s.h1), np(s.np), mp(s.mp), pk(s.h0, s.h1, s.np, s.mp) {}
-
-    // Packed positions of flat parameter f (second = transpose copy or -1);
-    // returns the log_std index j when f is a log-std entry, else -1.
-    __device__ int map(int f, int& p1, int& p2) const {
-        p2 = -1;
-        int g = f;
-        if (h0 == 0) {
-            if (g < m * n) { p1 = pk.W0 + (g / n) * np + g % n; return -1; }
-            if ((g -= m * n) < m) { p1 = pk.W0 + g * np + n; return -1; }
-            g -= m;
-            p1 = pk.ls + g;
-            return g;
-        }
-        if (g < h0 * n) { p1 = pk.W0 + (g / n) * np + g % n; return -1; }
-        if ((g -= h0 * n) < h0) { p1 = pk.W0 + g * np + n; return -1; }
-        if ((g -= h0) < h1 * h0) {
-            const int j = g / h0, k = g % h0;
-            p1 = pk.W1 + g;
-            p2 = pk.W1T + k * h1 + j;
-            return -1;
-        }
-        if ((g -= h1 * h0) < h1) { p1 = pk.b1 + g; return -1; }
-        if ((g -= h1) < m * h1) {
-            const int j = g / h1, k = g % h1;
-            p1 = pk.W2 + j * h1 + k;
-            p2 = pk.W2T + k * mp + j;
-            return -1;
-        }
-        if ((g -= m * h1) < m) { p1 = pk.b2 + g; return -1; }
-        g -= m;
-        p1 = pk.ls + g;
-        return g;
-    }
-};
-
-__device__ __forceinline__ void pack_one(const PackMap& pm, int f, float v, float* packed, bool clamp, float min_ls) {
-    int p1, p2;
-    const int j = pm.map(f, p1, p2);
-    if (j >= 0 && clamp) v = v < min_ls ? min_ls : v;   // torch.clamp(log_std, min) (gaussian_mlp.py:74-78)
-    packed[p1] = v;
-    if (p2 >= 0) packed[p2] = v;
-}
 
 __global__ void __launch_bounds__(256) k_pack(mjrl_shape s, const float* __restrict__ theta, float* __restrict__ packed,
                                               int clamp, float min_ls) {
@@ -487,6 +440,8 @@ __global__ void __launch_bounds__(CGM_T) k_cgm_init(mjrl_shape s, const float* _
         threadIdx.x == 0) {
         cg[0] = (float)t;   // rdotr
         cg[1] = 0.f;        // iterations run
+        reinterpret_cast<unsigned*>(cg)[10] = 0u;   // the one-launch CG solve's barrier counter
+        reinterpret_cast<unsigned*>(cg)[11] = 0u;   // and its error word (cgf.h)
         *done = 0;
     }
 }

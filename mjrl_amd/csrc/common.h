@@ -363,7 +363,7 @@ __device__ __forceinline__ float cg_logstd_curv(float log_std) {
 // (f32-rounded) gradient sum of f.  Writes z and this workgroup's partial of p.z
 // (cg[CG_PZ_PARTS + 2 blockIdx.x], a double); mjrl_cg_step_xr_p folds them.
 constexpr int CG_PZ_PARTS = 1024;   // float offset of the fused gather's p.z partials in the CG state
-__device__ __forceinline__ void cgz_epilogue(const CgZ& c, int f, int d, float gs) {
+__device__ __forceinline__ void cgz_epilogue(const CgZ& c, int f, int d, float gs, int slot = -1) {
     double pz = 0.0;
     if (f < d) {
         const float pf = c.p[f];
@@ -381,7 +381,7 @@ __device__ __forceinline__ void cgz_epilogue(const CgZ& c, int f, int d, float g
         pz = (double)pf * (double)zf;
     }
     pz = wave_sum(pz);
-    if ((threadIdx.x & 63) == 0) reinterpret_cast<double*>(c.cg + CG_PZ_PARTS)[blockIdx.x] = pz;
+    if ((threadIdx.x & 63) == 0) reinterpret_cast<double*>(c.cg + CG_PZ_PARTS)[slot < 0 ? (int)blockIdx.x : slot] = pz;
 }
 
 // Offsets (in floats) of the packed parameter set — see pack_params.
@@ -405,5 +405,55 @@ struct Packed {
         total = round_up(o, 4);
     }
 };
+
+// Packed positions of flat parameters (reference order W0, b0, W1, b1, W2, b2,
+// log_std; gaussian_mlp.py:61-64) in the padded / transposed packed set above.
+struct PackMap {
+    int n, m, h0, h1, np, mp;
+    Packed pk;
+    __host__ __device__ PackMap(const mjrl_shape& s)
+        : n(s.n), m(s.m), h0(s.h0), h1(s.h1), np(s.np), mp(s.mp), pk(s.h0, s.h1, s.np, s.mp) {}
+
+    // Packed positions of flat parameter f (second = transpose copy or -1);
+    // returns the log_std index j when f is a log-std entry, else -1.
+    __device__ int map(int f, int& p1, int& p2) const {
+        p2 = -1;
+        int g = f;
+        if (h0 == 0) {
+            if (g < m * n) { p1 = pk.W0 + (g / n) * np + g % n; return -1; }
+            if ((g -= m * n) < m) { p1 = pk.W0 + g * np + n; return -1; }
+            g -= m;
+            p1 = pk.ls + g;
+            return g;
+        }
+        if (g < h0 * n) { p1 = pk.W0 + (g / n) * np + g % n; return -1; }
+        if ((g -= h0 * n) < h0) { p1 = pk.W0 + g * np + n; return -1; }
+        if ((g -= h0) < h1 * h0) {
+            const int j = g / h0, k = g % h0;
+            p1 = pk.W1 + g;
+            p2 = pk.W1T + k * h1 + j;
+            return -1;
+        }
+        if ((g -= h1 * h0) < h1) { p1 = pk.b1 + g; return -1; }
+        if ((g -= h1) < m * h1) {
+            const int j = g / h1, k = g % h1;
+            p1 = pk.W2 + j * h1 + k;
+            p2 = pk.W2T + k * mp + j;
+            return -1;
+        }
+        if ((g -= m * h1) < m) { p1 = pk.b2 + g; return -1; }
+        g -= m;
+        p1 = pk.ls + g;
+        return g;
+    }
+};
+
+__device__ __forceinline__ void pack_one(const PackMap& pm, int f, float v, float* packed, bool clamp, float min_ls) {
+    int p1, p2;
+    const int j = pm.map(f, p1, p2);
+    if (j >= 0 && clamp) v = v < min_ls ? min_ls : v;   // torch.clamp(log_std, min) (gaussian_mlp.py:74-78)
+    packed[p1] = v;
+    if (p2 >= 0) packed[p2] = v;
+}
 
 }  // namespace mjrl

@@ -83,8 +83,10 @@ __device__ __forceinline__ void wgrad_lds(floatx4 (&acc)[NRW][NCW], const float*
     }
 }
 
+// The body of k_fused: this workgroup's tiles (blockIdx.x + k gridDim.x), then its
+// slab.  Also run once per CG iteration by the one-launch CG solve (cgf.h).
 template <int H0, int H1, int MP, int NCH, int MODE>
-__global__ void __launch_bounds__(FT, 1) k_fused(RowArgs a, FOut o) {
+__device__ __forceinline__ void fused_body(const RowArgs& a, const FOut& o) {
     using L = FLayout<H0, H1, MP>;
     constexpr int BT = L::BT, RB = 4, KC = L::KC;
     using S1 = Split8<RB, H0 / 16>;
@@ -446,6 +448,11 @@ __global__ void __launch_bounds__(FT, 1) k_fused(RowArgs a, FOut o) {
         __syncthreads();
         row_pass_final<MODE, MP, FT>(racc0, racc1, reinterpret_cast<double*>(smem), a.rpart, blk, tid);
     }
+}
+
+template <int H0, int H1, int MP, int NCH, int MODE>
+__global__ void __launch_bounds__(FT, 1) k_fused(RowArgs a, FOut o) {
+    fused_body<H0, H1, MP, NCH, MODE>(a, o);
 }
 
 }  // namespace

@@ -324,23 +324,6 @@ int mjrl_cg_step_xr_p(const mjrl_shape* s, float* x, const float* r, float* r_ou
                       const float* z, float* packed_p, float* cg, int32_t* done, float residual_tol,
                       void* stream);
 
-/* The whole CG solve in ONE launch for the shapes of the fused accumulate path
- * (mjrl_fused_path == 1: hidden 32 / 64, small observations; replaces, in one
- * process, the loop of cg_solve.py:9-20 over mjrl_fvp_accumulate +
- * mjrl_gather_cg_z + mjrl_cg_step_xr_p, npg_cg.py:55-74 / 122-125): iters
- * iterations (fewer after the residual_tol break) of FVP over the T rows, the
- * slab fold with the z step, and the iteration tail, the workgroups meeting at
- * grid barriers; bit-identical to that loop (r alternates r -> r2 -> r ..., as the
- * caller alternates r / r_out there).  After mjrl_cg_init (which zeroes the
- * barrier word cg[10] and the error word cg[11]).  The grid must be co-resident:
- * MJRL_ESHAPE when the shape / batch is not on the fused path or the occupancy
- * times the CUs is below the grid (use the loop); a barrier that cannot complete
- * (~0.1 s) sets cg[11] != 0 and the results are invalid — the caller checks it. */
-int mjrl_cg_solve_fused(const mjrl_shape* s, const mjrl_rows* rows, int64_t T, const float* packed_theta,
-                        float* packed_p, const float* out_scale, const mjrl_scratch* sc, float* x, float* r,
-                        float* r2, float* p, float* z, float* cg, int32_t* done, double inv_T, float damping,
-                        float residual_tol, int32_t iters, void* stream);
-
 /* The z step of that iteration from an all-reduced gradient sum (the sharded
  * path: gather, all-reduce of gsum, then this, then mjrl_cg_step_xr_p): z and the
  * per-64-parameter p.z partials exactly as mjrl_gather_cg_z writes them, so one

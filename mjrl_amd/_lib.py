@@ -80,8 +80,6 @@ SIGNATURES = {
     "mjrl_cg_init": [SP, P, P, P, P, P, P, P, P],
     "mjrl_cg_step": [SP, P, F64, F32, P, P, P, P, P, P, P, P, F32, P],
     "mjrl_gather_cg_z": [SP, C.POINTER(Rows), I64, C.POINTER(Scratch), P, P, F64, F32, P, P, P, P, P],
-    "mjrl_cg_solve_fused": [SP, C.POINTER(Rows), I64, P, P, P, C.POINTER(Scratch), P, P, P, P, P, P, P, F64, F32, F32,
-                            I32, P],
     "mjrl_cg_step_xr_p": [SP, P, P, P, P, P, P, P, P, F32, P],
     "mjrl_cg_z": [SP, P, F64, F32, P, P, P, P, P, P],
     "mjrl_cg_step1": [SP, P, F64, F32, P, P, P, P, P, P, P, P, P, F32, P],

@@ -440,8 +440,6 @@ __global__ void __launch_bounds__(CGM_T) k_cgm_init(mjrl_shape s, const float* _
         threadIdx.x == 0) {
         cg[0] = (float)t;   // rdotr
         cg[1] = 0.f;        // iterations run
-        reinterpret_cast<unsigned*>(cg)[10] = 0u;   // the one-launch CG solve's barrier counter
-        reinterpret_cast<unsigned*>(cg)[11] = 0u;   // and its error word (cgf.h)
         *done = 0;
     }
 }

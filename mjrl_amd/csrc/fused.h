@@ -84,7 +84,7 @@ __device__ __forceinline__ void wgrad_lds(floatx4 (&acc)[NRW][NCW], const float*
 }
 
 // The body of k_fused: this workgroup's tiles (blockIdx.x + k gridDim.x), then its
-// slab.  Also run once per CG iteration by the one-launch CG solve (cgf.h).
+// slab.
 template <int H0, int H1, int MP, int NCH, int MODE>
 __device__ __forceinline__ void fused_body(const RowArgs& a, const FOut& o) {
     using L = FLayout<H0, H1, MP>;

@@ -1146,7 +1146,6 @@ __global__ void __launch_bounds__(64) k_eval_final(const double* __restrict__ rp
 #include "fused.h"
 #include "ks.h"
 #include "kx.h"
-#include "cgf.h"
 
 namespace {
 
@@ -1401,32 +1400,6 @@ int launch_fused(const mjrl_shape* s, const RowArgs& ra, const FOut& fo, int gri
 #undef MJRL_FN
 #undef MJRL_F
     return MJRL_ESHAPE;
-}
-
-// the one-launch CG solve (cgf.h): its grid must be co-resident, so the occupancy
-// of the kernel times the CUs bounds it (checked once per instance and device)
-template <int H, int MP, int NCH>
-int launch_cgf_t(const RowArgs& ra, const FOut& fo, const CgfArgs& ca, int grid, hipStream_t st) {
-    using L = FLayout<H, H, MP>;
-    auto fn = k_cg_fused<H, H, MP, NCH>;
-    static int cap_dev = -1, cap = 0;
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return (int)e;
-    if (cap_dev != dev) {
-        e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, L::bytes);
-        if (e != hipSuccess) return (int)e;
-        int nb = 0, cus = 0;
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)fn, FT, L::bytes);
-        if (e != hipSuccess) return (int)e;
-        e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (e != hipSuccess) return (int)e;
-        cap = nb * cus;
-        cap_dev = dev;
-    }
-    if (grid > cap) return MJRL_ESHAPE;
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(FT), L::bytes, st, ra, fo, ca);
-    return (int)hipGetLastError();
 }
 
 int run_fused(int mode, const mjrl_shape* s, const mjrl_rows* r, int64_t T, const RowArgs& ra,
@@ -1693,53 +1666,6 @@ int mjrl_gather_cg_z(const mjrl_shape* s, const mjrl_rows* rows, int64_t T, cons
     const Packed pk(s->h0, s->h1, s->np, s->mp);
     CgZ cz{p, z, cg, packed_theta + pk.ls, inv_T, damping, s->d - s->m};
     return run_gather(s, rows, T, sc, nullptr, done, gsum, (hipStream_t)stream, cz);
-}
-
-int mjrl_cg_solve_fused(const mjrl_shape* s, const mjrl_rows* rows, int64_t T, const float* packed_theta,
-                        float* packed_p, const float* out_scale, const mjrl_scratch* sc, float* x, float* r, float* r2,
-                        float* p, float* z, float* cg, int32_t* done, double inv_T, float damping, float residual_tol,
-                        int32_t iters, void* stream) {
-    if (!rows_ok(s, rows) || !packed_theta || !packed_p || !sc || !x || !r || !r2 || r == r2 || !p || !z || !cg ||
-        !done || T <= 0 || T > rows->T || iters < 0)
-        return MJRL_EINVAL;
-    if (!shape_supported(s->h0, s->h1, s->mp) || acc_path(s, T) != 1) return MJRL_ESHAPE;
-    const int nch = (s->d + 63) / 64;
-    if (nch > (MJRL_CG_STATE - CG_PZ_PARTS) / 2) return MJRL_EINVAL;   // partials beyond the CG state
-    const int G = fused_grid(T);
-    if (G > sc->slices) return MJRL_EINVAL;
-    RowArgs ra = row_args(s, rows, T);
-    ra.P = packed_theta;
-    ra.V = packed_p;
-    ra.out_scale = out_scale;
-    ra.done = nullptr;
-    FOut fo{};
-    fo.wpart = sc->wpart;
-    fo.n = s->n;
-    fo.m = s->m;
-    fo.wcap = slab_floats(s, sc->slices);
-    const Packed pk(s->h0, s->h1, s->np, s->mp);
-    CgfArgs ca{};
-    ca.cz = CgZ{p, z, cg, packed_theta + pk.ls, inv_T, damping, s->d - s->m};
-    ca.x = x;
-    ca.r0 = r;
-    ca.r1 = r2;
-    ca.packed_p = packed_p;
-    ca.done = done;
-    ca.tol = residual_tol;
-    ca.iters = iters;
-    ca.d = s->d;
-    ca.d_mu = s->d - s->m;
-    ca.nch = nch;
-    ca.s = *s;
-    hipStream_t st = (hipStream_t)stream;
-    // observations up to 63 features (one 64-column chunk): wider rows keep the
-    // per-iteration launches (their persistent instances spill VGPRs)
-    const int nc = (s->np + 63) / 64;
-#define MJRL_F(H_, MP_) \
-    if (s->h0 == H_ && s->mp == MP_ && nc == 1) return launch_cgf_t<H_, MP_, 1>(ra, fo, ca, G, st);
-    MJRL_F(64, 16) MJRL_F(64, 32) MJRL_F(32, 16) MJRL_F(32, 32)
-#undef MJRL_F
-    return MJRL_ESHAPE;
 }
 
 int mjrl_fused_path(const mjrl_shape* s) { return s ? acc_path(s, 1) : 0; }

@@ -446,9 +446,6 @@ class DeviceBatch:
         return b
 
 
-# the whole CG solve of the fused-path shapes in one launch (mjrl_cg_solve_fused);
-# MJRL_AMD_CG_FUSED=0 keeps the per-iteration launches (A/B)
-CG_FUSED_SOLVE = os.environ.get("MJRL_AMD_CG_FUSED", "0") == "1"
 GRAPH_AUTO_ROWS = 300_000   # UpdateEngine.graphs == "auto": replay graphs up to this many rows (125k-row shard: 2.03 -> 1.97 ms; 1M rows: eager 4 % faster)
 HIDDEN_WIDTHS = (32, 64, 128, 256)   # hidden widths the row kernels are built for
 
@@ -938,23 +935,7 @@ class UpdateEngine:
                 # state holds one p.z partial per 64 parameters
                 cg_zx = (s.d + 63) // 64 <= (_lib.CG_STATE - _lib.CG_PZ_PARTS) // 2
                 fuse_cg = not sharded and cg_zx
-                n_iter = int(cg_iters)
-                # the whole solve in one launch (the k_fused shapes, one process, all rows;
-                # per-FVP timing events need the per-iteration launches)
-                if fuse_cg and sub is None and prof is None and L.mjrl_fused_path(sp) == 1 and CG_FUSED_SOLVE:
-                    rc = L.mjrl_cg_solve_fused(sp, C.byref(rows_fvp), T, _lib.ptr(self.packed_theta),
-                                               _lib.ptr(self.packed_p), _lib.ptr(osc), C.byref(sc_fvp),
-                                               _lib.ptr(v["x"]), _lib.ptr(v["r"]), _lib.ptr(v["r2"]), _lib.ptr(v["p"]),
-                                               _lib.ptr(v["z"]), _lib.ptr(self.cg), _lib.ptr(self.done), inv_T_fvp,
-                                               float(damping), float(residual_tol), int(cg_iters), st)
-                    if rc == 0:
-                        n_iter = 0   # done: skip the loop below
-                    elif rc != _lib.MJRL_ESHAPE:
-                        _lib.check(rc, "mjrl_cg_solve_fused")
-                # sharded: gather -> all-reduce -> mjrl_cg_z -> mjrl_cg_step_xr_p (the one-launch
-                # mjrl_cg_step1, which forms z over all of d in every workgroup, only past the
-                # CG state's p.z partial capacity)
-                for k in range(n_iter):
+                for k in range(int(cg_iters)):
                     rows_k, sc_k, T_k = rows_fvp, sc_fvp, T
                     if sub is not None:
                         rows_k, sc_k, T_k = self._subsample_rows(sub, k, adv_vpg)
@@ -1163,14 +1144,11 @@ class UpdateEngine:
         if h is None:
             h = self._host_res = (torch.empty(N_STATS, dtype=torch.float64, pin_memory=True),
                                   torch.empty(8, dtype=torch.float32, pin_memory=True),
-                                  torch.empty(12, dtype=torch.float32, pin_memory=True))
+                                  torch.empty(8, dtype=torch.float32, pin_memory=True))
         h[0].copy_(self.stats, non_blocking=True)
         h[1].copy_(self.out[:8], non_blocking=True)
-        h[2].copy_(self.cg[:12], non_blocking=True)
+        h[2].copy_(self.cg[:8], non_blocking=True)
         torch.cuda.current_stream(self.device).synchronize()
-        if h[2][11:12].view(torch.int32).item() != 0:
-            raise _lib.MjrlError("mjrl_cg_solve_fused: a grid barrier timed out (the grid was not co-resident); "
-                                 "results invalid.  Set MJRL_AMD_CG_FUSED=0 to use the per-iteration launches")
         return h[0].numpy().copy(), h[1].numpy().copy(), h[2].numpy().copy()
 
     @_on_device

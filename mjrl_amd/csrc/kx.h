@@ -935,15 +935,18 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
 
     // slabs in the flat, parameter-chunk-major layout wpart[f / 64][S][64] (f = the
     // reference's flat parameter index, S = gridDim.x): k_gather_flat then reads
-    // every chunk as one contiguous run
+    // every chunk as one contiguous run.  The values are staged in LDS in flat
+    // parameter order first (the tile loop's buffers are free) and leave in 16-byte
+    // stores, each chunk's 256 bytes from 16 lanes: ~15 wide stores per thread
+    // instead of ~60 scattered 4-byte ones (the scattered tail took 15.8k cycles per
+    // FVP launch, profiles/r04f/kx_phase_profile_125k.txt)
     const int64_t blk = blockIdx.x;
     if constexpr (GRAD) {
         const int n = o.n, mm = o.m;
         const int64_t S = gridDim.x;
-        auto put = [&](int f, float v) {
-            MJRL_SLAB_CHECK((((int64_t)(f >> 6)) * S + blk) * 64 + (f & 63), o.wcap);
-            o.wpart[(((int64_t)(f >> 6)) * S + blk) * 64 + (f & 63)] = v;
-        };
+        float* slab = smem;   // [d_mu] in flat parameter order
+        static_assert(H * NP + H + H * H + H + MP * H + MP <= L::bytes / 4, "slab staging in LDS");
+        auto put = [&](int f, float v) { slab[f] = v; };
         const int fb0 = H * n, fW1 = fb0 + H, fb1 = fW1 + H * H, fW2 = fb1 + H, fb2 = fW2 + mm * H;
 #pragma unroll
         for (int g = 0; g < KG; ++g) {
@@ -972,6 +975,20 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
         if (kh == 0 && q == 0) put(fb1 + cb * 16 + r16, b1acc);
         if ((w >> 2) < MP / 16 && (w & 3) == 0 && q == 0 && (w >> 2) * 16 + r16 < mm)
             put(fb2 + (w >> 2) * 16 + r16, b2acc);
+        __syncthreads();
+        const int dmu = fb2 + mm;
+        for (int f0 = 4 * tid; f0 < dmu; f0 += 4 * KT) {
+            const int64_t gi = (((int64_t)(f0 >> 6)) * S + blk) * 64 + (f0 & 63);   // f0 % 4 == 0: one chunk
+            if (f0 + 3 < dmu) {
+                MJRL_SLAB_CHECK(gi + 3, o.wcap);
+                *reinterpret_cast<float4*>(o.wpart + gi) = *reinterpret_cast<const float4*>(slab + f0);
+            } else {
+                for (int e = 0; f0 + e < dmu; ++e) {
+                    MJRL_SLAB_CHECK(gi + e, o.wcap);
+                    o.wpart[gi + e] = slab[f0 + e];
+                }
+            }
+        }
     }
     if (MODE != FVP) {
         __syncthreads();

@@ -3,10 +3,33 @@
 // Everything here is written for CDNA4 directly: 64-lane waves, the exact-f32
 // MFMA `v_mfma_f32_16x16x4_f32`, LDS-staged operands.  No CUDA shims.
 #pragma once
+
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "../../include/mjrl_amd.h"
+
+#ifdef MJRL_KX_PROF
+// phase profile (profiling builds) of k_kx / k_fused: wave 0 of block 0 accumulates s_memtime cycles
+// between stamps in (wave-uniform, scalar) registers, written once at the end;
+// read with mjrl_debug_kx_prof
+constexpr int KX_NPROF = 24;   // 0-14 phases, 15 launch preamble, 16 tail (slab writes), 17 launches, 18-23 preamble parts
+__device__ unsigned long long g_kx_prof[KX_NPROF];
+#define KX_STAMP(i)                                                     \
+    do {                                                                \
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime();   \
+        kx_acc_[i] += now_ - kx_last_;                                  \
+        kx_last_ = now_;                                                \
+    } while (0)
+#define KX_PRE(i) kx_pre_[i] = __builtin_amdgcn_s_memtime()
+#else
+#define KX_PRE(i) \
+    do {          \
+    } while (0)
+#define KX_STAMP(i) \
+    do {            \
+    } while (0)
+#endif
 
 namespace mjrl {
 

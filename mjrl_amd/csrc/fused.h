@@ -35,20 +35,88 @@ struct Split8 {
     __device__ static int rb0(int w) { return CB >= 8 ? 0 : w / CB; }
 };
 
-template <int H0, int H1, int MP>
+// LDS: the tile's activations / upstreams, the xhat chunk buffer(s) (one when the
+// observations fit one 64-column chunk: the gW0 sums then reuse phase 1's chunk),
+// and — where they fit in the 160 KB — row-major images of W1 and W2 (and the
+// tangent's in FVP mode; phases 4 / 5 read them transposed for W2^T / W1^T) and of
+// the first layer's W0 (one chunk), loaded once per launch: every phase's weight
+// operand is then an LDS read instead of an L2 round trip on the tile's critical path.
+template <int H0, int H1, int MP, int NCH, int MODE>
 struct FLayout {
     static constexpr int BT = 64;
     static constexpr int LD0 = H0 + 4, LD1 = H1 + 4, LDP = MP + 4, KC = 64, LDX = KC + 4;
+    static constexpr int LW0 = KC + 4, LW1 = H0 + 4, LW2 = H1 + 4;
+    static constexpr int NV = MODE == FVP ? 2 : 1;   // P's images (+ the tangent's)
     static constexpr int oD0 = 0;
     static constexpr int oA0 = oD0 + BT * LD0;
     static constexpr int oD1 = oA0 + BT * LD0;
     static constexpr int oA1 = oD1 + BT * LD1;
     static constexpr int oGP = oA1 + BT * LD1;
     static constexpr int oXS = oGP + BT * LDP;
-    static constexpr int total = oXS + 2 * BT * LDX;
+    static constexpr int oW1 = oXS + (NCH == 1 ? 1 : 2) * BT * LDX;
+    static constexpr int oW1V = oW1 + H1 * LW1;
+    static constexpr int oW2 = oW1 + NV * H1 * LW1;
+    static constexpr int oW2V = oW2 + MP * LW2;
+    static constexpr int oW0 = oW2 + NV * MP * LW2;
+    static constexpr int LDS_CAP = 160 * 1024 / 4;
+    static constexpr bool IMG = oW0 <= LDS_CAP;
+    static constexpr bool IMG0 = IMG && NCH == 1 && oW0 + H0 * LW0 <= LDS_CAP;
+    static constexpr int total = IMG0 ? oW0 + H0 * LW0 : (IMG ? oW0 : oW1);
     static constexpr int bytes = total * 4;
     static_assert(LD0 >= MP, "log-std scratch lives in D0");
+    static_assert(total <= LDS_CAP, "LDS");
 };
+
+// A [ROWS][COLS] row-major weight block (global, row stride ld_src) to an LDS image
+// (row stride ld_dst): all of a thread's 16-byte loads in flight before its stores.
+template <int ROWS, int COLS>
+struct ImgCopy {
+    static constexpr int N4 = ROWS * COLS / 4, IT = (N4 + FT - 1) / FT;
+    static_assert(COLS % 4 == 0, "16-byte rows");
+    float4 v[IT];
+    __device__ __forceinline__ void load(const float* __restrict__ src, int ld_src, int col_lim, int tid) {
+#pragma unroll
+        for (int u = 0; u < IT; ++u) {
+            const int idx = tid + u * FT;
+            const int row = idx / (COLS / 4), c = (idx % (COLS / 4)) * 4;
+            v[u] = (idx < N4 && c < col_lim) ? *reinterpret_cast<const float4*>(src + row * ld_src + c)
+                                             : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+    __device__ __forceinline__ void store(float* dst, int ld_dst, int tid) const {
+#pragma unroll
+        for (int u = 0; u < IT; ++u) {
+            const int idx = tid + u * FT;
+            if (idx < N4) *reinterpret_cast<float4*>(dst + (idx / (COLS / 4)) * ld_dst + (idx % (COLS / 4)) * 4) = v[u];
+        }
+    }
+};
+
+// gemm_tile with the weight operand read TRANSPOSED from a row-major LDS image:
+// acc[i][j] += sum_k A[rows of rb(i)][k] * Wt[k][cols of cb(j)], k in [0, ke).
+template <int NRW, int NCW>
+__device__ __forceinline__ void gemm_tile_t(floatx4 (&acc)[NRW][NCW], const float* As, int lda, int rb0, int rbs,
+                                            int rb_lim, const float* Wt, int ldt, int cb0, int cbs, int ke,
+                                            int lane) {
+    const int r = lane & 15, q = lane >> 4;
+#pragma unroll MJRL_GEMM_UNROLL
+    for (int k = 0; k < ke; k += 16) {
+        float4 b[NCW];
+#pragma unroll
+        for (int j = 0; j < NCW; ++j) {
+            const float* pb = Wt + (k + 4 * q) * ldt + (cb0 + j * cbs) * 16 + r;
+            b[j] = make_float4(pb[0], pb[ldt], pb[2 * ldt], pb[3 * ldt]);
+        }
+#pragma unroll
+        for (int i = 0; i < NRW; ++i) {
+            const int rb = rb0 + i * rbs;
+            if (rb >= rb_lim) continue;
+            const float4 a = *reinterpret_cast<const float4*>(As + (rb * 16 + r) * lda + k + 4 * q);
+#pragma unroll
+            for (int j = 0; j < NCW; ++j) acc[i][j] = mfma_k16(a, b[j], acc[i][j]);
+        }
+    }
+}
 
 struct FOut {
     float* wpart;
@@ -87,7 +155,7 @@ __device__ __forceinline__ void wgrad_lds(floatx4 (&acc)[NRW][NCW], const float*
 // slab.
 template <int H0, int H1, int MP, int NCH, int MODE>
 __device__ __forceinline__ void fused_body(const RowArgs& a, const FOut& o) {
-    using L = FLayout<H0, H1, MP>;
+    using L = FLayout<H0, H1, MP, NCH, MODE>;
     constexpr int BT = L::BT, RB = 4, KC = L::KC;
     using S1 = Split8<RB, H0 / 16>;
     using S2 = Split8<RB, H1 / 16>;
@@ -104,6 +172,12 @@ __device__ __forceinline__ void fused_body(const RowArgs& a, const FOut& o) {
     float* XS = smem + L::oXS;
 
     if (MODE == FVP && a.done && *a.done) return;
+#ifdef MJRL_KX_PROF
+    // phase profile (profiling builds, the k_kx counters): wave 0 of workgroup 0
+    unsigned long long kx_acc_[KX_NPROF] = {0};
+    unsigned long long kx_last_ = __builtin_amdgcn_s_memtime();
+    kx_acc_[17] = 1;
+#endif
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int r16 = lane & 15, q = lane >> 4;
     const int np = a.np, m = a.m;
@@ -147,36 +221,83 @@ __device__ __forceinline__ void fused_body(const RowArgs& a, const FOut& o) {
     };
 
     bool pre = false;
+    // FVP: this lane's cached activations for epilogues 1 / 2 of a tile (the
+    // tile's first loads)
+    float pa0[S1::NRW][S1::NCW][4], pa1[S2::NRW][S2::NCW][4];
+    auto paload = [&](int64_t row_base) {
+        if (MODE != FVP) return;
+#pragma unroll
+        for (int i = 0; i < S1::NRW; ++i)
+#pragma unroll
+            for (int j = 0; j < S1::NCW; ++j)
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    const int rb = S1::rb0(w) + i * S1::RBS;
+                    const int64_t gr = row_base + rb * 16 + 4 * q + rr;
+                    const int col = (S1::cb0(w) + j * S1::CBS) * 16 + r16;
+                    pa0[i][j][rr] = (rb < RB && gr < T) ? a.a0[gr * H0 + col] : 0.f;
+                }
+#pragma unroll
+        for (int i = 0; i < S2::NRW; ++i)
+#pragma unroll
+            for (int j = 0; j < S2::NCW; ++j)
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    const int rb = S2::rb0(w) + i * S2::RBS;
+                    const int64_t gr = row_base + rb * 16 + 4 * q + rr;
+                    const int col = (S2::cb0(w) + j * S2::CBS) * 16 + r16;
+                    pa1[i][j][rr] = (rb < RB && gr < T) ? a.a1[gr * H1 + col] : 0.f;
+                }
+    };
+    // weight images (once per launch; the barrier is the first tile's)
+    const float* W0b = V + pk.W0;   // phase 1's weights (row stride np)
+    int ldw0 = np;
+    const float* W1p = P + pk.W1;   // phase 2 / 5 (row stride H0)
+    const float* W1v = V + pk.W1;
+    int ldw1 = H0;
+    const float* W2p = P + pk.W2;   // phase 3 / 4 (row stride H1)
+    const float* W2v = V + pk.W2;
+    int ldw2 = H1;
+    if constexpr (L::IMG) {
+        ImgCopy<H1, H0> c1, c1v;
+        ImgCopy<MP, H1> c2, c2v;
+        ImgCopy<H0, L::KC> c0;
+        c1.load(W1p, H0, H0, tid);
+        c2.load(W2p, H1, H1, tid);
+        if (MODE == FVP) {
+            c1v.load(W1v, H0, H0, tid);
+            c2v.load(W2v, H1, H1, tid);
+        }
+        if (L::IMG0) c0.load(W0b, np, np, tid);
+        if (blockIdx.x < ntiles) {   // the first tile's first chunk, in flight with the images
+            gload((int64_t)blockIdx.x * BT, 0);
+            pre = true;
+        }
+        c1.store(smem + L::oW1, L::LW1, tid);
+        c2.store(smem + L::oW2, L::LW2, tid);
+        if (MODE == FVP) {
+            c1v.store(smem + L::oW1V, L::LW1, tid);
+            c2v.store(smem + L::oW2V, L::LW2, tid);
+        }
+        if (L::IMG0) c0.store(smem + L::oW0, L::LW0, tid);
+        W1p = smem + L::oW1;
+        W1v = MODE == FVP ? smem + L::oW1V : W1p;
+        W2p = smem + L::oW2;
+        W2v = MODE == FVP ? smem + L::oW2V : W2p;
+        ldw1 = L::LW1;
+        ldw2 = L::LW2;
+        if (L::IMG0) {
+            W0b = smem + L::oW0;
+            ldw0 = L::LW0;
+        }
+    }
+
+    KX_STAMP(15);
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t row_base = tile * BT;
 
-        // FVP: this lane's cached activations for epilogues 1 / 2, fetched up front
-        float pa0[S1::NRW][S1::NCW][4], pa1[S2::NRW][S2::NCW][4];
-        if (MODE == FVP) {
-#pragma unroll
-            for (int i = 0; i < S1::NRW; ++i)
-#pragma unroll
-                for (int j = 0; j < S1::NCW; ++j)
-#pragma unroll
-                    for (int rr = 0; rr < 4; ++rr) {
-                        const int rb = S1::rb0(w) + i * S1::RBS;
-                        const int64_t gr = row_base + rb * 16 + 4 * q + rr;
-                        const int col = (S1::cb0(w) + j * S1::CBS) * 16 + r16;
-                        pa0[i][j][rr] = (rb < RB && gr < T) ? a.a0[gr * H0 + col] : 0.f;
-                    }
-#pragma unroll
-            for (int i = 0; i < S2::NRW; ++i)
-#pragma unroll
-                for (int j = 0; j < S2::NCW; ++j)
-#pragma unroll
-                    for (int rr = 0; rr < 4; ++rr) {
-                        const int rb = S2::rb0(w) + i * S2::RBS;
-                        const int64_t gr = row_base + rb * 16 + 4 * q + rr;
-                        const int col = (S2::cb0(w) + j * S2::CBS) * 16 + r16;
-                        pa1[i][j][rr] = (rb < RB && gr < T) ? a.a1[gr * H1 + col] : 0.f;
-                    }
-        }
-
+        paload(row_base);
+        KX_STAMP(0);
         // ---------------- phase 1: [64 x H0] = xhat * W0^T (or dW0^T) ----------------
         floatx4 acc1[S1::NRW][S1::NCW];
         zero_acc(acc1);
@@ -189,9 +310,9 @@ __device__ __forceinline__ void fused_body(const RowArgs& a, const FOut& o) {
             if (c + 1 < NCH) gload(row_base, c + 1);
             const int kb = c * KC;
             const int ke = kb + KC < np ? kb + KC : np;
-            gemm_tile(acc1, xs, L::LDX, kb, S1::rb0(w), S1::RBS, RB, V + pk.W0, np, S1::cb0(w), S1::CBS, kb, ke,
-                      lane);
+            gemm_tile(acc1, xs, L::LDX, kb, S1::rb0(w), S1::RBS, RB, W0b, ldw0, S1::cb0(w), S1::CBS, kb, ke, lane);
         }
+        KX_STAMP(1);
         // epilogue 1
 #pragma unroll
         for (int i = 0; i < S1::NRW; ++i) {
@@ -218,19 +339,17 @@ __device__ __forceinline__ void fused_body(const RowArgs& a, const FOut& o) {
             }
         }
         __syncthreads();
+        KX_STAMP(2);
 
         // ---------------- phase 2: [64 x H1], K = H0 ----------------
         {
             floatx4 acc2[S2::NRW][S2::NCW];
             zero_acc(acc2);
             if (MODE == FVP) {
-                gemm_tile(acc2, D0, L::LD0, 0, S2::rb0(w), S2::RBS, RB, P + pk.W1, H0, S2::cb0(w), S2::CBS, 0, H0,
-                          lane);
-                gemm_tile(acc2, A0s, L::LD0, 0, S2::rb0(w), S2::RBS, RB, V + pk.W1, H0, S2::cb0(w), S2::CBS, 0,
-                          H0, lane);
+                gemm_tile(acc2, D0, L::LD0, 0, S2::rb0(w), S2::RBS, RB, W1p, ldw1, S2::cb0(w), S2::CBS, 0, H0, lane);
+                gemm_tile(acc2, A0s, L::LD0, 0, S2::rb0(w), S2::RBS, RB, W1v, ldw1, S2::cb0(w), S2::CBS, 0, H0, lane);
             } else {
-                gemm_tile(acc2, A0s, L::LD0, 0, S2::rb0(w), S2::RBS, RB, P + pk.W1, H0, S2::cb0(w), S2::CBS, 0, H0,
-                          lane);
+                gemm_tile(acc2, A0s, L::LD0, 0, S2::rb0(w), S2::RBS, RB, W1p, ldw1, S2::cb0(w), S2::CBS, 0, H0, lane);
             }
 #pragma unroll
             for (int i = 0; i < S2::NRW; ++i) {
@@ -259,19 +378,17 @@ __device__ __forceinline__ void fused_body(const RowArgs& a, const FOut& o) {
             }
         }
         __syncthreads();
+        KX_STAMP(3);
 
         // ---------------- phase 3: [64 x MP], K = H1 ----------------
         {
             floatx4 acc3[S3::NRW][S3::NCW];
             zero_acc(acc3);
             if (MODE == FVP) {
-                gemm_tile(acc3, D1, L::LD1, 0, S3::rb0(w), S3::RBS, RB, P + pk.W2, H1, S3::cb0(w), S3::CBS, 0, H1,
-                          lane);
-                gemm_tile(acc3, A1s, L::LD1, 0, S3::rb0(w), S3::RBS, RB, V + pk.W2, H1, S3::cb0(w), S3::CBS, 0,
-                          H1, lane);
+                gemm_tile(acc3, D1, L::LD1, 0, S3::rb0(w), S3::RBS, RB, W2p, ldw2, S3::cb0(w), S3::CBS, 0, H1, lane);
+                gemm_tile(acc3, A1s, L::LD1, 0, S3::rb0(w), S3::RBS, RB, W2v, ldw2, S3::cb0(w), S3::CBS, 0, H1, lane);
             } else {
-                gemm_tile(acc3, A1s, L::LD1, 0, S3::rb0(w), S3::RBS, RB, P + pk.W2, H1, S3::cb0(w), S3::CBS, 0, H1,
-                          lane);
+                gemm_tile(acc3, A1s, L::LD1, 0, S3::rb0(w), S3::RBS, RB, W2p, ldw2, S3::cb0(w), S3::CBS, 0, H1, lane);
             }
 #pragma unroll
             for (int i = 0; i < S3::NRW; ++i) {
@@ -302,6 +419,7 @@ __device__ __forceinline__ void fused_body(const RowArgs& a, const FOut& o) {
             }
         }
         __syncthreads();
+        KX_STAMP(4);
 
         // ---------------- FWD: log-likelihood, caches, VPG upstream ----------------
         if (MODE == FWD) {
@@ -309,12 +427,16 @@ __device__ __forceinline__ void fused_body(const RowArgs& a, const FOut& o) {
             __syncthreads();
         }
 
+        KX_STAMP(5);
         // ---------------- phase 4: gu1 = (1 - a1^2) (g W2) ----------------
         {
             floatx4 acc4[S2::NRW][S2::NCW];
             zero_acc(acc4);
-            gemm_tile(acc4, GPs, L::LDP, 0, S2::rb0(w), S2::RBS, RB, P + pk.W2T, MP, S2::cb0(w), S2::CBS, 0, MP,
-                      lane);
+            if constexpr (L::IMG)   // W2^T: the W2 image read transposed
+                gemm_tile_t(acc4, GPs, L::LDP, S2::rb0(w), S2::RBS, RB, W2p, ldw2, S2::cb0(w), S2::CBS, MP, lane);
+            else
+                gemm_tile(acc4, GPs, L::LDP, 0, S2::rb0(w), S2::RBS, RB, P + pk.W2T, MP, S2::cb0(w), S2::CBS, 0, MP,
+                          lane);
 #pragma unroll
             for (int i = 0; i < S2::NRW; ++i) {
                 const int rb = S2::rb0(w) + i * S2::RBS;
@@ -332,13 +454,17 @@ __device__ __forceinline__ void fused_body(const RowArgs& a, const FOut& o) {
             }
         }
         __syncthreads();
+        KX_STAMP(6);
 
         // ---------------- phase 5: gu0 = (1 - a0^2) (gu1 W1) ----------------
         {
             floatx4 acc5[S1::NRW][S1::NCW];
             zero_acc(acc5);
-            gemm_tile(acc5, D1, L::LD1, 0, S1::rb0(w), S1::RBS, RB, P + pk.W1T, H1, S1::cb0(w), S1::CBS, 0, H1,
-                      lane);
+            if constexpr (L::IMG)   // W1^T: the W1 image read transposed
+                gemm_tile_t(acc5, D1, L::LD1, S1::rb0(w), S1::RBS, RB, W1p, ldw1, S1::cb0(w), S1::CBS, H1, lane);
+            else
+                gemm_tile(acc5, D1, L::LD1, 0, S1::rb0(w), S1::RBS, RB, P + pk.W1T, H1, S1::cb0(w), S1::CBS, 0, H1,
+                          lane);
 #pragma unroll
             for (int i = 0; i < S1::NRW; ++i) {
                 const int rb = S1::rb0(w) + i * S1::RBS;
@@ -356,12 +482,14 @@ __device__ __forceinline__ void fused_body(const RowArgs& a, const FOut& o) {
             }
         }
         __syncthreads();
+        KX_STAMP(7);
 
         // ---------------- weight gradients, accumulated in registers ----------------
         wgrad_lds(g2, GPs, L::LDP, A1s, L::LD1, W2S::rb0(w), W2S::RBS, MP / 16, W2S::cb0(w), W2S::CBS, H1 / 16,
                   lane);
         wgrad_lds(g1, D1, L::LD1, A0s, L::LD0, W1S::rb0(w), W1S::RBS, H1 / 16, W1S::cb0(w), W1S::CBS, H0 / 16,
                   lane);
+        KX_STAMP(8);
         if (tid < H1) {
             float s = 0.f;
             for (int row = 0; row < BT; ++row) s += D1[row * L::LD1 + tid];
@@ -371,40 +499,58 @@ __device__ __forceinline__ void fused_body(const RowArgs& a, const FOut& o) {
             for (int row = 0; row < BT; ++row) s += GPs[row * L::LDP + tid - H1];
             b2acc += s;
         }
+        KX_STAMP(9);
         // gW0 += gu0^T xhat: re-stream the tile's chunks (L2-hot); the last chunk
         // prefetches the next tile's first chunk
         const int64_t next = tile + gridDim.x;
-        gload(row_base, 0);
+        if constexpr (NCH == 1) {
+            // the tile's only chunk is still in XS (phase 1's): no re-stream
+            if (next < ntiles) gload(next * BT, 0);
+            const int kb_lim = np / 16 < KC / 16 ? np / 16 : KC / 16;
+            wgrad_lds(g0[0], D0, L::LD0, XS, L::LDX, W0S::rb0(w), W0S::RBS, H0 / 16, W0S::cb0(w), W0S::CBS, kb_lim,
+                      lane);
+        } else {
+            gload(row_base, 0);
 #pragma unroll
-        for (int c = 0; c < NCH; ++c) {
-            float* xs = XS + (c & 1) * BT * L::LDX;
-            lstore(xs);
-            __syncthreads();
-            if (c + 1 < NCH) {
-                gload(row_base, c + 1);
-            } else if (next < ntiles) {
-                gload(next * BT, 0);
+            for (int c = 0; c < NCH; ++c) {
+                float* xs = XS + (c & 1) * BT * L::LDX;
+                lstore(xs);
+                __syncthreads();
+                if (c + 1 < NCH) {
+                    gload(row_base, c + 1);
+                } else if (next < ntiles) {
+                    gload(next * BT, 0);
+                }
+                const int kb_lim = (np - c * KC) / 16 < KC / 16 ? (np - c * KC) / 16 : KC / 16;
+                wgrad_lds(g0[c], D0, L::LD0, xs, L::LDX, W0S::rb0(w), W0S::RBS, H0 / 16, W0S::cb0(w), W0S::CBS,
+                          kb_lim, lane);
             }
-            const int kb_lim = (np - c * KC) / 16 < KC / 16 ? (np - c * KC) / 16 : KC / 16;
-            wgrad_lds(g0[c], D0, L::LD0, xs, L::LDX, W0S::rb0(w), W0S::RBS, H0 / 16, W0S::cb0(w), W0S::CBS,
-                      kb_lim, lane);
         }
         pre = next < ntiles;
         __syncthreads();
+        KX_STAMP(10);
     }
 
     // ---------------- this workgroup's slab (slice = blockIdx.x) in the flat,
     // parameter-chunk-major layout wpart[f / 64][S][64] (k_gather_flat): flat parameter
     // f in the reference order W0, b0, W1, b1, W2, b2 (gaussian_mlp.py:61-64); padded
-    // columns / rows are not stored ----------------
+    // columns / rows are not stored.  When the slab fits, it is staged in LDS in flat
+    // order (the tile buffers are free after the loop's last barrier) and leaves in
+    // 16-byte stores, as k_kx's does ----------------
     const int64_t blk = blockIdx.x;
     const int nobs = o.n, mact = o.m;
     const int fb0 = H0 * nobs, fW1 = fb0 + H0, fb1 = fW1 + H1 * H0, fW2 = fb1 + H1, fb2 = fW2 + mact * H1;
+    const int dmu = fb2 + mact;
+    const bool stage = dmu <= L::total;
     float* wp = o.wpart + blk * 64;
     const int64_t cs = (int64_t)gridDim.x * 64;
     auto put = [&](int f, float v) {
-        MJRL_SLAB_CHECK(blk * 64 + (int64_t)(f >> 6) * cs + (f & 63), o.wcap);
-        wp[(int64_t)(f >> 6) * cs + (f & 63)] = v;
+        if (stage) {
+            smem[f] = v;
+        } else {
+            MJRL_SLAB_CHECK(blk * 64 + (int64_t)(f >> 6) * cs + (f & 63), o.wcap);
+            wp[(int64_t)(f >> 6) * cs + (f & 63)] = v;
+        }
     };
 #pragma unroll
     for (int c = 0; c < NCH; ++c)
@@ -443,11 +589,33 @@ __device__ __forceinline__ void fused_body(const RowArgs& a, const FOut& o) {
         put(fb1 + tid, b1acc);
     else if (tid < H1 + mact)
         put(fb2 + (tid - H1), b2acc);
+    KX_STAMP(11);
+    if (stage) {
+        __syncthreads();
+        KX_STAMP(12);
+        for (int f0 = 4 * tid; f0 < dmu; f0 += 4 * FT) {
+            const int64_t gi = ((int64_t)(f0 >> 6) * gridDim.x + blk) * 64 + (f0 & 63);   // f0 % 4 == 0: one chunk
+            if (f0 + 3 < dmu) {
+                MJRL_SLAB_CHECK(gi + 3, o.wcap);
+                *reinterpret_cast<float4*>(o.wpart + gi) = *reinterpret_cast<const float4*>(smem + f0);
+            } else {
+                for (int e = 0; f0 + e < dmu; ++e) {
+                    MJRL_SLAB_CHECK(gi + e, o.wcap);
+                    o.wpart[gi + e] = smem[f0 + e];
+                }
+            }
+        }
+    }
     if (MODE == FWD) {
         static_assert(L::total >= 2 * FT, "row_pass_final scratch");
         __syncthreads();
         row_pass_final<MODE, MP, FT>(racc0, racc1, reinterpret_cast<double*>(smem), a.rpart, blk, tid);
     }
+#ifdef MJRL_KX_PROF
+    KX_STAMP(16);
+    if (blockIdx.x == 0 && tid == 0)
+        for (int i = 0; i < KX_NPROF; ++i) g_kx_prof[i] += kx_acc_[i];
+#endif
 }
 
 template <int H0, int H1, int MP, int NCH, int MODE>

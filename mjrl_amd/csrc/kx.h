@@ -22,27 +22,6 @@
 // P2 (layer 1), P3 (output layer), P4 (gu1), P5 (gu0), weight-gradient sums.
 #pragma once
 
-#ifdef MJRL_KX_PROF
-// phase profile (debug builds): wave 0 of block 0 accumulates s_memtime cycles
-// between stamps in (wave-uniform, scalar) registers, written once at the end;
-// read with mjrl_debug_kx_prof
-constexpr int KX_NPROF = 24;   // 0-14 phases, 15 launch preamble, 16 tail (slab writes), 17 launches, 18-23 preamble parts
-__device__ unsigned long long g_kx_prof[KX_NPROF];
-#define KX_STAMP(i)                                                     \
-    do {                                                                \
-        const unsigned long long now_ = __builtin_amdgcn_s_memtime();   \
-        kx_acc_[i] += now_ - kx_last_;                                  \
-        kx_last_ = now_;                                                \
-    } while (0)
-#define KX_PRE(i) kx_pre_[i] = __builtin_amdgcn_s_memtime()
-#else
-#define KX_PRE(i) \
-    do {          \
-    } while (0)
-#define KX_STAMP(i) \
-    do {            \
-    } while (0)
-#endif
 
 namespace {
 

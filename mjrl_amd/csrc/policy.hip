@@ -1374,7 +1374,7 @@ int launch_ks(const mjrl_shape* s, const RowArgs& ra, const FOut& fo, int grid, 
 
 template <int H, int MP, int NCH, int MODE>
 int launch_fused_t(const RowArgs& ra, const FOut& fo, int grid, hipStream_t st) {
-    using L = FLayout<H, H, MP>;
+    using L = FLayout<H, H, MP, NCH, MODE>;
     auto fn = k_fused<H, H, MP, NCH, MODE>;
     static bool attr = false;
     if (!attr) {

@@ -274,25 +274,42 @@ __global__ void __launch_bounds__(CGX_T) k_cgm_xrp_f(mjrl_shape s, float* __rest
     __shared__ unsigned ticket;
     if (*done) return;
     const int d = s.d;
+    // every load that does not depend on v / mu is issued up front: this thread's own
+    // element (p, x, r, z) and the first XRP_PRE terms of the r.r fold
+    const int f = blockIdx.x * CGX_T + threadIdx.x;
+    const bool own = f < d;
+    const float pf = own ? p[f] : 0.f, xf = own ? x[f] : 0.f, rfo = own ? r[f] : 0.f, zfo = own ? z[f] : 0.f;
+    constexpr int XRP_PRE = 8;
+    float rpre[XRP_PRE], zpre[XRP_PRE];
+#pragma unroll
+    for (int u = 0; u < XRP_PRE; ++u) {
+        const int g = threadIdx.x + u * CGX_T;
+        rpre[u] = g < d ? r[g] : 0.f;
+        zpre[u] = g < d ? z[g] : 0.f;
+    }
+    const float rdotr = cg[0];
     const double* pzp = reinterpret_cast<const double*>(cg + CG_PZ_PARTS);
     double q = 0.0;
     for (int i = threadIdx.x; i < ng; i += CGX_T) q += pzp[i];
     const float pz = (float)block_sum<CGX_T>(q, red);
-    const float rdotr = cg[0];
     const float v = rdotr / pz;   // v = rdotr / p.z
-    double acc = 0.0;
+    double acc = 0.0;   // the fold of r.r in f order, as before: the prefetched terms first
+#pragma unroll
+    for (int u = 0; u < XRP_PRE; ++u)
+        if (threadIdx.x + u * CGX_T < d) {
+            const float rf = __fsub_rn(rpre[u], __fmul_rn(v, zpre[u]));
+            acc += (double)rf * (double)rf;
+        }
 #pragma unroll 8
-    for (int f = threadIdx.x; f < d; f += CGX_T) {
-        const float rf = __fsub_rn(r[f], __fmul_rn(v, z[f]));
+    for (int g = threadIdx.x + XRP_PRE * CGX_T; g < d; g += CGX_T) {
+        const float rf = __fsub_rn(r[g], __fmul_rn(v, z[g]));
         acc += (double)rf * (double)rf;
     }
     const float rr = (float)block_sum<CGX_T>(acc, red);
     const float mu = rr / rdotr;
-    const int f = blockIdx.x * CGX_T + threadIdx.x;
-    if (f < d) {
-        const float pf = p[f];
-        x[f] = __fadd_rn(x[f], __fmul_rn(v, pf));
-        const float rf = __fsub_rn(r[f], __fmul_rn(v, z[f]));
+    if (own) {
+        x[f] = __fadd_rn(xf, __fmul_rn(v, pf));
+        const float rf = __fsub_rn(rfo, __fmul_rn(v, zfo));
         r_out[f] = rf;
         if (!(rr < tol)) {   // converged: p is not used again
             const float pn = __fadd_rn(rf, __fmul_rn(mu, pf));

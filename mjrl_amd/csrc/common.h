@@ -386,13 +386,14 @@ __device__ __forceinline__ float cg_logstd_curv(float log_std) {
 // (f32-rounded) gradient sum of f.  Writes z and this workgroup's partial of p.z
 // (cg[CG_PZ_PARTS + 2 blockIdx.x], a double); mjrl_cg_step_xr_p folds them.
 constexpr int CG_PZ_PARTS = 1024;   // float offset of the fused gather's p.z partials in the CG state
-__device__ __forceinline__ void cgz_epilogue(const CgZ& c, int f, int d, float gs, int slot = -1) {
+// (pf, lsv: p[f] and, on the log-std block, log_std[f - ls0], loaded by the caller)
+__device__ __forceinline__ void cgz_epilogue(const CgZ& c, int f, int d, float gs, float pf, float lsv,
+                                             int slot = -1) {
     double pz = 0.0;
     if (f < d) {
-        const float pf = c.p[f];
         float hv;
         if (f >= c.ls0) {
-            const float sg = expf(c.ls[f - c.ls0]);
+            const float sg = expf(lsv);
             const double uu = (double)sg * (double)sg;
             const double cc = 4.0 * uu * (2.0 * uu - 1e-8) / ((2.0 * uu + 1e-8) * (2.0 * uu + 1e-8));
             hv = (float)(cc * (double)pf);
@@ -405,6 +406,15 @@ __device__ __forceinline__ void cgz_epilogue(const CgZ& c, int f, int d, float g
     }
     pz = wave_sum(pz);
     if ((threadIdx.x & 63) == 0) reinterpret_cast<double*>(c.cg + CG_PZ_PARTS)[slot < 0 ? (int)blockIdx.x : slot] = pz;
+}
+__device__ __forceinline__ void cgz_load(const CgZ& c, int f, int d, float& pf, float& lsv) {
+    pf = f < d ? c.p[f] : 0.f;
+    lsv = f < d && f >= c.ls0 ? c.ls[f - c.ls0] : 0.f;
+}
+__device__ __forceinline__ void cgz_epilogue(const CgZ& c, int f, int d, float gs, int slot = -1) {
+    float pf, lsv;
+    cgz_load(c, f, d, pf, lsv);
+    cgz_epilogue(c, f, d, gs, pf, lsv, slot);
 }
 
 // Offsets (in floats) of the packed parameter set — see pack_params.

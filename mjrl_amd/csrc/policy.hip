@@ -1092,6 +1092,8 @@ __global__ void __launch_bounds__(64 * GATHER_WAVES) k_gather_flat(const float* 
     __shared__ double part[GATHER_WAVES][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int f = blockIdx.x * 64 + lane;
+    float pf = 0.f, lsv = 0.f;   // the CG z step's operands, in flight with the slab loads
+    if (w == 0 && cz.p) cgz_load(cz, f, d, pf, lsv);
     double acc = 0.0;
     if (f < d_mu) {
         const int per = (S + GATHER_WAVES - 1) / GATHER_WAVES;
@@ -1122,7 +1124,7 @@ __global__ void __launch_bounds__(64 * GATHER_WAVES) k_gather_flat(const float* 
             gs = (float)t;
             gsum[f] = gs;
         }
-        if (cz.p) cgz_epilogue(cz, f, d, gs);
+        if (cz.p) cgz_epilogue(cz, f, d, gs, pf, lsv);
     }
 }
 

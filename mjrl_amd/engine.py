@@ -795,7 +795,8 @@ class UpdateEngine:
         the RNG is left where the reference's early-exiting CG would leave it.
         graph (default self.graphs): replay a captured hipGraph of the update when
         the batch, shape and arguments repeat (npg / vpg / dapg, one process, no
-        subsampled Fisher, no line search; see _maybe_capture).
+        subsampled Fisher; TRPO's line search continues on the host after the
+        replayed graph, which ends at the first evaluation; see _maybe_capture).
         Returns host scalars plus the new device theta (self.vec['theta_new'])."""
         L = self.lib
         s = self.shape
@@ -830,7 +831,7 @@ class UpdateEngine:
             # or collective-call overhead between the latency-bound steps)
             want = T_all <= GRAPH_AUTO_ROWS or sharded
         use_graph = (bool(want) and (self.comm.world_size == 1 or getattr(self.comm, "capturable", False))
-                     and sub is None and algo in ("npg", "vpg", "dapg"))
+                     and sub is None and algo in ("npg", "vpg", "dapg", "trpo"))
         if use_graph:
             key = self._graph_key(batch, T_global, (algo, gamma, gae_lambda, n_step_size, const_lr, kl_dist, cg_iters,
                                                     damping, residual_tol, learn_rate, skip_gae, demo_coef))
@@ -841,7 +842,11 @@ class UpdateEngine:
                 gs["theta_in"].copy_(theta)
                 gs["graph"].replay()
                 self.last_T, self.last_T_global = T, T_global
-                return self._finish(algo, const_lr, gs["delta"], T_global, None, [], gs["timing"])
+                trials = []
+                if algo == "trpo":   # the graph ends at the first evaluation; the search stays on the host
+                    step, evaluate, _, _, timing, inv_T = gs["closures"]
+                    trials = self._trpo_search(step, evaluate, gs["delta"], kl_dist, inv_T, trpo_verbose, timing)
+                return self._finish(algo, const_lr, gs["delta"], T_global, None, trials, gs["timing"])
 
         def launch(theta, ev):
             """Every device launch of the update up to the first evaluation (the
@@ -995,13 +1000,14 @@ class UpdateEngine:
             def step(mode, delta, alpha_in, const):
                 _lib.check(L.mjrl_npg_step(sp, _lib.ptr(v["g"]), _lib.ptr(x), _lib.ptr(theta), mode, float(delta),
                                            float(alpha_in), int(const), self.min_log_std, _lib.ptr(v["theta_new"]),
-                                           _lib.ptr(self.packed_new), _lib.ptr(self.out), st), "mjrl_npg_step")
+                                           _lib.ptr(self.packed_new), _lib.ptr(self.out), _lib.stream_ptr()),
+                           "mjrl_npg_step")
 
             def evaluate():
                 _lib.check(L.mjrl_policy_eval(sp, C.byref(rows_fvp), T, _lib.ptr(self.packed_new),
                                               _lib.ptr(self.packed_theta), _lib.ptr(osh), _lib.ptr(osc),
-                                              C.byref(sc_fvp), C.c_void_p(self.stats[S_EVAL:].data_ptr()), st),
-                           "mjrl_policy_eval")
+                                              C.byref(sc_fvp), C.c_void_p(self.stats[S_EVAL:].data_ptr()),
+                                              _lib.stream_ptr()), "mjrl_policy_eval")
                 if ms_pending[0]:
                     self._reduce_stats(S_MS, S_EVAL + 2)   # surr_before's moments + the eval sums
                     ms_pending[0] = False
@@ -1029,32 +1035,41 @@ class UpdateEngine:
         trials = []
 
         if algo == "trpo":
-            res = self.stats[S_EVAL:S_EVAL + 2].cpu().numpy()
-            alpha = np.float32(self.out[0].item())
-            surr_before = float(self.stats[S_MS].item() / self.stats[S_MS + 2].item())
-            for k in range(100):
-                kl = np.float32(res[1] * inv_T)
-                surr = np.float32(res[0] * inv_T)
-                trials.append((float(alpha), float(kl), float(surr)))
-                if kl < kl_dist:
-                    break
-                alpha = np.float32(0.9 * alpha)   # trpo.py:114 (python float * np.float32)
-                if trpo_verbose:
-                    print("Step size too high. Backtracking. | kl = %f | surr diff = %f" % (kl, surr - surr_before))
-                if k == 99:
-                    alpha = np.float32(0.0)
-                    break
-                step(1, delta, alpha, 0)
-                evaluate()
-                res = self.stats[S_EVAL:S_EVAL + 2].cpu().numpy()
-            if float(alpha) != trials[-1][0]:   # final re-evaluation (trpo.py:120-123)
-                step(1, delta, alpha, 0)
-                evaluate()
-            timing[3].record()
+            trials = self._trpo_search(step, evaluate, delta, kl_dist, inv_T, trpo_verbose, timing)
         result = self._finish(algo, const_lr, delta, T_global, sub, trials, timing)
         if use_graph:
             self._maybe_capture(key, launch, theta, delta, T_global)
         return result
+
+    def _trpo_search(self, step, evaluate, delta, kl_dist, inv_T, verbose, timing):
+        """TRPO's KL backtracking on the host (trpo.py:98-124) after the first
+        evaluation: alpha *= 0.9 while KL >= kl_dist (at most 100 trials), then the
+        final re-evaluation at the accepted alpha.  step / evaluate launch on the
+        current stream (eager, or after a graph replay of everything before)."""
+        trials = []
+        res = self.stats[S_EVAL:S_EVAL + 2].cpu().numpy()
+        alpha = np.float32(self.out[0].item())
+        surr_before = float(self.stats[S_MS].item() / self.stats[S_MS + 2].item())
+        for k in range(100):
+            kl = np.float32(res[1] * inv_T)
+            surr = np.float32(res[0] * inv_T)
+            trials.append((float(alpha), float(kl), float(surr)))
+            if kl < kl_dist:
+                break
+            alpha = np.float32(0.9 * alpha)   # trpo.py:114 (python float * np.float32)
+            if verbose:
+                print("Step size too high. Backtracking. | kl = %f | surr diff = %f" % (kl, surr - surr_before))
+            if k == 99:
+                alpha = np.float32(0.0)
+                break
+            step(1, delta, alpha, 0)
+            evaluate()
+            res = self.stats[S_EVAL:S_EVAL + 2].cpu().numpy()
+        if float(alpha) != trials[-1][0]:   # final re-evaluation (trpo.py:120-123)
+            step(1, delta, alpha, 0)
+            evaluate()
+        timing[3].record()
+        return trials
 
     # ------------------------------------------------------------------
     # hipGraph replay of whole updates (one process): the second consecutive
@@ -1092,7 +1107,7 @@ class UpdateEngine:
             finally:
                 graph_prof = self.kernel_timing
                 self.kernel_timing = prof_saved
-            gs.update(key=key, graph=g, theta_in=theta_in, timing=out[4], delta=delta, prof=graph_prof)
+            gs.update(key=key, graph=g, theta_in=theta_in, timing=out[4], delta=delta, prof=graph_prof, closures=out)
             self.st = _lib.stream_ptr()    # launch() cached the capture stream
             return
         import warnings

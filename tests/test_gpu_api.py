@@ -504,6 +504,42 @@ def test_graph_replay_matches_eager(name):
     assert np.array_equal(eng.vec["theta_new"].cpu().numpy(), ref2)
 
 
+@pytest.mark.parametrize("name", ["c3_trpo_backtrack", "c3_halfcheetah_trpo"])
+def test_trpo_graph_replay_matches_eager(name):
+    """TRPO under UpdateEngine.graphs: everything up to the first evaluation is
+    captured and replayed, the KL backtracking (trpo.py:98-124) continues on the
+    host after it; the replayed updates (trials included) must equal the eager one
+    bit for bit.  c3_trpo_backtrack backtracks several times."""
+    from oracle import npg_cpu as O
+    from mjrl_amd.engine import UpdateEngine
+    import test_gpu_parity as P
+    c = O.load_case(os.path.join(GOLDEN, name + ".npz"))
+    kw = O.case_kwargs(c)
+    assert kw["algo"] == "trpo"
+    dev = torch.device("cuda:0")
+    eng = UpdateEngine(int(c["n"]), int(c["m"]), c["hidden_t"], device=dev)
+    if c["transforms"] is not None:
+        eng.set_transformations(*c["transforms"])
+    batch = P.make_batch(c, dev)
+    th = torch.from_numpy(c["theta0"].astype(np.float32)).to(dev)
+    lam = None if np.isnan(c["gae_lambda"]) else float(c["gae_lambda"])
+    args = dict(algo="trpo", gamma=float(c["gamma"]), gae_lambda=lam, kl_dist=kw["kl_dist"],
+                cg_iters=kw.get("cg_iters", 10), damping=kw.get("damping", 1e-4), trpo_verbose=False)
+    ref = eng.update(batch, th, graph=False, **args)
+    ref_theta = eng.vec["theta_new"].cpu().numpy()
+    eng.graphs = True
+    outs = []
+    for _ in range(4):
+        res = eng.update(batch, th, **args)
+        outs.append((res, eng.vec["theta_new"].cpu().numpy()))
+    assert eng._gstate.get("graph") is not None
+    for res, theta in outs:
+        assert np.array_equal(theta, ref_theta)
+        assert res["trials"] == ref["trials"]
+        for k in ("alpha", "kl_dist", "surr_after", "surr_before", "cg_iters"):
+            assert res[k] == ref[k], k
+
+
 def test_mlp_baseline_fit_matches_reference():
     """MLPBaseline.fit / predict on the GPU (mlp_baseline.py:59-115) against the
     reference's own CPU fit: same initial weights, same minibatch order (numpy

@@ -272,7 +272,6 @@ __global__ void __launch_bounds__(CGX_T) k_cgm_xrp_f(mjrl_shape s, float* __rest
                                                      int32_t* __restrict__ done, float tol, int ng) {
     __shared__ double red[CGX_T / 64];
     __shared__ unsigned ticket;
-    if (*done) return;
     const int d = s.d;
     // every load that does not depend on v / mu is issued up front: this thread's own
     // element (p, x, r, z) and the first XRP_PRE terms of the r.r fold
@@ -307,6 +306,9 @@ __global__ void __launch_bounds__(CGX_T) k_cgm_xrp_f(mjrl_shape s, float* __rest
     }
     const float rr = (float)block_sum<CGX_T>(acc, red);
     const float mu = rr / rdotr;
+    // a converged CG loop (cg_solve.py:19-20): nothing is stored; checked after the
+    // folds, so the flag's load overlaps the state's
+    if (*done) return;
     if (own) {
         x[f] = __fadd_rn(xf, __fmul_rn(v, pf));
         const float rf = __fsub_rn(rfo, __fmul_rn(v, zfo));

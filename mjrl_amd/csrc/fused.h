@@ -171,7 +171,6 @@ __device__ __forceinline__ void fused_body(const RowArgs& a, const FOut& o) {
     float* GPs = smem + L::oGP;
     float* XS = smem + L::oXS;
 
-    if (MODE == FVP && a.done && *a.done) return;
 #ifdef MJRL_KX_PROF
     // phase profile (profiling builds, the k_kx counters): wave 0 of workgroup 0
     unsigned long long kx_acc_[KX_NPROF] = {0};
@@ -291,6 +290,9 @@ __device__ __forceinline__ void fused_body(const RowArgs& a, const FOut& o) {
             ldw0 = L::LW0;
         }
     }
+    // a converged CG loop (cg_solve.py:19-20): checked once the preamble's loads have
+    // been consumed, so the flag's load overlaps them
+    if (MODE == FVP && a.done && *a.done) return;
 
     KX_STAMP(15);
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {

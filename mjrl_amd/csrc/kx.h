@@ -294,7 +294,6 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
     char* A0i = sb + L::oA0;
     char* A1i = sb + L::oA1;
 
-    if (MODE == FVP && a.done && *a.done) return;
 #ifdef MJRL_KX_PROF
     const unsigned long long kx_t0_ = __builtin_amdgcn_s_memtime();
     unsigned long long kx_pre_[6];
@@ -394,6 +393,9 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
         }
     }
     KX_PRE(4);
+    // a converged CG loop (cg_solve.py:19-20): checked once the preamble's loads have
+    // been consumed (image stores, W0 slice split), so the flag's load overlaps them
+    if (MODE == FVP && a.done && *a.done) return;
 
     floatx4 g0[KG];
 #pragma unroll

@@ -1088,7 +1088,6 @@ __global__ void __launch_bounds__(64 * GATHER_WAVES) k_gather_flat(const float* 
                                                                    int mp, float* __restrict__ gsum,
                                                                    const int32_t* __restrict__ done, CgZ cz,
                                                                    int64_t wcap) {
-    if (done && *done) return;
     __shared__ double part[GATHER_WAVES][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int f = blockIdx.x * 64 + lane;
@@ -1114,6 +1113,9 @@ __global__ void __launch_bounds__(64 * GATHER_WAVES) k_gather_flat(const float* 
         for (int b = b0; b < b1; ++b) acc += lspart[(int64_t)b * mp + lsj];
     }
     part[w][lane] = acc;
+    // a converged CG loop: nothing is stored (checked after the slab loads, whose
+    // results the store above consumed, so the flag's load overlaps them)
+    if (done && *done) return;
     __syncthreads();
     if (w == 0) {
         float gs = 0.f;

@@ -266,6 +266,7 @@ __global__ void __launch_bounds__(CGM_T) k_cgm_xr(int d, const float* __restrict
 // have read rdotr by then) records rdotr, mu, v, p.z, the iteration count and the
 // residual_tol break.
 constexpr int CGX_T = 1024;
+template <int XRP_PRE>   // terms of the r.r fold per thread loaded up front (8: d <= 8192, 32: d <= 32768)
 __global__ void __launch_bounds__(CGX_T) k_cgm_xrp_f(mjrl_shape s, float* __restrict__ p, const float* __restrict__ z,
                                                      float* __restrict__ x, const float* __restrict__ r,
                                                      float* __restrict__ r_out, float* __restrict__ packed_p, float* cg,
@@ -274,11 +275,10 @@ __global__ void __launch_bounds__(CGX_T) k_cgm_xrp_f(mjrl_shape s, float* __rest
     __shared__ unsigned ticket;
     const int d = s.d;
     // every load that does not depend on v / mu is issued up front: this thread's own
-    // element (p, x, r, z) and the first XRP_PRE terms of the r.r fold
+    // element (p, x, r, z) and the first XRP_PRE terms of the r.r fold per thread
     const int f = blockIdx.x * CGX_T + threadIdx.x;
     const bool own = f < d;
     const float pf = own ? p[f] : 0.f, xf = own ? x[f] : 0.f, rfo = own ? r[f] : 0.f, zfo = own ? z[f] : 0.f;
-    constexpr int XRP_PRE = 8;
     float rpre[XRP_PRE], zpre[XRP_PRE];
 #pragma unroll
     for (int u = 0; u < XRP_PRE; ++u) {
@@ -639,8 +639,14 @@ int mjrl_cg_step_xr_p(const mjrl_shape* s, float* x, const float* r, float* r_ou
     if (!s || !x || !r || !r_out || r_out == r || !p || !z || !packed_p || !cg || !done) return MJRL_EINVAL;
     const int ng = (s->d + 63) / 64;   // the fused gather's workgroups
     if (ng > CG_PZ_MAX) return MJRL_EINVAL;
-    hipLaunchKernelGGL(k_cgm_xrp_f, dim3((s->d + CGX_T - 1) / CGX_T), dim3(CGX_T), 0, (hipStream_t)stream, *s, p, z,
-                       x, r, r_out, packed_p, cg, done, residual_tol, ng);
+    // every term of the r.r fold in flight at once up to d = 32768 (Humanoid: 29,410);
+    // small d keeps 8, its masked loads past d would cost more than they hide
+    if (s->d > 8 * CGX_T)
+        hipLaunchKernelGGL(k_cgm_xrp_f<32>, dim3((s->d + CGX_T - 1) / CGX_T), dim3(CGX_T), 0, (hipStream_t)stream, *s,
+                           p, z, x, r, r_out, packed_p, cg, done, residual_tol, ng);
+    else
+        hipLaunchKernelGGL(k_cgm_xrp_f<8>, dim3((s->d + CGX_T - 1) / CGX_T), dim3(CGX_T), 0, (hipStream_t)stream, *s,
+                           p, z, x, r, r_out, packed_p, cg, done, residual_tol, ng);
     return err(hipGetLastError());
 }
 

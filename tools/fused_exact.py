@@ -29,7 +29,7 @@ SHAPES = [  # (n, m, hidden, T)
 
 
 UPDATE_CASES = ["c2_swimmer", "c2_constlr", "c2_logstd_clamp", "c2_nogae", "c2_ragged", "c2_hvp_sub", "c2_h48x32",
-                "c1_pointmass_mlp32", "c3_halfcheetah_full", "c3_trpo_backtrack"]
+                "c1_pointmass_mlp32", "c3_halfcheetah_full", "c3_trpo_backtrack", "c4_humanoid", "c4_humanoid_scaled"]
 
 
 def dump(path):

@@ -92,3 +92,37 @@ def test_rows_path_vs_fp64(n, m, h, T):
     for a, b in zip(offs[:-1], offs[1:]):
         assert nrel(g[a:b], vpg64[a:b]) < 1e-4, (a, b, nrel(g[a:b], vpg64[a:b]))
         assert nrel(fv[a:b], fv64[a:b]) < 1e-4, (a, b, nrel(fv[a:b], fv64[a:b]))
+
+
+@pytest.mark.parametrize("n,m,h,T", [
+    (8, 2, (64, 64), 12500),       # Swimmer: every weight image in LDS, one observation chunk
+    (8, 2, (64, 64), 64),          # one tile
+    (8, 2, (64, 64), 40000),       # more tiles than workgroups
+    (17, 6, (32, 32), 9001),       # hidden 32, partial last tile
+    (45, 20, (64, 64), 5000),      # MP 32: W1 / W2 images, W0 from L2
+    (100, 6, (64, 64), 7777),      # two observation chunks (the gW0 re-stream)
+    (150, 20, (32, 32), 4001),     # three chunks, MP 32
+])
+def test_fused_path_vs_fp64(n, m, h, T):
+    """The fused persistent kernel (k_fused: weight images in LDS, W1^T / W2^T read
+    transposed from them, the slab staged through LDS) against the same fp64
+    closed forms, on each of its layout variants."""
+    from mjrl_amd.engine import UpdateEngine
+    rs = np.random.RandomState(n * 1000 + T)
+    obs, act, adv = rs.randn(T, n), rs.randn(T, m), rs.randn(T)
+    d = h[0] * n + h[0] + h[1] * h[0] + h[1] + m * h[1] + m + m
+    theta = (rs.randn(d) * 0.1).astype(np.float32)
+    theta[-m:] = np.linspace(-1.0, 0.3, m)
+    v = (rs.randn(d) * 1e-2).astype(np.float32)
+    vpg64, fv64 = _truth(obs, act, adv, theta, v, 1e-4, n, m, h)
+    eng = UpdateEngine(n, m, h, device="cuda:0", precision="f32")
+    assert eng.accumulate_path() == 1
+    eng.load_rows(obs, act, adv)
+    g = eng.forward_pass(torch.from_numpy(theta).cuda(), T).cpu().numpy()
+    fv = eng.fvp(torch.from_numpy(v).cuda(), damping=1e-4, T=T).cpu().numpy()
+    assert nrel(g, vpg64) < 1e-5, nrel(g, vpg64)
+    assert nrel(fv, fv64) < 1e-5, nrel(fv, fv64)
+    offs = np.cumsum([0, h[0] * n, h[0], h[1] * h[0], h[1], m * h[1], m, m])
+    for a, b in zip(offs[:-1], offs[1:]):
+        assert nrel(g[a:b], vpg64[a:b]) < 1e-4, (a, b, nrel(g[a:b], vpg64[a:b]))
+        assert nrel(fv[a:b], fv64[a:b]) < 1e-4, (a, b, nrel(fv[a:b], fv64[a:b]))

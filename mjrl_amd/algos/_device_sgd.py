@@ -20,6 +20,8 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
+from .._capture import capture
+
 LOG_2PI = float(np.log(2 * np.pi))
 
 
@@ -173,7 +175,7 @@ class DeviceTrainer:
                 body()
             torch.cuda.current_stream(dev).wait_stream(s)
             graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
+            with capture(graph):
                 body()
         finally:
             with torch.no_grad():

@@ -27,6 +27,8 @@ import numpy as np
 import torch
 import torch.nn as nn
 
+from .._capture import capture
+
 
 def _features_np(paths, n):
     """mlp_baseline.py:37-56 on the host (f64, as the reference builds it)."""
@@ -177,7 +179,7 @@ class MLPBaseline:
                 body()
             torch.cuda.current_stream(dev).wait_stream(s)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with capture(g):
                 body()
         finally:
             # restored whether or not the capture succeeded (a failed capture falls

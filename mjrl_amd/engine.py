@@ -22,6 +22,7 @@ import numpy as np
 import torch
 
 from . import _lib
+from ._capture import capture
 from .comm import LocalComm
 
 # slots (doubles) in the per-update stats buffer; each moments result takes 8 (6
@@ -844,8 +845,7 @@ class UpdateEngine:
                 self.last_T, self.last_T_global = T, T_global
                 trials = []
                 if algo == "trpo":   # the graph ends at the first evaluation; the search stays on the host
-                    step, evaluate, _, _, timing, inv_T = gs["closures"]
-                    trials = self._trpo_search(step, evaluate, gs["delta"], kl_dist, inv_T, trpo_verbose, timing)
+                    trials = self._trpo_search(gs["plan"], gs["delta"], kl_dist, trpo_verbose, gs["timing"])
                 return self._finish(algo, const_lr, gs["delta"], T_global, None, trials, gs["timing"])
 
         def launch(theta, ev):
@@ -996,57 +996,73 @@ class UpdateEngine:
                 cg_iters_run = None
             timing[2].record()
 
-            # a14: step size + update; a16 TRPO backtracking
-            def step(mode, delta, alpha_in, const):
-                _lib.check(L.mjrl_npg_step(sp, _lib.ptr(v["g"]), _lib.ptr(x), _lib.ptr(theta), mode, float(delta),
-                                           float(alpha_in), int(const), self.min_log_std, _lib.ptr(v["theta_new"]),
-                                           _lib.ptr(self.packed_new), _lib.ptr(self.out), _lib.stream_ptr()),
-                           "mjrl_npg_step")
-
-            def evaluate():
-                _lib.check(L.mjrl_policy_eval(sp, C.byref(rows_fvp), T, _lib.ptr(self.packed_new),
-                                              _lib.ptr(self.packed_theta), _lib.ptr(osh), _lib.ptr(osc),
-                                              C.byref(sc_fvp), C.c_void_p(self.stats[S_EVAL:].data_ptr()),
-                                              _lib.stream_ptr()), "mjrl_policy_eval")
-                if ms_pending[0]:
-                    self._reduce_stats(S_MS, S_EVAL + 2)   # surr_before's moments + the eval sums
-                    ms_pending[0] = False
-                else:
-                    self._reduce_stats(S_EVAL, S_EVAL + 2)
-
+            # a14: step size + update; a16 TRPO backtracking.  `plan` holds the
+            # buffers the step and the evaluation read (no reference to the engine:
+            # a captured graph keeps it for the TRPO search after each replay, and
+            # an engine <-> graph cycle would leave the graph's destruction to the
+            # cyclic GC, at any later allocation, possibly inside another capture)
+            plan = dict(x=x, theta=theta, rows=rows_fvp, sc=sc_fvp, T=T, osh=osh, osc=osc, ms_pending=[True],
+                        inv_T=inv_T)
             if algo == "vpg":
-                step(1, 0.0, np.float32(learn_rate), 0)
+                self._step(plan, 1, 0.0, np.float32(learn_rate), 0)
                 delta = None
             elif algo == "npg" and const_lr is not None:
-                step(1, 0.0, np.float32(const_lr), 1)
+                self._step(plan, 1, 0.0, np.float32(const_lr), 1)
                 delta = None
             elif algo == "npg":
                 delta = n_step_size if kl_dist is None else 2.0 * kl_dist
-                step(0, delta, 0.0, 0)
+                self._step(plan, 0, delta, 0.0, 0)
             else:   # trpo / dapg: delta = 2 kl_dist
                 delta = 2.0 * kl_dist
-                step(0, delta, 0.0, 0)
-            evaluate()
+                self._step(plan, 0, delta, 0.0, 0)
+            self._evaluate(plan)
             if algo != "trpo":
                 timing[3].record()
-            return step, evaluate, delta, x, timing, inv_T
+            return plan, delta, timing
 
-        step, evaluate, delta, x, timing, inv_T = launch(theta, lambda: torch.cuda.Event(enable_timing=True))
+        plan, delta, timing = launch(theta, lambda: torch.cuda.Event(enable_timing=True))
         trials = []
 
         if algo == "trpo":
-            trials = self._trpo_search(step, evaluate, delta, kl_dist, inv_T, trpo_verbose, timing)
+            trials = self._trpo_search(plan, delta, kl_dist, trpo_verbose, timing)
         result = self._finish(algo, const_lr, delta, T_global, sub, trials, timing)
         if use_graph:
             self._maybe_capture(key, launch, theta, delta, T_global)
         return result
 
-    def _trpo_search(self, step, evaluate, delta, kl_dist, inv_T, verbose, timing):
+    def _step(self, plan, mode, delta, alpha_in, const):
+        """a14: theta_new = theta + alpha x (npg_cg.py:128-141), alpha from the
+        step-size rule (mode 0) or given (mode 1), log-std clamp, repack."""
+        L = self.lib
+        _lib.check(L.mjrl_npg_step(C.byref(self.shape), _lib.ptr(self.pvec["g"]), _lib.ptr(plan["x"]),
+                                   _lib.ptr(plan["theta"]), mode, float(delta), float(alpha_in), int(const),
+                                   self.min_log_std, _lib.ptr(self.pvec["theta_new"]), _lib.ptr(self.packed_new),
+                                   _lib.ptr(self.out), _lib.stream_ptr()), "mjrl_npg_step")
+
+    def _evaluate(self, plan):
+        """Surrogate and KL at theta_new (npg_cg.py:142-143): one EVAL pass, then
+        (sharded) the all-reduce of its sums; the first one carries surr_before's
+        moments too."""
+        L = self.lib
+        _lib.check(L.mjrl_policy_eval(C.byref(self.shape), C.byref(plan["rows"]), plan["T"],
+                                      _lib.ptr(self.packed_new), _lib.ptr(self.packed_theta), _lib.ptr(plan["osh"]),
+                                      _lib.ptr(plan["osc"]), C.byref(plan["sc"]),
+                                      C.c_void_p(self.stats[S_EVAL:].data_ptr()), _lib.stream_ptr()),
+                   "mjrl_policy_eval")
+        if plan["ms_pending"][0]:
+            self._reduce_stats(S_MS, S_EVAL + 2)   # surr_before's moments + the eval sums
+            plan["ms_pending"][0] = False
+        else:
+            self._reduce_stats(S_EVAL, S_EVAL + 2)
+
+    def _trpo_search(self, plan, delta, kl_dist, verbose, timing):
         """TRPO's KL backtracking on the host (trpo.py:98-124) after the first
         evaluation: alpha *= 0.9 while KL >= kl_dist (at most 100 trials), then the
-        final re-evaluation at the accepted alpha.  step / evaluate launch on the
-        current stream (eager, or after a graph replay of everything before)."""
+        final re-evaluation at the accepted alpha.  The step and the evaluation
+        launch on the current stream (eager, or after a graph replay of everything
+        before)."""
         trials = []
+        inv_T = plan["inv_T"]
         res = self.stats[S_EVAL:S_EVAL + 2].cpu().numpy()
         alpha = np.float32(self.out[0].item())
         surr_before = float(self.stats[S_MS].item() / self.stats[S_MS + 2].item())
@@ -1062,12 +1078,12 @@ class UpdateEngine:
             if k == 99:
                 alpha = np.float32(0.0)
                 break
-            step(1, delta, alpha, 0)
-            evaluate()
+            self._step(plan, 1, delta, alpha, 0)
+            self._evaluate(plan)
             res = self.stats[S_EVAL:S_EVAL + 2].cpu().numpy()
         if float(alpha) != trials[-1][0]:   # final re-evaluation (trpo.py:120-123)
-            step(1, delta, alpha, 0)
-            evaluate()
+            self._step(plan, 1, delta, alpha, 0)
+            self._evaluate(plan)
         timing[3].record()
         return trials
 
@@ -1099,7 +1115,7 @@ class UpdateEngine:
                 self.kernel_timing = []    # the capture's own per-FVP events
             g = torch.cuda.CUDAGraph()
             try:
-                with torch.cuda.graph(g):
+                with capture(g):
                     out = launch(theta_in, ev)
             except Exception as e:         # timing events inside a capture unsupported: capture without
                 err = e
@@ -1107,7 +1123,8 @@ class UpdateEngine:
             finally:
                 graph_prof = self.kernel_timing
                 self.kernel_timing = prof_saved
-            gs.update(key=key, graph=g, theta_in=theta_in, timing=out[4], delta=delta, prof=graph_prof, closures=out)
+            # plan: buffers only (no closure over the engine, see launch())
+            gs.update(key=key, graph=g, theta_in=theta_in, timing=out[2], delta=delta, prof=graph_prof, plan=out[0])
             self.st = _lib.stream_ptr()    # launch() cached the capture stream
             return
         import warnings

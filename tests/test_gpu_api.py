@@ -469,20 +469,30 @@ def test_train_step_baseline_fit_path():
     np.testing.assert_allclose(base._coeffs, host._coeffs, rtol=1e-7, atol=1e-9)
 
 
-@pytest.mark.parametrize("name", ["c2_swimmer", "c4_humanoid"])
+@pytest.mark.parametrize("name", ["c2_swimmer", "c4_humanoid", "c3_halfcheetah_trpo", "c5_door_dapg"])
 def test_graph_replay_matches_eager(name):
     """UpdateEngine.graphs: the second identical update is captured as a hipGraph
     and later ones replay it; the replayed update must equal the eager one bit
-    for bit (same kernels, same order, same reductions)."""
+    for bit (same kernels, same order, same reductions).  Covers every kernel
+    family under capture: k_fused (c2), k_kx (c4), k_rows + k_wgrad_all (c3,
+    run as NPG here; its TRPO search is the next test) and k_rows + k_wgrad
+    with demo rows (c5, DAPG)."""
     from oracle import npg_cpu as O
     from mjrl_amd.engine import UpdateEngine
     import test_gpu_parity as P
     c = O.load_case(os.path.join(GOLDEN, name + ".npz"))
+    kw = O.case_kwargs(c)
     dev = torch.device("cuda:0")
     eng = UpdateEngine(int(c["n"]), int(c["m"]), c["hidden_t"], device=dev)
+    if c["transforms"] is not None:
+        eng.set_transformations(*c["transforms"])
     batch = P.make_batch(c, dev)
     th = torch.from_numpy(c["theta0"].astype(np.float32)).to(dev)
-    args = dict(algo="npg", gamma=float(c["gamma"]), gae_lambda=float(c["gae_lambda"]), n_step_size=0.05)
+    lam = None if np.isnan(c["gae_lambda"]) else float(c["gae_lambda"])
+    args = dict(algo="npg", gamma=float(c["gamma"]), gae_lambda=lam, n_step_size=0.05)
+    if kw["algo"] == "dapg":
+        args = dict(algo="dapg", gamma=float(c["gamma"]), gae_lambda=lam, kl_dist=kw["kl_dist"],
+                    demo_coef=kw["demo_coef"])
     ref = eng.update(batch, th, graph=False, **args)
     ref_theta = eng.vec["theta_new"].cpu().numpy()
     eng.graphs = True
@@ -538,6 +548,47 @@ def test_trpo_graph_replay_matches_eager(name):
         assert res["trials"] == ref["trials"]
         for k in ("alpha", "kl_dist", "surr_after", "surr_before", "cg_iters"):
             assert res[k] == ref[k], k
+
+
+def test_capture_survives_dead_graph_cycles():
+    """The round-4 driver abort: the cyclic GC destroying a dead
+    engine's captured graph, pinned readback buffers and events while another
+    engine captures.  Dead cycles holding captured graphs are left for the
+    collector (disabled meanwhile, so they are still there at the capture), then
+    a TRPO update of the HalfCheetah shape is captured and replayed: every
+    capture goes through mjrl_amd._capture.capture, which collects them first
+    and keeps the collector off until the capture ends."""
+    import gc
+    from oracle import npg_cpu as O
+    from mjrl_amd.engine import UpdateEngine
+    import test_gpu_parity as P
+    dev = torch.device("cuda:0")
+
+    def engine(name, **extra):
+        c = O.load_case(os.path.join(GOLDEN, name + ".npz"))
+        eng = UpdateEngine(int(c["n"]), int(c["m"]), c["hidden_t"], device=dev)
+        batch = P.make_batch(c, dev)
+        th = torch.from_numpy(c["theta0"].astype(np.float32)).to(dev)
+        lam = None if np.isnan(c["gae_lambda"]) else float(c["gae_lambda"])
+        eng.graphs = True
+        outs = [eng.update(batch, th, gamma=float(c["gamma"]), gae_lambda=lam, **extra) for _ in range(3)]
+        assert eng._gstate.get("graph") is not None
+        return eng, outs
+
+    enabled = gc.isenabled()
+    gc.disable()
+    try:
+        for _ in range(2):
+            a, _ = engine("c2_swimmer", algo="npg", n_step_size=0.05)
+            a._cycle = a
+            del a
+        kl = O.case_kwargs(O.load_case(os.path.join(GOLDEN, "c3_trpo_backtrack.npz")))["kl_dist"]
+        b, outs = engine("c3_trpo_backtrack", algo="trpo", kl_dist=kl, trpo_verbose=False)
+    finally:
+        if enabled:
+            gc.enable()
+    assert outs[1]["trials"] == outs[2]["trials"] and outs[1]["alpha"] == outs[2]["alpha"]
+    torch.cuda.synchronize()
 
 
 def test_mlp_baseline_fit_matches_reference():

@@ -694,6 +694,8 @@ def main():
             out["vs_cpu_baseline"] = round(out["value"] / out["cpu_baseline"]["value"], 2)
         print(json.dumps(out), file=json_out, flush=True)
     if world > 1:
+        from mjrl_amd.comm import release_comms
+        release_comms()
         torch.distributed.destroy_process_group()
 
 

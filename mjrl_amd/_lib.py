@@ -96,6 +96,8 @@ SIGNATURES = {
     "mjrl_policy_mean": [SP, P, I64, P, P, P, P, P, P, P],
     "mjrl_host_stage_f64": [P, I64, I32, P, P, P],
     "mjrl_host_stage_f32": [P, I64, I32, P, P, P],
+    "mjrl_host_stage_f64_portable": [P, I64, I32, P, P, P],
+    "mjrl_host_stage_avx512": [],
 }
 
 _LIB = None
@@ -125,6 +127,29 @@ def load(path=None):
         fn.restype = C.c_int
     _LIB = lib
     return lib
+
+
+STAGE_LIB_PATH = os.path.join(HERE, "lib", "libmjrl_stage.so")
+STAGE_FUNCS = ("mjrl_host_stage_f64", "mjrl_host_stage_f32", "mjrl_host_stage_f64_portable", "mjrl_host_stage_avx512")
+_STAGE = None
+
+
+def stage_lib():
+    """The host-only staging library (csrc/stage.cpp, lib/libmjrl_stage.so): the
+    f64 -> f32 convert-and-range pass of the staging threads and of the pool
+    controller, without loading the HIP library or its code objects."""
+    global _STAGE
+    if _STAGE is None:
+        if not os.path.exists(STAGE_LIB_PATH):
+            raise MjrlError("mjrl_amd staging library not built: %s (run `python -m mjrl_amd.build`)"
+                            % STAGE_LIB_PATH)
+        lib = C.CDLL(STAGE_LIB_PATH)
+        for name in STAGE_FUNCS:
+            fn = getattr(lib, name)
+            fn.argtypes = SIGNATURES[name]
+            fn.restype = C.c_int
+        _STAGE = lib
+    return _STAGE
 
 
 def lib():

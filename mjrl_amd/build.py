@@ -25,7 +25,9 @@ FLAGS = [
 SOURCES = ["batch.hip", "policy.hip", "cg.hip", "baseline.hip", "rollout.hip"]
 # host-only C++ (the staging conversion of csrc/stage.cpp), built with g++
 HOST_SOURCES = ["stage.cpp"]
-HOST_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-mavx2", "-Wall"]
+# no -m flag: the AVX-512 path is selected at run time (csrc/stage.cpp)
+HOST_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall"]
+STAGE_LIB = os.path.join(OUTDIR, "libmjrl_stage.so")
 
 
 def _deps():
@@ -61,6 +63,14 @@ def build(force=False, jobs=None, prof=False, tag="", extra=()):
         objs = list(ex.map(lambda s: _compile(s, force, prof, tag, extra), SOURCES + HOST_SOURCES))
     if force or not os.path.exists(lib) or os.path.getmtime(lib) < max(os.path.getmtime(o) for o in objs):
         cmd = [HIPCC, "-shared", "--offload-arch=" + ARCH, "-fPIC"] + objs + ["-o", lib]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("link failed:\n%s\n%s" % (" ".join(cmd), r.stderr[-8000:]))
+    # the host-only staging library (no HIP): the same stage object, linked by g++
+    stage_o = [o for o in objs if os.path.basename(o).startswith("stage")]
+    slib = STAGE_LIB.replace(".so", tag + ".so") if tag else STAGE_LIB
+    if not prof and (force or not os.path.exists(slib) or os.path.getmtime(slib) < os.path.getmtime(stage_o[0])):
+        cmd = [os.environ.get("CXX", "g++"), "-shared", "-fPIC"] + stage_o + ["-o", slib]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError("link failed:\n%s\n%s" % (" ".join(cmd), r.stderr[-8000:]))

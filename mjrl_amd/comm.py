@@ -231,16 +231,41 @@ def default_comm():
     return LocalComm()
 
 
+_RCCL_CACHE = {}
+
+
 def _group_comm(group=None):
     """The communicator of an initialised torch.distributed group: RCCL driven
     directly (RcclComm) when the group's backend is nccl (= RCCL) and
     MJRL_AMD_COMM is not 'torch'; torch's own collectives (DistComm) otherwise
-    (gloo: the CPU tests)."""
+    (gloo: the CPU tests).  One RcclComm per (group, device) for the life of the
+    group: agents built without an explicit comm share it (every new one would
+    be another ncclCommInitRank collective, in whatever order each rank builds
+    its agents), and it is destroyed at exit (release_comms)."""
     import os
     import torch.distributed as dist
     if dist.get_backend(group) == "nccl" and os.environ.get("MJRL_AMD_COMM", "rccl") != "torch":
-        return RcclComm(torch.device("cuda", torch.cuda.current_device()), group=group)
+        dev = torch.device("cuda", torch.cuda.current_device())
+        key = (id(group) if group is not None else None, dev.index)
+        c = _RCCL_CACHE.get(key)
+        if c is None or getattr(c, "_comm", None) is None:
+            if not _RCCL_CACHE:
+                import atexit
+                atexit.register(release_comms)
+            c = _RCCL_CACHE[key] = RcclComm(dev, group=group)
+        return c
     return DistComm(group)
+
+
+def release_comms():
+    """Destroys the cached RCCL communicators (at exit, or before the process
+    group is destroyed)."""
+    for c in list(_RCCL_CACHE.values()):
+        try:
+            c.close()
+        except Exception:
+            pass
+    _RCCL_CACHE.clear()
 
 
 def launched_world():

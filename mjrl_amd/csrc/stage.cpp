@@ -5,20 +5,35 @@
 // does that cast once, on the host thread pool, straight into a pinned slab, and
 // takes each column's range in the same pass: the split rows' column scales then
 // need no device pass over the batch (mjrl_obs_colscale_range), and the pack of a
-// chunk never waits for a whole-batch reduction on the device.  Plain C++ built
-// with g++ into libmjrl_amd.so; loops the compiler vectorises (min / max written
-// as the compare-select that maps to minps / maxps, NaN skipped).
+// chunk never waits for a whole-batch reduction on the device.
+//
+// Host-only C++ (g++), built into its own library lib/libmjrl_stage.so (the pool
+// controller and the staging threads never load the HIP library) and linked into
+// libmjrl_amd.so too, which exports the whole C ABI.  Two code paths, chosen at
+// run time (no -m flag ties the library to one CPU):
+//   AVX-512 (Zen 4/5, Xeon): per block of rows (32 KB of f32), strip by strip of
+//     192 columns, each 16-column chunk is converted (two masked 8 x f64 loads ->
+//     one 16 x f32 vector), folded into the strip's column range held in
+//     registers across the block's rows (min / max, NaN skipped: vminps returns
+//     its second operand when either is NaN) and written to an L1/L2-resident
+//     block buffer; the block, which is contiguous in the slab, then leaves with
+//     non-temporal 64-byte stores.  Round 4's scalar-typed loop did cached stores:
+//     every written line was first read from DRAM (read-for-ownership) and the
+//     slab displaced the source from the caches, so the conversion, not the PCIe
+//     copy, set the end-to-end time.
+//   portable: the same one-pass loop, auto-vectorised for the build's baseline ISA.
 #include <cstdint>
+#include <cstring>
+
+#include <immintrin.h>
 
 #include "../../include/mjrl_amd.h"
 
 namespace {
 
 template <typename S>
-int stage_rows(const S* __restrict__ src, int64_t rows, int32_t n, float* __restrict__ dst, float* __restrict__ cmin,
-               float* __restrict__ cmax) {
-    if (rows < 0 || n <= 0 || (rows > 0 && (!src || !dst))) return MJRL_EINVAL;
-    if ((cmin == nullptr) != (cmax == nullptr)) return MJRL_EINVAL;
+int stage_portable(const S* __restrict__ src, int64_t rows, int32_t n, float* __restrict__ dst,
+                   float* __restrict__ cmin, float* __restrict__ cmax) {
     const int64_t ne = rows * (int64_t)n;
     if (!cmin) {
         for (int64_t i = 0; i < ne; ++i) dst[i] = (float)src[i];
@@ -38,6 +53,117 @@ int stage_rows(const S* __restrict__ src, int64_t rows, int32_t n, float* __rest
     return MJRL_OK;
 }
 
+#define MJRL_AVX512 __attribute__((target("avx512f,avx512vl,avx512dq,avx512bw")))
+
+MJRL_AVX512 inline __m512 load16(const double* p, __mmask16 m) {
+    const __m256 lo = _mm512_cvtpd_ps(_mm512_maskz_loadu_pd((__mmask8)(m & 0xff), p));
+    const __m256 hi = _mm512_cvtpd_ps(_mm512_maskz_loadu_pd((__mmask8)(m >> 8), p + 8));
+    return _mm512_insertf32x8(_mm512_castps256_ps512(lo), hi, 1);
+}
+MJRL_AVX512 inline __m512 load16(const float* p, __mmask16 m) { return _mm512_maskz_loadu_ps(m, p); }
+
+// `count` floats from an L1/L2-resident buffer to dst with non-temporal stores
+// (64-byte aligned body; head and tail with masked ordinary stores)
+MJRL_AVX512 inline void stream_out(float* dst, const float* buf, int64_t count) {
+    int64_t i = 0;
+    const int64_t mis = (int64_t)(reinterpret_cast<uintptr_t>(dst) & 63) / 4;
+    if (reinterpret_cast<uintptr_t>(dst) & 3) {   // not even float aligned: ordinary stores throughout
+        std::memcpy(dst, buf, count * sizeof(float));
+        return;
+    }
+    if (mis) {
+        const int64_t h = 16 - mis < count ? 16 - mis : count;
+        const __mmask16 m = (__mmask16)((1u << h) - 1);
+        _mm512_mask_storeu_ps(dst, m, _mm512_maskz_loadu_ps(m, buf));
+        i = h;
+    }
+    for (; i + 16 <= count; i += 16) _mm512_stream_ps(dst + i, _mm512_loadu_ps(buf + i));
+    if (i < count) {
+        const __mmask16 m = (__mmask16)((1u << (count - i)) - 1);
+        _mm512_mask_storeu_ps(dst + i, m, _mm512_maskz_loadu_ps(m, buf + i));
+    }
+}
+
+// One column strip [c0, c0 + 16 NCH) of rows r0 .. r1 - 1: converted into the block
+// buffer, the strip's range kept in 2 NCH registers across the rows
+template <typename S, bool RANGE, int NCH>
+MJRL_AVX512 inline void strip(const S* __restrict__ src, int64_t r0, int64_t r1, int32_t n, int c0, int nc,
+                              __mmask16 tail, float* __restrict__ buf, float* __restrict__ cmin,
+                              float* __restrict__ cmax) {
+    __m512 lo[NCH], hi[NCH];
+    __mmask16 mk[NCH];
+#pragma GCC unroll 16
+    for (int j = 0; j < NCH; ++j) {
+        const int c = c0 / 16 + j;
+        mk[j] = c < nc ? (c + 1 < nc ? (__mmask16)0xffff : tail) : (__mmask16)0;
+        if (RANGE) {
+            lo[j] = _mm512_maskz_loadu_ps(mk[j], cmin + 16 * c);
+            hi[j] = _mm512_maskz_loadu_ps(mk[j], cmax + 16 * c);
+        }
+    }
+    for (int64_t r = r0; r < r1; ++r) {
+        const S* s = src + r * n + c0;
+        float* b = buf + (r - r0) * n + c0;
+#pragma GCC unroll 16
+        for (int j = 0; j < NCH; ++j) {
+            const __m512 v = load16(s + 16 * j, mk[j]);
+            _mm512_mask_storeu_ps(b + 16 * j, mk[j], v);
+            if (RANGE) {
+                // vminps / vmaxps return the SECOND operand when either is NaN:
+                // (v, range) keeps the range for a NaN value, and for a -0.0 / 0.0 tie
+                lo[j] = _mm512_min_ps(v, lo[j]);
+                hi[j] = _mm512_max_ps(v, hi[j]);
+            }
+        }
+    }
+    if (RANGE) {
+#pragma GCC unroll 16
+        for (int j = 0; j < NCH; ++j) {
+            const int c = c0 / 16 + j;
+            _mm512_mask_storeu_ps(cmin + 16 * c, mk[j], lo[j]);
+            _mm512_mask_storeu_ps(cmax + 16 * c, mk[j], hi[j]);
+        }
+    }
+}
+
+template <typename S, bool RANGE>
+MJRL_AVX512 int stage_avx512(const S* __restrict__ src, int64_t rows, int32_t n, float* __restrict__ dst,
+                             float* __restrict__ cmin, float* __restrict__ cmax) {
+    constexpr int BUF = 8192;   // floats of the block buffer (32 KB: stays in L1 / L2)
+    constexpr int NCH = 12;     // 16-column chunks per strip: 24 range registers of the 32
+    alignas(64) float buf[BUF + 16];
+    const int64_t rb = n <= BUF ? BUF / n : 0;
+    if (rb == 0) return stage_portable(src, rows, n, dst, cmin, cmax);
+    const int nc = (n + 15) / 16;
+    const __mmask16 tail = (__mmask16)(n % 16 ? (1u << (n % 16)) - 1 : 0xffff);
+    for (int64_t r0 = 0; r0 < rows; r0 += rb) {
+        const int64_t r1 = r0 + rb < rows ? r0 + rb : rows;
+        // strip by strip over the block: the block's source (rb rows) stays in the
+        // core's caches between strips, the ranges in registers within one
+        for (int c0 = 0; c0 < n; c0 += 16 * NCH) strip<S, RANGE, NCH>(src, r0, r1, n, c0, nc, tail, buf, cmin, cmax);
+        stream_out(dst + r0 * n, buf, (r1 - r0) * n);
+    }
+    _mm_sfence();   // the streamed lines are globally visible before the caller's H2D copy
+    return MJRL_OK;
+}
+
+bool have_avx512() {
+    static const int ok = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512vl") &&
+                          __builtin_cpu_supports("avx512dq") && __builtin_cpu_supports("avx512bw");
+    return ok;
+}
+
+template <typename S>
+int stage_rows(const S* src, int64_t rows, int32_t n, float* dst, float* cmin, float* cmax) {
+    if (rows < 0 || n <= 0 || (rows > 0 && (!src || !dst))) return MJRL_EINVAL;
+    if ((cmin == nullptr) != (cmax == nullptr)) return MJRL_EINVAL;
+    if (rows == 0) return MJRL_OK;
+    if (have_avx512())
+        return cmin ? stage_avx512<S, true>(src, rows, n, dst, cmin, cmax)
+                    : stage_avx512<S, false>(src, rows, n, dst, cmin, cmax);
+    return stage_portable(src, rows, n, dst, cmin, cmax);
+}
+
 }  // namespace
 
 extern "C" {
@@ -49,5 +175,14 @@ int mjrl_host_stage_f64(const double* src, int64_t rows, int32_t n, float* dst, 
 int mjrl_host_stage_f32(const float* src, int64_t rows, int32_t n, float* dst, float* cmin, float* cmax) {
     return stage_rows(src, rows, n, dst, cmin, cmax);
 }
+
+// The portable loop, callable whatever the CPU (tests compare the two paths).
+int mjrl_host_stage_f64_portable(const double* src, int64_t rows, int32_t n, float* dst, float* cmin, float* cmax) {
+    if (rows < 0 || n <= 0 || (rows > 0 && (!src || !dst))) return MJRL_EINVAL;
+    if ((cmin == nullptr) != (cmax == nullptr)) return MJRL_EINVAL;
+    return stage_portable(src, rows, n, dst, cmin, cmax);
+}
+
+int mjrl_host_stage_avx512(void) { return have_avx512() ? 1 : 0; }
 
 }  // extern "C"

@@ -51,10 +51,12 @@ def _linear_coeffs(baseline, n):
     return c if len(c) == n + 4 else False
 
 
-def _host_threads():
+def _host_threads(cap=16):
     """Host threads for staging: the CPUs this process may actually use — its
     affinity set capped by the cgroup CPU quota (a container's affinity can list
-    the whole machine while its quota is a fraction of it) — at most 16."""
+    the whole machine while its quota is a fraction of it) — at most `cap` (16
+    for one GPU's staging; the pool controller, which converts every GPU's shard,
+    passes 16 per GPU)."""
     try:
         n = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
@@ -74,18 +76,19 @@ def _host_threads():
             pass
     if quota:
         n = min(n, max(1, int(quota)))
-    return max(1, min(16, n))
+    return max(1, min(int(cap), n))
 
 
 def host_stage(arrs, view, offs, a0, a1, lo=None, hi=None):
     """Arrays a0 .. a1 - 1 of `arrs` into their rows offs[i]:offs[i+1] of `view`
     (a pinned host array), converted to view's dtype; with lo / hi (float32 [n])
     the column ranges of what was written are folded in.  f64 / f32 arrays go
-    through the native one-pass convert-and-range loop (mjrl_host_stage_*, ctypes
+    through the native one-pass convert-and-range loop (mjrl_host_stage_* of the
+    host-only lib/libmjrl_stage.so: AVX-512 with streaming stores; ctypes
     releases the GIL), anything else through numpy."""
     fns = None
     if view.dtype == np.float32 and view.ndim == 2:
-        L = _lib.load()
+        L = _lib.stage_lib()
         fns = {np.dtype(np.float64): L.mjrl_host_stage_f64, np.dtype(np.float32): L.mjrl_host_stage_f32}
     for i in range(a0, a1):
         dst = view[offs[i]:offs[i + 1]]

@@ -106,10 +106,13 @@ class _Layout:
 
 def _segment_dtype(agent):
     """float32 segments when the agent stages its observations in float32 and
-    fits its baseline from the batch in HBM (device LinearBaseline / MLPBaseline):
-    nothing in the worker then reads the float64 values; otherwise float64."""
+    its baseline predicts and fits from the batch in HBM (the device
+    LinearBaseline): nothing in the worker then reads the float64 values.
+    Otherwise float64: MLPBaseline builds its features from the path
+    observations on the host (clip(o) / 10 in f64, mlp_baseline.py:37-56), which
+    float32 views of a segment would round first."""
     f32 = np.dtype(getattr(agent, "staging_dtype", np.float64)) == np.float32
-    dev_fit = type(getattr(agent, "baseline", None)).__name__ in ("LinearBaseline", "MLPBaseline")
+    dev_fit = type(getattr(agent, "baseline", None)).__name__ == "LinearBaseline"
     return np.float32 if (f32 and dev_fit) else np.float64
 
 
@@ -312,6 +315,9 @@ class DevicePool:
                 p.kill()
         self._free_segments()
         self._listener.close()
+        if getattr(self, "_fillex", None) is not None:
+            self._fillex.shutdown(wait=False)
+            self._fillex = None
 
     def _state(self, agent, commit=True):
         """The agent as the workers rebuild it: its __getstate__ (the device
@@ -330,6 +336,15 @@ class DevicePool:
             self._digests = digests
         return dict(cls=type(agent), changed=changed, dropped=dropped)
 
+    def _fill_pool(self):
+        """The controller's conversion threads: 16 per GPU worker, within the CPUs
+        this process may use (engine._host_threads)."""
+        if getattr(self, "_fillex", None) is None:
+            import concurrent.futures as cf
+            from .engine import _host_threads
+            self._fillex = cf.ThreadPoolExecutor(_host_threads(16 * self.world), thread_name_prefix="mjrl_fill")
+        return self._fillex
+
     # ---- one update -------------------------------------------------------------
     def step(self, agent, paths, mode, gamma=0.995, gae_lambda=0.98, fit=False, return_errors=False):
         """The update of `agent` on `paths` by the workers.  mode 'samples':
@@ -346,27 +361,26 @@ class DevicePool:
                              % (len(paths), self.world))
         with_adv = mode == "paths"
         dtype = _segment_dtype(agent)
-        from .engine import _STAGING
-
         try:
             t0 = time.perf_counter()
             state = self._state(agent)
             t1 = time.perf_counter()
             layouts = []
-            for r in range(self.world):
-                # every shard's conversion spread over the staging thread pool
-                p0, p1 = parts[r]
-                L = _Layout(int(lengths[p0:p1].sum()), p1 - p0, n, m, with_adv, dtype)
-                _fill_shard(self._segment(r, L.nbytes).buf, L, paths[p0:p1], lengths[p0:p1], _STAGING.pool())
-                layouts.append(L)
-            t2 = time.perf_counter()
             rng = np.random.get_state()
             for r in range(self.world):
-                L = layouts[r]
+                # every shard's conversion spread over the controller's thread pool
+                # (16 threads per GPU, within the process's CPU share), and the shard
+                # handed to its worker as soon as it is filled: worker r stages
+                # (H2D) and starts its update while the controller fills shard r + 1
+                p0, p1 = parts[r]
+                L = _Layout(int(lengths[p0:p1].sum()), p1 - p0, n, m, with_adv, dtype)
+                _fill_shard(self._segment(r, L.nbytes).buf, L, paths[p0:p1], lengths[p0:p1], self._fill_pool())
+                layouts.append(L)
                 self._conns[r].send(("step", dict(state=state, shm=self._shm[r].name, T=L.T, P=L.P, n=n, m=m,
                                                   dtype=L.dtype.str, mode=mode, gamma=gamma, gae_lambda=gae_lambda,
                                                   fit=fit, return_errors=return_errors, rng=rng,
                                                   with_adv=with_adv)))
+            t2 = time.perf_counter()
             replies = self._recv_all()
             t3 = time.perf_counter()
         except BaseException:
@@ -516,11 +530,18 @@ def _worker_main(args):
                            logs=list(agent.logger.get_current_log().items()) if agent.save_logs else [],
                            sync={k: agent.__dict__[k] for k in _SYNC if k in agent.__dict__},
                            rng=np.random.get_state())
+            # the controller rewrites the segment after the reply: the DMA copies
+            # out of its registered memory must have completed first
+            from .engine import _STAGING
+            _STAGING.wait_host("obs")
+            _STAGING.wait_host("act")
             conn.send(("ok", out))
         except Exception:
             conn.send(("error", traceback.format_exc()))
     paths = agent = None
     _attach(shm, unreg, None)
+    from .comm import release_comms
+    release_comms()
     dist.destroy_process_group()
     return 0
 

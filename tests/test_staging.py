@@ -46,6 +46,40 @@ def test_host_stage_converts_and_takes_ranges(lib, dtype):
     assert np.array_equal(view2, ref, equal_nan=True)
 
 
+@pytest.mark.parametrize("n", [1, 15, 16, 17, 37, 376, 9000])
+def test_host_stage_avx512_equals_portable(lib, n):
+    """The AVX-512 path (block buffer + streaming stores, run-time selected) writes
+    the same floats and the same ranges as the portable loop, for every column
+    count (masked tails), destination alignment (streamed head / body / tail) and
+    special value (NaN skipped by the range, -0.0 vs 0.0 ties, f32 overflow);
+    n = 9000 is wider than the block buffer (the portable loop takes over)."""
+    import ctypes as C
+    from mjrl_amd import _lib
+    L = _lib.stage_lib()
+    if not L.mjrl_host_stage_avx512():
+        pytest.skip("no AVX-512 on this CPU")
+    rs = np.random.RandomState(n)
+    rows = 3 if n == 9000 else 203
+    src = rs.standard_normal((rows, n)) * np.logspace(-3, 3, n)
+    src[1, 0] = np.nan
+    src[2, -1] = -0.0
+    src[0, -1] = 0.0
+    src[-1, n // 2] = 1e300
+    for shift in (0, 1, 5, 15):   # destination misalignment in floats
+        outs = []
+        for fn in (L.mjrl_host_stage_f64, L.mjrl_host_stage_f64_portable):
+            buf = np.zeros(rows * n + 32, np.float32)
+            dst = buf[shift:shift + rows * n]
+            lo, hi = np.full(n, np.inf, np.float32), np.full(n, -np.inf, np.float32)
+            assert fn(src.ctypes.data, rows, n, dst.ctypes.data, lo.ctypes.data, hi.ctypes.data) == 0
+            outs.append((buf.copy(), lo, hi))
+        (b0, lo0, hi0), (b1, lo1, hi1) = outs
+        assert np.array_equal(b0.view(np.uint32), b1.view(np.uint32))     # bit for bit, padding untouched
+        assert np.array_equal(lo0.view(np.uint32), lo1.view(np.uint32))
+        assert np.array_equal(hi0.view(np.uint32), hi1.view(np.uint32))
+        assert np.array_equal(b0[shift:shift + rows * n].reshape(rows, n), src.astype(np.float32), equal_nan=True)
+
+
 def test_staging_chunks_fold_ranges(lib):
     """_PinnedStaging folds the per-chunk ranges of many chunks (device-free part:
     the chunk fills, driven directly)."""

@@ -385,6 +385,10 @@ int mjrl_policy_mean(const mjrl_shape* s, const float* obs, int64_t N, const flo
  * dst / cmin / cmax. */
 int mjrl_host_stage_f64(const double* src, int64_t rows, int32_t n, float* dst, float* cmin, float* cmax);
 int mjrl_host_stage_f32(const float* src, int64_t rows, int32_t n, float* dst, float* cmin, float* cmax);
+/* mjrl_host_stage_f64 over `count` arrays srcs[i] (rows[i] x n, row-major, f64)
+ * written one after another into dst: one call per chunk of paths. */
+int mjrl_host_stage_paths_f64(const double* const* srcs, const int64_t* rows, int32_t count, int32_t n, float* dst,
+                              float* cmin, float* cmax);
 /* The portable (non-AVX-512) path of mjrl_host_stage_f64, whatever the CPU, and
  * whether the CPU runs the AVX-512 path (1) or not (0); both for tests.  All the
  * mjrl_host_stage_* entry points are also in the host-only lib/libmjrl_stage.so. */

@@ -96,6 +96,7 @@ SIGNATURES = {
     "mjrl_policy_mean": [SP, P, I64, P, P, P, P, P, P, P],
     "mjrl_host_stage_f64": [P, I64, I32, P, P, P],
     "mjrl_host_stage_f32": [P, I64, I32, P, P, P],
+    "mjrl_host_stage_paths_f64": [P, P, I32, I32, P, P, P],
     "mjrl_host_stage_f64_portable": [P, I64, I32, P, P, P],
     "mjrl_host_stage_avx512": [],
 }
@@ -130,7 +131,8 @@ def load(path=None):
 
 
 STAGE_LIB_PATH = os.path.join(HERE, "lib", "libmjrl_stage.so")
-STAGE_FUNCS = ("mjrl_host_stage_f64", "mjrl_host_stage_f32", "mjrl_host_stage_f64_portable", "mjrl_host_stage_avx512")
+STAGE_FUNCS = ("mjrl_host_stage_f64", "mjrl_host_stage_f32", "mjrl_host_stage_paths_f64",
+               "mjrl_host_stage_f64_portable", "mjrl_host_stage_avx512")
 _STAGE = None
 
 

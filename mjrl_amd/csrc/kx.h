@@ -264,6 +264,12 @@ __device__ __forceinline__ void wstore(const float (&v)[IR], char* img, int imgb
     }
 }
 
+#ifdef MJRL_KX_ABL_NOCHAIN
+constexpr bool KX_ABL_NOCHAIN = true;    // timing ablation only: the FVP's P2-P5 skipped (barriers kept)
+#else
+constexpr bool KX_ABL_NOCHAIN = false;
+#endif
+
 template <int MP, int KG, int MODE>
 __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
     // multiply-add chains in this kernel contract to FMA (the reference-order
@@ -572,6 +578,9 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
 
         // ---- P1: first layer, partial over this wave's observation half ----
         floatx4 acc1[2] = {zero4(), zero4()};
+#ifdef MJRL_KX_ABL_NOP1
+        if (MODE != FVP)   // timing ablation only: the FVP's first-layer products skipped
+#endif
         {
 #pragma unroll
             for (int s = 0; s < KS; ++s) {
@@ -627,7 +636,7 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
         }
 
         // ---- P2: layer 1, wave -> (rb = kh, cb) ----
-        {
+        if (!(KX_ABL_NOCHAIN && MODE == FVP)) {
             const int j = cb * 16 + lr16;
             floatx4 acc = zero4();
             float rinv = 1.f;
@@ -694,7 +703,7 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
         KX_STAMP(3);
 
         // ---- P3: output layer [32 x MP], waves < 2 * MP/16 -> (rb3, cbo3) ----
-        if (w < 2 * (MP / 16)) {
+        if (w < 2 * (MP / 16) && !(KX_ABL_NOCHAIN && MODE == FVP)) {
             floatx4 acc = zero4();
             if (MODE == FVP) {
                 // D1 W2^T (W2c, folded) + a1 dW2^T (dW2r)
@@ -774,7 +783,7 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
 
         xload(tile + gridDim.x, ltid, 0, L::XPER / 2);   // first half of the next tile's xhat
         // ---- P4: gu1 = (1 - a1^2) (gp W2), wave -> (rb = kh, cb) ----
-        {
+        if (!(KX_ABL_NOCHAIN && MODE == FVP)) {
             const int hcol = cb * 16 + lr16;
             half8 ah[1], al[1];
             const float rinv = adyn<1>(GPf, L::LDG, kh, lq, lr16, nullptr, ah, al);
@@ -819,7 +828,7 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
                 for (int rr = 0; rr < 4; ++rr) g2[rr] += t[rr] * s4[rr];
             }
         };
-        if (MODE == FVP) gw2_sum();
+        if (MODE == FVP && !KX_ABL_NOCHAIN) gw2_sum();
         __syncthreads();
         KX_STAMP(6);
         // ---- P5: gu0 = (1 - a0^2) (gu1 W1), times the xhat row scale; beside it the
@@ -877,14 +886,19 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
         };
         // (running the two halves in opposite orders on the two waves of a SIMD,
         // kh = 0 / 1, measured 0.5 %: the phase is issue-bound, not latency-bound)
-        p5_gu0();
-        p5_gw();
+        if (!(KX_ABL_NOCHAIN && MODE == FVP)) {
+            p5_gu0();
+            p5_gw();
+        }
         if (MODE != FVP) gw2_sum();
         __syncthreads();
         KX_STAMP(7);
 
         // ---- P6: the gW0 sums ----
         KX_STAMP(10);
+#ifdef MJRL_KX_ABL_NOP6
+        if (false)   // timing ablation only (the two-kernel decomposition): results are wrong
+#endif
         {
             // gW0 (xhat transposed reads)
             half8 gh, gl;

@@ -126,7 +126,7 @@ MJRL_AVX512 inline void strip(const S* __restrict__ src, int64_t r0, int64_t r1,
     }
 }
 
-template <typename S, bool RANGE>
+template <typename S, bool RANGE, bool PREFETCH = true>
 MJRL_AVX512 int stage_avx512(const S* __restrict__ src, int64_t rows, int32_t n, float* __restrict__ dst,
                              float* __restrict__ cmin, float* __restrict__ cmax) {
     constexpr int BUF = 8192;   // floats of the block buffer (32 KB: stays in L1 / L2)
@@ -138,6 +138,15 @@ MJRL_AVX512 int stage_avx512(const S* __restrict__ src, int64_t rows, int32_t n,
     const __mmask16 tail = (__mmask16)(n % 16 ? (1u << (n % 16)) - 1 : 0xffff);
     for (int64_t r0 = 0; r0 < rows; r0 += rb) {
         const int64_t r1 = r0 + rb < rows ? r0 + rb : rows;
+        // the next block's source lines requested now (one contiguous run of rb
+        // rows), so the strips below find them in L2: the strips' short strided
+        // pieces (rb rows x 192 columns) are not a stream the hardware prefetcher
+        // follows
+        if (PREFETCH && r1 < rows) {
+            const char* p = reinterpret_cast<const char*>(src + r1 * n);
+            const int64_t nb = ((r1 + rb < rows ? r1 + rb : rows) - r1) * n * (int64_t)sizeof(S);
+            for (int64_t o = 0; o < nb; o += 64) _mm_prefetch(p + o, _MM_HINT_T1);
+        }
         // strip by strip over the block: the block's source (rb rows) stays in the
         // core's caches between strips, the ranges in registers within one
         for (int c0 = 0; c0 < n; c0 += 16 * NCH) strip<S, RANGE, NCH>(src, r0, r1, n, c0, nc, tail, buf, cmin, cmax);
@@ -176,6 +185,20 @@ int mjrl_host_stage_f32(const float* src, int64_t rows, int32_t n, float* dst, f
     return stage_rows(src, rows, n, dst, cmin, cmax);
 }
 
+// `count` row-major arrays (srcs[i]: rows[i] x n) converted one after another into
+// dst, one call per chunk of paths instead of one per path (a path of the action
+// slot is 17 x 1000 values: per-call overhead, not bandwidth, set its time).
+int mjrl_host_stage_paths_f64(const double* const* srcs, const int64_t* rows, int32_t count, int32_t n, float* dst,
+                              float* cmin, float* cmax) {
+    if (count < 0 || (count > 0 && (!srcs || !rows))) return MJRL_EINVAL;
+    for (int32_t i = 0; i < count; ++i) {
+        const int rc = stage_rows(srcs[i], rows[i], n, dst, cmin, cmax);
+        if (rc != MJRL_OK) return rc;
+        dst += rows[i] * (int64_t)n;
+    }
+    return MJRL_OK;
+}
+
 // The portable loop, callable whatever the CPU (tests compare the two paths).
 int mjrl_host_stage_f64_portable(const double* src, int64_t rows, int32_t n, float* dst, float* cmin, float* cmax) {
     if (rows < 0 || n <= 0 || (rows > 0 && (!src || !dst))) return MJRL_EINVAL;
@@ -184,5 +207,14 @@ int mjrl_host_stage_f64_portable(const double* src, int64_t rows, int32_t n, flo
 }
 
 int mjrl_host_stage_avx512(void) { return have_avx512() ? 1 : 0; }
+
+// The AVX-512 path without the next-block prefetch (tools/stage_convert_probe.py A/B).
+int mjrl_host_stage_f64_nopf(const double* src, int64_t rows, int32_t n, float* dst, float* cmin, float* cmax) {
+    if (rows < 0 || n <= 0 || (rows > 0 && (!src || !dst))) return MJRL_EINVAL;
+    if ((cmin == nullptr) != (cmax == nullptr)) return MJRL_EINVAL;
+    if (rows == 0 || !have_avx512()) return stage_portable(src, rows, n, dst, cmin, cmax);
+    return cmin ? stage_avx512<double, true, false>(src, rows, n, dst, cmin, cmax)
+                : stage_avx512<double, false, false>(src, rows, n, dst, cmin, cmax);
+}
 
 }  // extern "C"

@@ -90,6 +90,34 @@ def host_stage(arrs, view, offs, a0, a1, lo=None, hi=None):
     if view.dtype == np.float32 and view.ndim == 2:
         L = _lib.stage_lib()
         fns = {np.dtype(np.float64): L.mjrl_host_stage_f64, np.dtype(np.float32): L.mjrl_host_stage_f32}
+        # the common case, every array of the chunk C-contiguous f64 of the view's
+        # width: one native call for the whole chunk
+        srcs = [np.asarray(arrs[i]) for i in range(a0, a1)]
+        n = view.shape[1]
+        if srcs and all(a.dtype == np.float64 and a.ndim == 2 and a.shape[1] == n and a.flags.c_contiguous
+                        and a.shape[0] == offs[i + 1] - offs[i] for i, a in zip(range(a0, a1), srcs)):
+            k = len(srcs)
+            ptrs = (C.c_void_p * k)(*[a.ctypes.data for a in srcs])
+            rows = (C.c_int64 * k)(*[a.shape[0] for a in srcs])
+            dst = view[offs[a0]:offs[a1]]
+            if dst.shape[0]:
+                _lib.check(L.mjrl_host_stage_paths_f64(ptrs, rows, k, n, dst.ctypes.data,
+                                                       None if lo is None else lo.ctypes.data,
+                                                       None if hi is None else hi.ctypes.data), "mjrl_host_stage")
+            return
+    elif a1 > a0:
+        # other slots (1-D rewards / offsets / flags, f64 observations): one
+        # numpy concatenate per chunk (a copyto per path cost ~25 us each: 25 ms
+        # summed over the 1000 reward arrays of a 1M-row batch)
+        srcs = [np.asarray(arrs[i]) for i in range(a0, a1)]
+        if all(a.dtype == view.dtype and a.shape[1:] == view.shape[1:] and a.shape[0] == offs[i + 1] - offs[i]
+               for i, a in zip(range(a0, a1), srcs)):
+            np.concatenate(srcs, out=view[offs[a0]:offs[a1]])
+            if lo is not None and view.ndim == 2 and offs[a1] > offs[a0]:
+                dst = view[offs[a0]:offs[a1]]
+                np.fmin(lo, np.nanmin(dst, axis=0), out=lo)
+                np.fmax(hi, np.nanmax(dst, axis=0), out=hi)
+            return
     for i in range(a0, a1):
         dst = view[offs[i]:offs[i + 1]]
         if dst.shape[0] == 0:
@@ -232,11 +260,14 @@ class _PinnedStaging:
         cur = torch.cuda.current_stream(device)
         cs = self._copy_stream(device)
         cs.wait_stream(cur)   # a reused device slot may still be read by queued work
-        # chunks of whole arrays of about CHUNK_BYTES each
+        # chunks of whole arrays of about CHUNK_BYTES each, and at least two per
+        # staging thread (a narrow slot, e.g. the actions, in a few 16 MB chunks
+        # left most threads idle: 10.5 ms for 68 MB, tools/stage_convert_probe.py)
+        cb = max(1 << 20, min(self.CHUNK_BYTES, nbytes // (2 * _host_threads())))
         bounds, acc, r0 = [0], 0, 0
         for i, r in enumerate(rows):
             acc += r * width * dtype.itemsize
-            if acc >= self.CHUNK_BYTES:
+            if acc >= cb:
                 bounds.append(i + 1)
                 acc = 0
         if bounds[-1] != len(rows):

@@ -85,7 +85,9 @@ for _ in range(4):
 t = sorted(ts)[1]
 print("read-only pass (numpy sum, threads): %.1f ms (%.1f GB/s)" % (t * 1e3, R * n * 8 / t / 1e9), flush=True)
 res = {}
-for name, fn in (("portable", SL.mjrl_host_stage_f64_portable), ("avx512", SL.mjrl_host_stage_f64)):
+SL.mjrl_host_stage_f64_nopf.argtypes = SL.mjrl_host_stage_f64.argtypes
+for name, fn in (("portable", SL.mjrl_host_stage_f64_portable), ("avx512", SL.mjrl_host_stage_f64),
+                 ("avx512-nopf", SL.mjrl_host_stage_f64_nopf)):
     for ranges in (True, False):
         ts = []
         for _ in range(4):
@@ -117,3 +119,36 @@ for _ in range(4):
     torch.cuda.synchronize()
     ts.append(time.perf_counter() - t)
 print("engine stage (convert || h2d, ranges): %.1f ms (median of 4)" % (sorted(ts)[1] * 1e3), flush=True)
+
+# the bench's e2e staging call: every slot of a DeviceBatch (obs with ranges, act,
+# rewards, offsets, flags) and the device LinearBaseline predict
+from mjrl_amd.baselines.linear_baseline import LinearBaseline  # noqa: E402
+from mjrl_amd.utils.gym_env import EnvSpec  # noqa: E402
+acts = [rs.randn(L, 17) for _ in range(P)]
+pd = [dict(observations=o, actions=a, rewards=rs.randn(L), terminated=False) for o, a in zip(paths, acts)]
+base = LinearBaseline(EnvSpec(n, 17, L, 1))
+base._coeffs = rs.randn(n + 4) * 0.01
+for _ in range(2):
+    engine.DeviceBatch.from_paths(pd, dev, baseline=base, reuse=True)
+ts = []
+for _ in range(4):
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    engine.DeviceBatch.from_paths(pd, dev, baseline=base, reuse=True)
+    torch.cuda.synchronize()
+    ts.append(time.perf_counter() - t)
+print("DeviceBatch.from_paths (all slots + device baseline): %.1f ms (median of 4)" % (sorted(ts)[1] * 1e3))
+st.trace = tr = []
+t0 = time.perf_counter()
+engine.DeviceBatch.from_paths(pd, dev, baseline=base, reuse=True)
+torch.cuda.synchronize()
+st.trace = None
+by = {}
+for c in tr:
+    if c["fill"]:
+        d = by.setdefault(c["slot"], [1e9, 0, 0.0])
+        d[0] = min(d[0], c["fill"][0] - t0)
+        d[1] = max(d[1], c["fill"][1] - t0)
+        d[2] += c["fill"][1] - c["fill"][0]
+for k, (a, b, busy) in by.items():
+    print("  slot %-6s fill span %.1f -> %.1f ms, summed chunk fill %.1f ms" % (k, a * 1e3, b * 1e3, busy * 1e3))

@@ -614,7 +614,7 @@ def main():
     # (algorithmic flops at the matrix peak of the form it computes in) and its ideal
     # HBM time (algorithmic bytes at 8 TB/s)
     t_dom = kern[dom]["avg_ms"] * 1e-3
-    peak_mm = PEAK_SPLIT if eng.split else PEAK_F32_MFMA
+    peak_mm = PEAK_SPLIT if eng.precision == "split" else PEAK_F32_MFMA
     flops_dom = (acc_fl if dom == acc_name else gat_fl) * rows_rank
     bytes_dom = fvp_bytes * rows_rank if dom == acc_name else None
     t_mm = flops_dom / (peak_mm * 1e12)
@@ -630,7 +630,7 @@ def main():
                 traffic_GBps=None if traffic is None else round(traffic / t_dom / 1e9, 1),
                 flops_per_timestep=acc_fl if dom == acc_name else gat_fl, rows_per_launch=rows_rank,
                 mfma_form="split-f16 (3 x v_mfma_f32_16x16x32_f16 per f32 product), peak %.1f TFLOP/s f32-equivalent"
-                          % PEAK_SPLIT if eng.split else "f32 (v_mfma_f32_16x16x4_f32)",
+                          % PEAK_SPLIT if eng.precision == "split" else "f32 (v_mfma_f32_16x16x4_f32)",
                 ideal_ms=dict(mfma=round(t_mm * 1e3, 4), hbm=round(t_hbm * 1e3, 4)),
                 achieved_tflops=round(flops_dom / t_dom / 1e12, 3),
                 launches=len(samples), kernels={k: {kk: round(vv, 4) for kk, vv in v.items()}
@@ -640,10 +640,10 @@ def main():
     ut = ufl * T_total / (elapsed / args.steps) / 1e12
     # priced against the peak of the form the kernels compute in (split-f16: three
     # f16 MFMAs per f32 product, PEAK_SPLIT), not the exact-f32 matrix peak
-    peak_u = PEAK_SPLIT if eng.split else PEAK_F32_MFMA
+    peak_u = PEAK_SPLIT if eng.precision == "split" else PEAK_F32_MFMA
     roof["update"] = dict(flops_per_timestep=ufl, achieved=round(ut, 3), unit="TFLOP/s",
                           peak=round(peak_u * world, 1), frac=round(ut / (peak_u * world), 4),
-                          peak_form="split-f16 (f32-equivalent)" if eng.split else "exact f32 MFMA",
+                          peak_form="split-f16 (f32-equivalent)" if eng.precision == "split" else "exact f32 MFMA",
                           frac_of_exact_f32_peak=round(ut / (PEAK_F32_MFMA * world), 4),
                           note="algorithmic FLOPs of a whole update / wall time per update, vs n_gpus x the "
                                "matrix peak of the form the kernels use (frac); frac_of_exact_f32_peak prices "
@@ -651,7 +651,7 @@ def main():
 
     # the same update on the exact-f32 MFMA kernels (precision='f32'), for reference
     f32_ms = None
-    if world == 1 and eng.split and not args.no_f32:
+    if world == 1 and eng.precision == "split" and not args.no_f32:
         log("exact-f32 companion timing")
         e32 = UpdateEngine(n, m, hidden, device=device, precision="f32")
         e32.graphs = eng.graphs
@@ -675,7 +675,7 @@ def main():
                    vs_baseline=round(T_total * args.steps / elapsed / REF_CPU[args.config][0], 1)
                    if args.config in REF_CPU and not args.paths else None,
                    vs_baseline_source=REF_CPU[args.config][1] if args.config in REF_CPU and not args.paths else None,
-                   dtype="f32" if not eng.split else "f32 (split-f16 MFMA, f32 accumulate)",
+                   dtype="f32" if eng.precision != "split" else "f32 (split-f16 MFMA, f32 accumulate)",
                    data="synthetic (seeded N(0,1) obs/act/rewards, LinearBaseline fitted on 20 paths)",
                    config=dict(workload=cfg["workload"], obs_dim=n, act_dim=m, hidden=list(hidden),
                                algo=cfg["algo"], timesteps=T_total, paths=cfg["paths"], horizon=H,

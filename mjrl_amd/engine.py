@@ -588,6 +588,7 @@ class UpdateEngine:
         if prec == "split" and not can_split:
             raise ValueError("split precision is not available for this policy shape")
         self.split = can_split and prec != "f32"
+        self.precision = "split" if self.split else "f32"   # the form the policy products compute in
 
     # ------------------------------------------------------------------
     @property

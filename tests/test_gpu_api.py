@@ -779,3 +779,35 @@ def test_pack_split_f32_input_matches_f64(n):
 def _lib_stream():
     from mjrl_amd import _lib
     return _lib.stream_ptr()
+
+
+@pytest.mark.parametrize("reuse", [False, True])
+def test_staged_batch_matches_numpy(reuse):
+    """DeviceBatch.from_paths on the GPU: numpy f64 sampler
+    paths -> the host convert-and-range pass (AVX-512 streaming path where the CPU
+    has it, one native call per chunk of paths) -> pinned slabs -> chunked H2D.
+    The staged observations / actions are numpy's f32 cast bit for bit (the
+    reference's torch .float() of the concatenation, gaussian_mlp.py:103), rewards,
+    offsets and flags exact, the column ranges the f32 min / max; enough paths of
+    uneven lengths for many chunks, odd widths for the masked vector tails."""
+    from mjrl_amd.engine import DeviceBatch
+    rs = np.random.RandomState(7)
+    n, m = 45, 7
+    lengths = rs.randint(1, 900, size=300)
+    paths = [dict(observations=rs.randn(h, n) * np.logspace(-3, 3, n), actions=rs.randn(h, m),
+                  rewards=rs.randn(h), terminated=bool(i % 3 == 0)) for i, h in enumerate(lengths)]
+    paths[5]["observations"][3, 7] = np.nan
+    dev = torch.device("cuda:0")
+    for _ in range(2):   # the second call reuses the pinned slabs (and, with reuse, the device slots)
+        b = DeviceBatch.from_paths(paths, dev, baseline=None, reuse=reuse)
+        torch.cuda.synchronize()
+        obs = np.concatenate([p["observations"] for p in paths]).astype(np.float32)
+        act = np.concatenate([p["actions"] for p in paths]).astype(np.float32)
+        assert np.array_equal(b.obs.cpu().numpy(), obs, equal_nan=True)
+        assert np.array_equal(b.act.cpu().numpy(), act)
+        assert np.array_equal(b.rewards.cpu().numpy(), np.concatenate([p["rewards"] for p in paths]))
+        assert np.array_equal(b.path_off.cpu().numpy(), np.concatenate([[0], np.cumsum(lengths)]))
+        assert np.array_equal(b.terminated.cpu().numpy(), np.array([p["terminated"] for p in paths], np.uint8))
+        rng = b.obs_range.cpu().numpy()
+        np.testing.assert_array_equal(rng[0], np.nanmin(obs, axis=0))
+        np.testing.assert_array_equal(rng[1], np.nanmax(obs, axis=0))

@@ -80,6 +80,27 @@ def test_host_stage_avx512_equals_portable(lib, n):
         assert np.array_equal(b0[shift:shift + rows * n].reshape(rows, n), src.astype(np.float32), equal_nan=True)
 
 
+def test_host_stage_under_asan(tmp_path):
+    """csrc/stage.cpp built with the host AddressSanitizer and UBSan into the
+    driver tests/native/stage_asan.cpp and run over exactly-sized heap buffers:
+    masked tails, streamed heads at every misalignment, the next-block prefetch and
+    the batched per-chunk entry stay inside their buffers (ASan aborts otherwise)."""
+    import os
+    import shutil
+    import subprocess
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("no g++")
+    here = os.path.dirname(os.path.abspath(__file__))
+    exe = str(tmp_path / "stage_asan")
+    subprocess.run([gxx, "-O1", "-g", "-std=c++17", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
+                    "-fno-sanitize-recover=undefined", os.path.join(here, "native", "stage_asan.cpp"), "-o", exe],
+                   check=True, capture_output=True, timeout=180)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:verify_asan_link_order=0")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
 def test_staging_chunks_fold_ranges(lib):
     """_PinnedStaging folds the per-chunk ranges of many chunks (device-free part:
     the chunk fills, driven directly)."""

@@ -394,6 +394,11 @@ int mjrl_host_stage_paths_f64(const double* const* srcs, const int64_t* rows, in
  * mjrl_host_stage_* entry points are also in the host-only lib/libmjrl_stage.so. */
 int mjrl_host_stage_f64_portable(const double* src, int64_t rows, int32_t n, float* dst, float* cmin, float* cmax);
 int mjrl_host_stage_avx512(void);
+/* Same-type concatenation: `count` byte runs srcs[i] (nbytes[i] bytes) copied one
+ * after another into dst (the 1-D slots of a chunk of paths: rewards, advantages,
+ * host baseline predictions; npg_cg.py:87-89 concatenate).  One call per chunk,
+ * no Python per path. */
+int mjrl_host_gather(const void* const* srcs, const int64_t* nbytes, int32_t count, void* dst);
 
 #ifdef __cplusplus
 }

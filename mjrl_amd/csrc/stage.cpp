@@ -208,6 +208,21 @@ int mjrl_host_stage_f64_portable(const double* src, int64_t rows, int32_t n, flo
 
 int mjrl_host_stage_avx512(void) { return have_avx512() ? 1 : 0; }
 
+// The 1-D slots of a chunk (rewards, advantages, host predictions): np.concatenate
+// over a chunk's 125 reward arrays held the GIL across its per-array work, so the
+// staging threads ran those chunks one at a time (3.9 ms for the 8 MB of a 1M-row
+// batch, profiles/r05d/stage_probe4.txt); a native call releases it.
+int mjrl_host_gather(const void* const* srcs, const int64_t* nbytes, int32_t count, void* dst) {
+    if (count < 0 || (count > 0 && (!srcs || !nbytes || !dst))) return MJRL_EINVAL;
+    char* d = static_cast<char*>(dst);
+    for (int32_t i = 0; i < count; ++i) {
+        if (nbytes[i] < 0 || (nbytes[i] > 0 && !srcs[i])) return MJRL_EINVAL;
+        if (nbytes[i]) std::memcpy(d, srcs[i], (size_t)nbytes[i]);
+        d += nbytes[i];
+    }
+    return MJRL_OK;
+}
+
 // The AVX-512 path without the next-block prefetch (tools/stage_convert_probe.py A/B).
 int mjrl_host_stage_f64_nopf(const double* src, int64_t rows, int32_t n, float* dst, float* cmin, float* cmax) {
     if (rows < 0 || n <= 0 || (rows > 0 && (!src || !dst))) return MJRL_EINVAL;

@@ -112,7 +112,16 @@ def host_stage(arrs, view, offs, a0, a1, lo=None, hi=None):
         srcs = [np.asarray(arrs[i]) for i in range(a0, a1)]
         if all(a.dtype == view.dtype and a.shape[1:] == view.shape[1:] and a.shape[0] == offs[i + 1] - offs[i]
                for i, a in zip(range(a0, a1), srcs)):
-            np.concatenate(srcs, out=view[offs[a0]:offs[a1]])
+            dst = view[offs[a0]:offs[a1]]
+            if lo is None and dst.flags.c_contiguous and all(a.flags.c_contiguous for a in srcs):
+                # one native call per chunk (ctypes releases the GIL; np.concatenate
+                # holds it across the chunk's per-array work)
+                k = len(srcs)
+                ptrs = (C.c_void_p * k)(*[a.ctypes.data for a in srcs])
+                nb = (C.c_int64 * k)(*[a.nbytes for a in srcs])
+                _lib.check(_lib.stage_lib().mjrl_host_gather(ptrs, nb, k, dst.ctypes.data), "mjrl_host_gather")
+                return
+            np.concatenate(srcs, out=dst)
             if lo is not None and view.ndim == 2 and offs[a1] > offs[a0]:
                 dst = view[offs[a0]:offs[a1]]
                 np.fmin(lo, np.nanmin(dst, axis=0), out=lo)

@@ -36,6 +36,17 @@ def test_every_declared_symbol_is_exported(lib):
     assert set(names) <= set(_lib.SIGNATURES), set(names) - set(_lib.SIGNATURES)
 
 
+def test_stage_lib_exports_every_host_entry_point(lib):
+    """The host-only lib/libmjrl_stage.so carries every mjrl_host_* entry point the
+    header declares (the pool controller loads only it)."""
+    from mjrl_amd import _lib
+    host = [n for n in declared() if n.startswith("mjrl_host_")]
+    assert set(host) == set(_lib.STAGE_FUNCS)
+    S = _lib.stage_lib()
+    for n in host:
+        assert hasattr(S, n), n
+
+
 @pytest.mark.parametrize("n,m,h,np_,mp,d", [
     (6, 2, (0, 0), 16, 16, 16),            # point_mass, linear policy
     (8, 2, (64, 64), 16, 16, 4868),        # swimmer

@@ -101,6 +101,24 @@ def test_host_stage_under_asan(tmp_path):
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
 
 
+@pytest.mark.parametrize("dtype", [np.float64, np.int64, np.uint8])
+def test_host_gather_concatenates_1d_slots(lib, dtype):
+    """1-D slots (rewards, offsets, flags) go through mjrl_host_gather: the same
+    bytes as np.concatenate, for empty arrays too; a non-contiguous array falls
+    back to numpy."""
+    from mjrl_amd.engine import host_stage
+    rs = np.random.RandomState(5)
+    arrs = [(rs.standard_normal(h) * 100).astype(dtype) for h in (1000, 0, 7, 1, 333)]
+    arrs.append((rs.standard_normal(40) * 100).astype(dtype)[::2])   # strided
+    offs = np.concatenate([[0], np.cumsum([len(a) for a in arrs])])
+    view = np.zeros(offs[-1], dtype)
+    host_stage(arrs, view, offs, 0, 5)
+    host_stage(arrs, view, offs, 5, 6)
+    assert np.array_equal(view.view(np.uint8), np.concatenate(arrs).view(np.uint8))
+    from mjrl_amd import _lib
+    assert _lib.stage_lib().mjrl_host_gather(None, None, -1, None) != 0
+
+
 def test_staging_chunks_fold_ranges(lib):
     """_PinnedStaging folds the per-chunk ranges of many chunks (device-free part:
     the chunk fills, driven directly)."""

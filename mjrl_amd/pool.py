@@ -116,14 +116,20 @@ def _segment_dtype(agent):
     return np.float32 if (f32 and dev_fit) else np.float64
 
 
-def _fill_shard(buf, L, sh, lengths, ex=None, chunk_rows=1 << 16):
+def _fill_shard(buf, L, sh, lengths, ex=None, chunk_rows=None):
     """The shard's paths `sh` into its segment.  float32 layouts: the native
     convert-and-range pass (engine.host_stage, the staging path's own) writes
     obs / act and the per-column (min, max) of obs into 'orange'.  ex: a thread
-    pool; the paths are then cut into chunks of about chunk_rows timesteps,
-    converted in parallel (ctypes / numpy release the GIL), their ranges folded."""
+    pool; the paths are then cut into chunks of about chunk_rows timesteps
+    (default: two chunks per pool thread, at least 1024 rows; a fixed 64k rows
+    left half of 16 threads idle on a 500k-row shard), converted in parallel
+    (ctypes releases the GIL), their ranges folded; the 1-D slots go through the
+    same native gather as the staging path's."""
     lengths = np.asarray(lengths, dtype=np.int64)
     offs = np.concatenate([[0], np.cumsum(lengths)])
+    if chunk_rows is None:
+        nthr = getattr(ex, "_max_workers", 1) if ex is not None else 1
+        chunk_rows = max(1024, int(offs[-1]) // (2 * nthr) if nthr > 1 else 1 << 16)
     bounds = [0]
     for i in range(len(sh)):
         if offs[i + 1] - offs[bounds[-1]] >= chunk_rows:
@@ -154,12 +160,13 @@ def _fill_shard(buf, L, sh, lengths, ex=None, chunk_rows=1 << 16):
         for k in range(nchunk):
             conv(k)
     if sh:
+        from .engine import host_stage
         if f32:
             o = L.view(buf, "orange").reshape(2, L.n)
             o[0], o[1] = rng[:, 0].min(axis=0), rng[:, 1].max(axis=0)
-        np.concatenate([np.asarray(p["rewards"], np.float64) for p in sh], out=L.view(buf, "rew"))
+        host_stage([np.asarray(p["rewards"], np.float64) for p in sh], L.view(buf, "rew"), offs, 0, len(sh))
         if L.fields["adv_in"][1]:
-            np.concatenate([np.asarray(p["advantages"], np.float64) for p in sh], out=L.view(buf, "adv_in"))
+            host_stage([np.asarray(p["advantages"], np.float64) for p in sh], L.view(buf, "adv_in"), offs, 0, len(sh))
     L.view(buf, "lengths")[:] = lengths
     L.view(buf, "term")[:] = [int(bool(p.get("terminated", False))) for p in sh]
 

@@ -4,7 +4,8 @@
 TAG=${1:-chk}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
-timeout -k 10 1000 python3 -m pytest tests/ -x -q -m gpu -p no:cacheprovider > $OUT/pytest.log 2>&1   # the driver's exact command || { echo "PYTEST FAILED"; tail -30 $OUT/pytest.log; exit 1; }
+# the driver's exact command
+timeout -k 10 1000 python3 -m pytest tests/ -x -q -m gpu -p no:cacheprovider > $OUT/pytest.log 2>&1 || { echo "PYTEST FAILED"; tail -30 $OUT/pytest.log; exit 1; }
 tail -3 $OUT/pytest.log
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo "SMOKE FAILED"; cat $OUT/smoke.log; exit 1; }
 cat $OUT/smoke.log

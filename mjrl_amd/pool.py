@@ -116,20 +116,19 @@ def _segment_dtype(agent):
     return np.float32 if (f32 and dev_fit) else np.float64
 
 
-def _fill_shard(buf, L, sh, lengths, ex=None, chunk_rows=None):
+def _fill_shard(buf, L, sh, lengths, ex=None, chunk_rows=None, threads=1):
     """The shard's paths `sh` into its segment.  float32 layouts: the native
     convert-and-range pass (engine.host_stage, the staging path's own) writes
     obs / act and the per-column (min, max) of obs into 'orange'.  ex: a thread
     pool; the paths are then cut into chunks of about chunk_rows timesteps
-    (default: two chunks per pool thread, at least 1024 rows; a fixed 64k rows
-    left half of 16 threads idle on a 500k-row shard), converted in parallel
+    (default: two chunks per pool thread, `threads` of them, at least 1024 rows;
+    a fixed 64k rows left half of 16 threads idle on a 500k-row shard), converted in parallel
     (ctypes releases the GIL), their ranges folded; the 1-D slots go through the
     same native gather as the staging path's."""
     lengths = np.asarray(lengths, dtype=np.int64)
     offs = np.concatenate([[0], np.cumsum(lengths)])
     if chunk_rows is None:
-        nthr = getattr(ex, "_max_workers", 1) if ex is not None else 1
-        chunk_rows = max(1024, int(offs[-1]) // (2 * nthr) if nthr > 1 else 1 << 16)
+        chunk_rows = max(1024, int(offs[-1]) // (2 * threads)) if ex is not None and threads > 1 else 1 << 16
     bounds = [0]
     for i in range(len(sh)):
         if offs[i + 1] - offs[bounds[-1]] >= chunk_rows:
@@ -349,7 +348,8 @@ class DevicePool:
         if getattr(self, "_fillex", None) is None:
             import concurrent.futures as cf
             from .engine import _host_threads
-            self._fillex = cf.ThreadPoolExecutor(_host_threads(16 * self.world), thread_name_prefix="mjrl_fill")
+            self._fill_threads = _host_threads(16 * self.world)
+            self._fillex = cf.ThreadPoolExecutor(self._fill_threads, thread_name_prefix="mjrl_fill")
         return self._fillex
 
     # ---- one update -------------------------------------------------------------
@@ -381,7 +381,8 @@ class DevicePool:
                 # (H2D) and starts its update while the controller fills shard r + 1
                 p0, p1 = parts[r]
                 L = _Layout(int(lengths[p0:p1].sum()), p1 - p0, n, m, with_adv, dtype)
-                _fill_shard(self._segment(r, L.nbytes).buf, L, paths[p0:p1], lengths[p0:p1], self._fill_pool())
+                _fill_shard(self._segment(r, L.nbytes).buf, L, paths[p0:p1], lengths[p0:p1], self._fill_pool(),
+                            threads=self._fill_threads)
                 layouts.append(L)
                 self._conns[r].send(("step", dict(state=state, shm=self._shm[r].name, T=L.T, P=L.P, n=n, m=m,
                                                   dtype=L.dtype.str, mode=mode, gamma=gamma, gae_lambda=gae_lambda,

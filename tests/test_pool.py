@@ -148,7 +148,8 @@ def test_fill_shard_layouts():
     import concurrent.futures as cf
     ex = cf.ThreadPoolExecutor(4)
     for dt, kw in ((np.float64, {}), (np.float32, {}), (np.float64, dict(ex=ex, chunk_rows=20)),
-                   (np.float32, dict(ex=ex, chunk_rows=20))):   # one chunk / several chunks in parallel
+                   (np.float32, dict(ex=ex, chunk_rows=20)),    # one chunk / several chunks in parallel
+                   (np.float32, dict(ex=ex, threads=4))):       # the default chunking (two per thread)
         L = _Layout(int(lengths.sum()), len(paths), N_OBS, N_ACT, True, dt)
         buf = bytearray(L.nbytes)
         _fill_shard(buf, L, paths, lengths, **kw)

@@ -1,4 +1,4 @@
-"""world_size-2 gloo test of the sharded update's collective schedule (CPU).
+"""world_size-2 / -4 gloo tests of the sharded update's collective schedule (CPU).
 
 Every rank takes its shard of a golden batch (mjrl_amd.comm.partition_paths),
 computes the per-shard quantities the device kernels produce (the local moment
@@ -76,10 +76,9 @@ def _worker(rank, world, port, name, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name", ["c2_ragged", "c3_halfcheetah_trpo"])
-def test_sharded_schedule_equals_unsharded(name):
+@pytest.mark.parametrize("name,world", [("c2_ragged", 2), ("c3_halfcheetah_trpo", 2), ("c2_ragged", 4)])
+def test_sharded_schedule_equals_unsharded(name, world):
     from oracle import npg_cpu as O
-    world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -96,13 +95,15 @@ def test_sharded_schedule_equals_unsharded(name):
     c = O.load_case(os.path.join(GOLDEN, name + ".npz"))
     w = np.concatenate([out[r][0] for r in range(world)])
     np.testing.assert_allclose(w, c["adv_whitened"], rtol=1e-10, atol=1e-12)
-    np.testing.assert_allclose(out[0][1], c["base_stats"], rtol=1e-10)
-    np.testing.assert_allclose(out[1][1], c["base_stats"], rtol=1e-10)
-    g0, g1 = out[0][2], out[1][2]
-    assert np.array_equal(g0, g1)                                  # replicated after the all-reduce
+    for r in range(world):
+        np.testing.assert_allclose(out[r][1], c["base_stats"], rtol=1e-10)
+    g0 = out[0][2]
+    for r in range(1, world):
+        assert np.array_equal(out[r][2], g0)                       # replicated after the all-reduce
     assert np.linalg.norm(g0 - c["vpg_grad"]) / np.linalg.norm(c["vpg_grad"]) < 1e-5
-    x0, x1 = out[0][3], out[1][3]
-    assert np.array_equal(x0, x1)
+    x0 = out[0][3]
+    for r in range(1, world):
+        assert np.array_equal(out[r][3], x0)
     tol = max(1e-3, 3 * float(c["spread_x"]))
     assert np.linalg.norm(x0 - c["cg_x"]) / np.linalg.norm(c["cg_x"]) < tol
 

@@ -277,6 +277,20 @@ int mjrl_policy_eval(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_eval,
 int mjrl_vpg_accumulate(const mjrl_shape* s, const mjrl_rows* rows, const float* packed_theta,
                         const float* out_shift, const float* out_scale, const mjrl_scratch* sc,
                         void* stream);
+/* mjrl_vpg_accumulate / mjrl_policy_vpg with the batch assembly (a5,
+ * npg_cg.py:87-89; mjrl_pack_batch_split_f32 with null in_shift / in_scale) fused
+ * in: the forward pass reads the staged f32 observations obs[T][n] and writes the
+ * split rows rows->xs / rows->xu (outputs here; rows->xc must hold the column
+ * scales) bit for bit as the pack does, for the FVP and evaluation passes after
+ * it.  The identity input normalisation only (MuNet's default; with in_shift /
+ * in_scale, pack first).  Split shapes (mjrl_split_supported) with n % 4 == 0 and
+ * 16-byte-aligned obs / xs, else MJRL_ESHAPE; rows->act must hold f32 actions. */
+int mjrl_vpg_accumulate_pack(const mjrl_shape* s, const mjrl_rows* rows, const float* obs,
+                             const float* packed_theta, const float* out_shift, const float* out_scale,
+                             const mjrl_scratch* sc, void* stream);
+int mjrl_policy_vpg_pack(const mjrl_shape* s, const mjrl_rows* rows, const float* obs,
+                         const float* packed_theta, const float* out_shift, const float* out_scale,
+                         const mjrl_scratch* sc, float* gsum, void* stream);
 int mjrl_fvp_accumulate(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_fvp,
                         const float* packed_theta, const float* packed_v, const float* out_scale,
                         const int32_t* done, const mjrl_scratch* sc, void* stream);

@@ -74,6 +74,8 @@ SIGNATURES = {
     "mjrl_policy_fvp": [SP, C.POINTER(Rows), I64, P, P, P, C.POINTER(Scratch), P, P, P],
     "mjrl_policy_eval": [SP, C.POINTER(Rows), I64, P, P, P, P, C.POINTER(Scratch), P, P],
     "mjrl_vpg_accumulate": [SP, C.POINTER(Rows), P, P, P, C.POINTER(Scratch), P],
+    "mjrl_vpg_accumulate_pack": [SP, C.POINTER(Rows), P, P, P, P, C.POINTER(Scratch), P],
+    "mjrl_policy_vpg_pack": [SP, C.POINTER(Rows), P, P, P, P, C.POINTER(Scratch), P, P],
     "mjrl_fvp_accumulate": [SP, C.POINTER(Rows), I64, P, P, P, P, C.POINTER(Scratch), P],
     "mjrl_gather_grads": [SP, C.POINTER(Rows), I64, C.POINTER(Scratch), I32, P, P, P],
     "mjrl_fused_path": [SP],

@@ -270,7 +270,15 @@ constexpr bool KX_ABL_NOCHAIN = true;    // timing ablation only: the FVP's P2-P
 constexpr bool KX_ABL_NOCHAIN = false;
 #endif
 
-template <int MP, int KG, int MODE>
+// PACK (FWD only): the batch assembly (k_pack_split_q, a5) fused into the forward
+// pass: the tile's f32 observation rows are loaded instead of split rows and split
+// in the publish, with the pack's own f32 operations (bit-identical rows), which
+// also writes them to a.xs_w / a.xu_w for the FVP and EVAL passes.  The identity
+// input normalisation only (the policy's default; the division of a given
+// in_shift / in_scale spilled 115 registers here, so those batches keep the
+// separate pack); n_obs % 4 == 0 and 16-byte-aligned rows (mjrl_vpg_accumulate_pack
+// checks).
+template <int MP, int KG, int MODE, bool PACK = false>
 __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
     // multiply-add chains in this kernel contract to FMA (the reference-order
     // elementwise code lives in other kernels; -ffp-contract=off is the file default)
@@ -399,6 +407,14 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
         }
     }
     KX_PRE(4);
+    // PACK: 1 / xc of every column (exact: powers of two) in LDS (the D0B region,
+    // FVP-only), read by the tile publish
+    float* picx = D0B;
+    if constexpr (PACK) {
+        static_assert(MODE == FWD, "the fused pack is the forward pass's");
+        static_assert(NP * 4 <= L::BT * L::LD * 4, "pack table in the D0B region");
+        for (int k = tid; k < NP; k += KT) picx[k] = 1.f / a.xc[k];
+    }
     // a converged CG loop (cg_solve.py:19-20): checked once the preamble's loads have
     // been consumed (image stores, W0 slice split), so the flag's load overlaps them
     if (MODE == FVP && a.done && *a.done) return;
@@ -433,6 +449,19 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
         const int64_t rb_ = t_ * BT;
         const int row = tid_ >> 4, c16 = tid_ & 15;
         const bool ok = t_ < ntiles && rb_ + row < T;
+        if constexpr (PACK) {
+            // the f32 row's columns 8 ch .. 8 ch + 7 of the thread's chunks ch = c16 + 16 c
+            // (c < UH): pieces 2c, 2c + 1 (columns >= n_obs read as zero; n_obs % 4 == 0)
+            const float* src = a.obs32 + (ok ? (rb_ + row) * (int64_t)a.n_obs : 0);
+#pragma unroll
+            for (int u = 0; u < L::XPER; ++u)
+                if (u >= u0 && u < u1) {
+                    const int col = 8 * (c16 + 16 * (u >> 1)) + 4 * (u & 1);
+                    xn[u] = ok && col < a.n_obs ? *reinterpret_cast<const float4*>(src + col)
+                                                : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+            return;
+        }
         const char* src = reinterpret_cast<const char*>(a.xs) + (ok ? (rb_ + row) * (4 * NP) : 0);
 #pragma unroll
         for (int u = 0; u < L::XPER; ++u)
@@ -512,7 +541,54 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
 
         // ---- publish: xhat tile -> images, row scales; FVP: cached activations ----
         asm volatile("" ::"v"(touch[0]), "v"(touch[1]));
-        {
+        if constexpr (PACK) {
+            // the pack (k_pack_split_q) of this thread's 24 columns of its row: the bias
+            // column 1 -> / xc; the row's power-of-two scale over its 16 lanes; hi / lo to
+            // the images and to the split rows in HBM
+#pragma clang fp contract(off)
+            constexpr int UH = NP / 128;
+            const int row = ltid >> 4, c16 = ltid & 15;
+            const bool ok = row < nrow;
+            float8v v[UH];
+            float mx = 0.f;
+#pragma unroll
+            for (int c = 0; c < UH; ++c) {
+                const int c0 = 8 * (c16 + 16 * c);
+                v[c] = float8v{xn[2 * c].x, xn[2 * c].y, xn[2 * c].z, xn[2 * c].w,
+                               xn[2 * c + 1].x, xn[2 * c + 1].y, xn[2 * c + 1].z, xn[2 * c + 1].w};
+                const float8v ic = load8(picx + c0);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    if (c0 + e == a.n_obs && ok) v[c][e] = 1.f;   // bias column (rows past T stay zero)
+                    v[c][e] *= ic[e];
+                }
+                mx = fmaxf(mx, absmax8(v[c]));
+            }
+            mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
+            mx = fmaxf(mx, __shfl_xor(mx, 2, 64));
+            mx = fmaxf(mx, __shfl_xor(mx, 4, 64));
+            mx = fmaxf(mx, __shfl_xor(mx, 8, 64));
+            float inv;
+            const float sc = pow2_scale(mx, inv);
+            char* dst = XHb + row * L::RBYTES + 16 * (c16 ^ chunk_swz(row));
+            _Float16* gdst = a.xs_w + (row_base + row) * (2 * (int64_t)NP);
+#pragma unroll
+            for (int c = 0; c < UH; ++c) {
+                half8 h, l;
+                split8(v[c], sc, h, l);
+                *reinterpret_cast<half8*>(dst + 256 * c) = h;
+                *reinterpret_cast<half8*>(dst + BT * L::RBYTES + 256 * c) = l;
+                if (ok) {
+                    const int c0 = 8 * (c16 + 16 * c);
+                    *reinterpret_cast<half8*>(gdst + c0) = h;
+                    *reinterpret_cast<half8*>(gdst + NP + c0) = l;
+                }
+            }
+            if (c16 == 0) {
+                Us[row] = inv;
+                if (ok) a.xu_w[row_base + row] = inv;
+            }
+        } else {
             const int row = ltid >> 4, c16 = ltid & 15;
             char* dst = XHb + row * L::RBYTES + 16 * (c16 ^ chunk_swz(row));
 #pragma unroll

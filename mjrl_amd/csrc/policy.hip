@@ -48,6 +48,13 @@ struct RowArgs {
     const void* xs;       // split-f16 xhat rows [T][hi NP | lo NP] (k_kx), or null
     const float* xu;      // [T] power-of-two row scales of xs
     const float* xc;      // [NP] power-of-two column scales of xs
+    // FWD with the batch assembly fused in (k_kx<.., FWD, true>): the staged f32
+    // observations [T][n_obs] (identity input normalisation), converted to the split
+    // rows in the tile publish, which also writes them to xs_w / xu_w
+    const float* obs32;
+    _Float16* xs_w;
+    float* xu_w;
+    int n_obs;
 };
 
 // rows per k_rows tile for a hidden width.  128-wide layers: 32 rows keep the f32
@@ -1337,10 +1344,10 @@ int launch_ks_t(const RowArgs& ra, const FOut& fo, int grid, hipStream_t st) {
     return (int)hipGetLastError();
 }
 
-template <int MP, int KG, int MODE>
+template <int MP, int KG, int MODE, bool PACK = false>
 int launch_kx_t(const RowArgs& ra, const FOut& fo, int grid, hipStream_t st) {
     using L = XLayout<MP, KG>;
-    auto fn = k_kx<MP, KG, MODE>;
+    auto fn = k_kx<MP, KG, MODE, PACK>;
     static bool attr = false;
     if (!attr) {
         hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, L::bytes);
@@ -1426,6 +1433,33 @@ int run_fused(int mode, const mjrl_shape* s, const mjrl_rows* r, int64_t T, cons
         return launch_ks<FVP>(s, ra, fo, G, st);
     }
     return mode == FWD ? launch_fused<FWD>(s, ra, fo, G, st) : launch_fused<FVP>(s, ra, fo, G, st);
+}
+
+// FWD with the fused batch assembly (k_kx<.., FWD, true>): the same workgroups and
+// slabs as run_fused's k_kx FWD
+int run_fwd_pack(const mjrl_shape* s, const mjrl_rows* r, int64_t T, const RowArgs& ra, const mjrl_scratch* sc,
+                 hipStream_t st) {
+    const int G = ks_grid(T);
+    JobSet js = make_jobs(s, r, G);
+    FOut fo{};
+    fo.wpart = sc->wpart;
+    fo.wcap = slab_floats(s, sc->slices);
+    fo.off0 = js.job[0].off;
+    fo.off1 = js.job[1].off;
+    fo.boff1 = js.job[1].boff;
+    fo.off2 = js.job[2].off;
+    fo.boff2 = js.job[2].boff;
+    fo.n = s->n;
+    fo.m = s->m;
+    const int kg = s->np / 32;
+#define MJRL_K(MP_, KG_) \
+    if (s->mp == MP_ && kg == KG_) return launch_kx_t<MP_, KG_, FWD, true>(ra, fo, G, st);
+#define MJRL_KN(MP_) MJRL_K(MP_, 4) MJRL_K(MP_, 8) MJRL_K(MP_, 12)
+    MJRL_KN(16)
+    MJRL_KN(32)
+#undef MJRL_KN
+#undef MJRL_K
+    return MJRL_ESHAPE;
 }
 
 int run_gather(const mjrl_shape* s, const mjrl_rows* r, int64_t T, const mjrl_scratch* sc, const double* lspart,
@@ -1614,6 +1648,37 @@ int mjrl_vpg_accumulate(const mjrl_shape* s, const mjrl_rows* rows, const float*
     int e = launch_rows<FWD>(s, ra, row_grid(s, T), st);
     if (e) return e;
     return run_wgrad_only(s, rows, T, sc, nullptr, st);
+}
+
+int mjrl_vpg_accumulate_pack(const mjrl_shape* s, const mjrl_rows* rows, const float* obs, const float* packed_theta,
+                             const float* out_shift, const float* out_scale, const mjrl_scratch* sc, void* stream) {
+    if (!rows_ok(s, rows) || !rows->xs || !obs || !packed_theta || !sc || !rows->act || !rows->adv_vpg ||
+        !rows->mu0 || !rows->ll0)
+        return MJRL_EINVAL;
+    if (!ksx_supported(s) || s->n % 4 || (reinterpret_cast<uintptr_t>(obs) & 15) ||
+        (reinterpret_cast<uintptr_t>(rows->xs) & 15))
+        return MJRL_ESHAPE;
+    const int64_t T = rows->T;
+    if (T == 0) return mjrl_vpg_accumulate(s, rows, packed_theta, out_shift, out_scale, sc, stream);
+    hipStream_t st = (hipStream_t)stream;
+    RowArgs ra = row_args(s, rows, T);
+    ra.P = packed_theta;
+    ra.out_shift = out_shift;
+    ra.out_scale = out_scale;
+    ra.rpart = sc->rpart;
+    ra.obs32 = obs;
+    ra.xs_w = (_Float16*)rows->xs;
+    ra.xu_w = const_cast<float*>(rows->xu);
+    ra.n_obs = s->n;
+    return run_fwd_pack(s, rows, T, ra, sc, st);
+}
+
+int mjrl_policy_vpg_pack(const mjrl_shape* s, const mjrl_rows* rows, const float* obs, const float* packed_theta,
+                         const float* out_shift, const float* out_scale, const mjrl_scratch* sc, float* gsum,
+                         void* stream) {
+    int e = mjrl_vpg_accumulate_pack(s, rows, obs, packed_theta, out_shift, out_scale, sc, stream);
+    if (e) return e;
+    return mjrl_gather_grads(s, rows, rows->T, sc, 1, nullptr, gsum, stream);
 }
 
 int mjrl_fvp_accumulate(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_fvp, const float* packed_theta,

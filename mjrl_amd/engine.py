@@ -490,6 +490,8 @@ class DeviceBatch:
         return b
 
 
+# the forward pass assembles the split rows itself where it can (UpdateEngine._fused_pack)
+FUSED_PACK = os.environ.get("MJRL_AMD_FUSED_PACK", "1") != "0"
 GRAPH_AUTO_ROWS = 300_000   # UpdateEngine.graphs == "auto": replay graphs up to this many rows (125k-row shard: 2.03 -> 1.97 ms; 1M rows: eager 4 % faster)
 HIDDEN_WIDTHS = (32, 64, 128, 256)   # hidden widths the row kernels are built for
 
@@ -747,6 +749,32 @@ class UpdateEngine:
                                                  C.c_void_p(self.stats[base:].data_ptr()), st),
                    "mjrl_moments_combine")
 
+    def _fused_pack(self, batch, T_all, T_vpg):
+        """Whether this update's forward pass assembles the split rows itself
+        (mjrl_policy_vpg_pack: the pack's read and write of the whole batch saved):
+        split rows, f32 observations [T_all][n] 16-byte aligned with n % 4 == 0, the
+        identity input normalisation, a forward pass over every staged row.
+        MJRL_AMD_FUSED_PACK=0 turns it off (A/B runs)."""
+        o = batch.obs
+        return (self.split and FUSED_PACK and o.dtype == torch.float32 and batch.act.dtype == torch.float32
+                and self.transforms[0] is None and self.shape.n % 4 == 0 and o.is_contiguous()
+                and o.data_ptr() % 16 == 0 and T_vpg == T_all and o.dim() == 2 and o.shape[0] >= T_all)
+
+    def _colscale(self, obs, T, st, obs_range=None):
+        """The split rows' power-of-two column scales of this batch (w['xc']):
+        from the staged per-column ranges (no pass over obs), or a device pass."""
+        w = self.ws
+        ins, isc, _, _ = self.transforms
+        sp = C.byref(self.shape)
+        if obs_range is not None:
+            _lib.check(self.lib.mjrl_obs_colscale_range(_lib.ptr(obs_range[0]), _lib.ptr(obs_range[1]), sp,
+                                                        _lib.ptr(ins), _lib.ptr(isc), _lib.ptr(w["xc"]), st),
+                       "mjrl_obs_colscale_range")
+        else:
+            cs = self.lib.mjrl_obs_colscale_f32 if obs.dtype == torch.float32 else self.lib.mjrl_obs_colscale
+            _lib.check(cs(_lib.ptr(obs), T, sp, _lib.ptr(ins), _lib.ptr(isc), _lib.ptr(w["xc"]), st),
+                       "mjrl_obs_colscale")
+
     def _pack(self, obs, act, T, st, obs_range=None):
         """a5 batch assembly: f64 obs / act -> the row format the policy passes read.
         obs_range: the staged batch's per-column (min, max) (DeviceBatch.obs_range),
@@ -759,14 +787,7 @@ class UpdateEngine:
             raise ValueError("observations and actions must be staged in the same dtype")
         if self.split:
             # column scales of this batch, then the split rows
-            if obs_range is not None:
-                _lib.check(self.lib.mjrl_obs_colscale_range(_lib.ptr(obs_range[0]), _lib.ptr(obs_range[1]), sp,
-                                                            _lib.ptr(ins), _lib.ptr(isc), _lib.ptr(w["xc"]), st),
-                           "mjrl_obs_colscale_range")
-            else:
-                cs = self.lib.mjrl_obs_colscale_f32 if f32 else self.lib.mjrl_obs_colscale
-                _lib.check(cs(_lib.ptr(obs), T, sp, _lib.ptr(ins), _lib.ptr(isc), _lib.ptr(w["xc"]), st),
-                           "mjrl_obs_colscale")
+            self._colscale(obs, T, st, obs_range)
             fn = self.lib.mjrl_pack_batch_split_f32 if f32 else self.lib.mjrl_pack_batch_split
             _lib.check(fn(_lib.ptr(obs), _lib.ptr(act), T, sp, _lib.ptr(ins), _lib.ptr(isc), _lib.ptr(w["xc"]),
                           _lib.ptr(w["xs"]), _lib.ptr(w["xu"]), _lib.ptr(w["act32"]), st), "mjrl_pack_batch_split")
@@ -914,8 +935,15 @@ class UpdateEngine:
                 self.returns_advantages(batch, gamma, None, stream=C.c_void_p(side.cuda_stream))
             elif not skip_gae:
                 self.returns_advantages(batch, gamma, gae_lambda, stream=C.c_void_p(side.cuda_stream))
-            # a5: batch assembly (f64 -> f32, input normalisation, bias column)
-            self._pack(batch.obs, batch.act, T_all, st, batch.obs_range)
+            # a5: batch assembly (f64 -> f32, input normalisation, bias column); fused
+            # into the forward pass below when it can be (_fused_pack): then only the
+            # column scales and the f32 actions here
+            fused = self._fused_pack(batch, T_all, T_all if (algo == "dapg" and demo_coef is not None) else T)
+            if fused:
+                self._colscale(batch.obs, T_all, st, batch.obs_range)
+                w["act32"][:T_all].copy_(batch.act[:T_all])
+            else:
+                self._pack(batch.obs, batch.act, T_all, st, batch.obs_range)
             main.wait_stream(side)
             # whitening (npg_cg.py:91) and path-return statistics (npg_cg.py:97-102):
             # two-pass fp64 moments, both quantities in one launch per pass; when
@@ -962,8 +990,13 @@ class UpdateEngine:
             sc = self._scratch(T_vpg)
             rows = self._rows(T_vpg, adv_vpg)
             timing[0].record()
-            _lib.check(L.mjrl_policy_vpg(sp, C.byref(rows), _lib.ptr(self.packed_theta), _lib.ptr(osh), _lib.ptr(osc),
-                                         C.byref(sc), _lib.ptr(v["gsum"]), st), "mjrl_policy_vpg")
+            if fused:
+                _lib.check(L.mjrl_policy_vpg_pack(sp, C.byref(rows), _lib.ptr(batch.obs), _lib.ptr(self.packed_theta),
+                                                  _lib.ptr(osh), _lib.ptr(osc), C.byref(sc), _lib.ptr(v["gsum"]), st),
+                           "mjrl_policy_vpg_pack")
+            else:
+                _lib.check(L.mjrl_policy_vpg(sp, C.byref(rows), _lib.ptr(self.packed_theta), _lib.ptr(osh),
+                                             _lib.ptr(osc), C.byref(sc), _lib.ptr(v["gsum"]), st), "mjrl_policy_vpg")
             self.comm.allreduce_sum(v["gsum"])
             _lib.check(L.mjrl_scale_vec(_lib.ptr(v["gsum"]), s.d, inv_T, _lib.ptr(v["g"]), st), "mjrl_scale_vec")
             timing[1].record()

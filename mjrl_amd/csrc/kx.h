@@ -72,6 +72,20 @@ __device__ __forceinline__ int swz128(int r) { return (((r >> 1) & 1) << 1) | ((
 __device__ __forceinline__ int woff(int row, int col) { return row * 128 + 16 * ((col >> 3) ^ swz128(row)) + 2 * (col & 7); }
 __device__ __forceinline__ int aoff(int f, int row) { return f * 64 + 16 * ((row >> 3) ^ (((f >> 3) & 1) << 1)) + 2 * (row & 7); }
 
+// max over the 16 lanes of a DPP row (lanes 16 r .. 16 r + 15), in every lane of
+// the row: quad_perm [1, 0, 3, 2], quad_perm [2, 3, 0, 1], row_half_mirror,
+// row_mirror (VALU only, where __shfl_xor is an LDS-queue ds_bpermute per step)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float row16_max(float v) {
+    v = fmaxf(v, dpp_f<0xB1>(v));
+    v = fmaxf(v, dpp_f<0x4E>(v));
+    v = fmaxf(v, dpp_f<0x141>(v));
+    return fmaxf(v, dpp_f<0x140>(v));
+}
+
 __device__ __forceinline__ half8 cat_tr(const short4v& a, const short4v& b) {
     return __builtin_bit_cast(half8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
 }
@@ -564,10 +578,7 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
                 }
                 mx = fmaxf(mx, absmax8(v[c]));
             }
-            mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
-            mx = fmaxf(mx, __shfl_xor(mx, 2, 64));
-            mx = fmaxf(mx, __shfl_xor(mx, 4, 64));
-            mx = fmaxf(mx, __shfl_xor(mx, 8, 64));
+            mx = row16_max(mx);
             float inv;
             const float sc = pow2_scale(mx, inv);
             char* dst = XHb + row * L::RBYTES + 16 * (c16 ^ chunk_swz(row));

@@ -319,7 +319,13 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 constexpr int GAE_WAVES = 2;       // waves (paths in flight) per workgroup (3 x 8 KB windows each)
-constexpr int GU = 8;              // serial steps per batch of LDS reads
+// serial steps per batch of LDS reads: 8 / 16 / 32 measured 47.8 / 45.1 / 44.3 us for
+// 125 paths of 1000 steps (profiles/r05x/gae.txt): the chain is the dependent fp64
+// multiply -> add (~44 ns a step), not the LDS reads
+#ifndef MJRL_GAE_GU
+#define MJRL_GAE_GU 32
+#endif
+constexpr int GU = MJRL_GAE_GU;
 
 __global__ void __launch_bounds__(64 * GAE_WAVES) k_gae(const double* __restrict__ rew,
                                                         const double* __restrict__ base,

@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 N, M, H = 376, 17, (64, 64)
 
 
-def _batch(rs, lengths, dtype=np.float32):
+def _batch(rs, lengths, dtype=np.float32, demos=()):
     from mjrl_amd.baselines.linear_baseline import LinearBaseline
     from mjrl_amd.engine import DeviceBatch
     from mjrl_amd.utils.gym_env import EnvSpec
@@ -24,9 +24,11 @@ def _batch(rs, lengths, dtype=np.float32):
         o = rs.randn(h, N) * scales
         o[:, :3] = 0.0
         paths.append(dict(observations=o, actions=rs.randn(h, M), rewards=rs.randn(h), terminated=bool(h % 2)))
+    demo_paths = [dict(observations=rs.randn(h, N) * scales, actions=rs.randn(h, M)) for h in demos]
     base = LinearBaseline(EnvSpec(N, M, max(lengths), 1))
     base._coeffs = rs.randn(N + 4) * 0.01
-    return DeviceBatch.from_paths(paths, torch.device("cuda:0"), baseline=base, obs_dtype=dtype), paths
+    return DeviceBatch.from_paths(paths, torch.device("cuda:0"), baseline=base, obs_dtype=dtype,
+                                  demo_paths=demo_paths or None), paths
 
 
 def _run(fused, batch, theta, algo, graph):
@@ -38,14 +40,16 @@ def _run(fused, batch, theta, algo, graph):
         eng.graphs = graph
         kw = dict(algo=algo, gamma=0.995, gae_lambda=0.97, cg_iters=10, damping=1e-4, trpo_verbose=False)
         kw.update(dict(n_step_size=0.01) if algo == "npg" else dict(kl_dist=0.01))
+        if algo == "dapg":
+            kw["demo_coef"] = 0.1
         outs = []
         for _ in range(3 if graph else 1):          # graph: capture, then replays
             out = eng.update(batch, theta, **kw)
             torch.cuda.synchronize()
             outs.append((out, eng.vec["theta_new"].clone()))
-        T = batch.T
+        T = batch.T + batch.T_demo
         ws = {k: eng.ws[k][:T].clone() for k in ("xs", "xu", "mu0", "ll0", "a0", "a1")}
-        return outs, ws, eng._fused_pack(batch, batch.T + batch.T_demo, batch.T)
+        return outs, ws, eng._fused_pack(batch, T, T if algo == "dapg" else batch.T)
     finally:
         E.FUSED_PACK = old
 
@@ -54,14 +58,15 @@ def _same(a, b):
     return np.array_equal(np.atleast_1d(np.asarray(a)).view(np.uint8), np.atleast_1d(np.asarray(b)).view(np.uint8))
 
 
-@pytest.mark.parametrize("algo,graph,lengths", [
-    ("npg", False, (1000, 999, 1, 37, 500)),        # 2537 rows: a partial last tile
-    ("npg", True, (64,) * 40),
-    ("trpo", False, (700, 333, 1000)),
+@pytest.mark.parametrize("algo,graph,lengths,demos", [
+    ("npg", False, (1000, 999, 1, 37, 500), ()),        # 2537 rows: a partial last tile
+    ("npg", True, (64,) * 40, ()),
+    ("trpo", False, (700, 333, 1000), ()),
+    ("dapg", False, (600, 411), (200, 77)),             # demo rows behind the RL rows, in the forward pass
 ])
-def test_fused_pack_update_is_bit_identical(algo, graph, lengths):
+def test_fused_pack_update_is_bit_identical(algo, graph, lengths, demos):
     rs = np.random.RandomState(len(lengths))
-    batch, _ = _batch(rs, lengths)
+    batch, _ = _batch(rs, lengths, demos=demos)
     theta = torch.from_numpy((rs.randn(29410) * 0.05).astype(np.float32)).cuda()
     (o1, ws1, f1), (o0, ws0, f0) = _run(True, batch, theta, algo, graph), _run(False, batch, theta, algo, graph)
     assert f1 and not f0

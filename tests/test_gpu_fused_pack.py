@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 N, M, H = 376, 17, (64, 64)
 
 
-def _batch(rs, lengths, dtype=np.float32, demos=()):
+def _batch(rs, lengths, dtype=np.float32, demos=(), N=N):
     from mjrl_amd.baselines.linear_baseline import LinearBaseline
     from mjrl_amd.engine import DeviceBatch
     from mjrl_amd.utils.gym_env import EnvSpec
@@ -31,7 +31,7 @@ def _batch(rs, lengths, dtype=np.float32, demos=()):
                                   demo_paths=demo_paths or None), paths
 
 
-def _run(fused, batch, theta, algo, graph):
+def _run(fused, batch, theta, algo, graph, N=N):
     from mjrl_amd import engine as E
     old = E.FUSED_PACK
     E.FUSED_PACK = fused
@@ -79,16 +79,18 @@ def test_fused_pack_update_is_bit_identical(algo, graph, lengths, demos):
             assert _same(np.asarray(a[k], np.float64), np.asarray(b[k], np.float64)), k
 
 
-def test_fused_pack_rows_equal_the_pack():
+@pytest.mark.parametrize("N", [N, 252, 120])   # 384 / 256 / 128 split columns (KG 12 / 8 / 4)
+def test_fused_pack_rows_equal_the_pack(N):
     """xs / xu written by the fused forward pass equal mjrl_pack_batch_split_f32's
     (the all-zero leading columns and the bias column included); a batch with an
     input normalisation, or staged in f64, takes the separate pack."""
     from mjrl_amd import engine as E
     rs = np.random.RandomState(7)
-    batch, _ = _batch(rs, (300, 5, 411))
+    batch, _ = _batch(rs, (300, 5, 411), N=N)
     T = batch.T
-    theta = torch.from_numpy((rs.randn(29410) * 0.05).astype(np.float32)).cuda()
-    _, ws1, f1 = _run(True, batch, theta, "npg", False)
+    d = E.UpdateEngine(N, M, H, device="cuda:0", precision="split").shape.d
+    theta = torch.from_numpy((rs.randn(d) * 0.05).astype(np.float32)).cuda()
+    _, ws1, f1 = _run(True, batch, theta, "npg", False, N=N)
     eng = E.UpdateEngine(N, M, H, device="cuda:0", precision="split")
     eng._ensure(T, batch.P)
     from mjrl_amd import _lib
@@ -101,6 +103,6 @@ def test_fused_pack_rows_equal_the_pack():
     # not fused: an input normalisation; f64 observations
     eng.set_transformations(rs.randn(N), np.abs(rs.randn(N)) + 0.5)
     assert not eng._fused_pack(batch, T, T)
-    b64, _ = _batch(rs, (100, 20), dtype=np.float64)
+    b64, _ = _batch(rs, (100, 20), dtype=np.float64, N=N)
     eng2 = E.UpdateEngine(N, M, H, device="cuda:0", precision="split")
     assert not eng2._fused_pack(b64, b64.T, b64.T)

@@ -283,6 +283,11 @@ constexpr bool KX_ABL_NOCHAIN = true;    // timing ablation only: the FVP's P2-P
 #else
 constexpr bool KX_ABL_NOCHAIN = false;
 #endif
+#ifdef MJRL_KX_ABL_NOCOLS
+constexpr bool KX_ABL_NOCOLS = true;     // timing ablation only: the FVP preamble's column scales not computed
+#else
+constexpr bool KX_ABL_NOCOLS = false;
+#endif
 
 // PACK (FWD only): the batch assembly (k_pack_split_q, a5) fused into the forward
 // pass: the tile's f32 observation rows are loaded instead of split rows and split
@@ -404,11 +409,13 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
         } else {
             wrows_store<64>(rv1, S2, L::WIMG, sc2, tid);
             wrows_store<32>(rv2, S4, L::WIMG2, sc4v, tid);
-            wscale<true>(w1v, sc1, red1, tid);
-            wscale<true>(w3v, sc3, red3, tid);
+            if (!(KX_ABL_NOCOLS && MODE == FVP)) {
+                wscale<true>(w1v, sc1, red1, tid);
+                wscale<true>(w3v, sc3, red3, tid);
+            }
         }
         KX_PRE(2);
-        if (MODE != EVAL) {
+        if (MODE != EVAL && !(KX_ABL_NOCOLS && MODE == FVP)) {
             __syncthreads();
             wscale_cols(sc1, red1, tid);
             wscale_cols(sc3, red3, tid);

@@ -30,6 +30,7 @@ of the reference update, oracle/npg_cpu.py) on a bounded sample on this host.
 import argparse
 import json
 import os
+import re
 import sys
 import time
 
@@ -134,23 +135,33 @@ def log(msg):
     print("bench: " + msg, file=sys.stderr, flush=True)
 
 
+def pmc_file():
+    """The newest committed PMC summary, profiles/r*/pmc_traffic.json, or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")))
+    return files[-1] if files else None
+
+
 def pmc_traffic(kernel_key):
     """HBM bytes per launch of a kernel from the newest committed PMC summary
     (profiles/r*/pmc_traffic.json, written from separate rocprofv3 --pmc passes
     of FETCH_SIZE and WRITE_SIZE with the gfx950 2x FETCH_SIZE correction; the
-    correction checks out on k_pack_batch, whose 3.14 GB read is known exactly)."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")))
-    if not files:
-        return None, None
-    data = json.load(open(files[-1]))
-    src = os.path.relpath(files[-1], ROOT)
+    correction checks out on k_pack_batch, whose 3.14 GB read is known exactly).
+    kernel_key: the demangled instantiation prefix ('k_kx<32, 12, 1, false>'),
+    matched after the '::' of the name.  Returns (bytes, source, error): a summary
+    that exists but lacks the kernel is an error, not a silent None (tests/
+    test_host_logic.py checks the committed file against the default key)."""
+    f = pmc_file()
+    if f is None:
+        return None, None, "no profiles/r*/pmc_traffic.json committed"
+    data = json.load(open(f))
+    src = os.path.relpath(f, ROOT)
     for name, v in data.items():
-        if isinstance(v, dict) and kernel_key in name:
+        if isinstance(v, dict) and re.search(r"(^|[\s:])" + re.escape(kernel_key), name):
             # the commit the PMC passes measured (recorded when the summary was filed)
             head = data.get("_measured_at_commit")
-            return v["hbm_bytes_per_launch"], src + (" @ " + head if head else "")
-    return None, None
+            return v["hbm_bytes_per_launch"], src + (" @ " + head if head else ""), None
+    return None, None, "%s has no entry for %s" % (src, kernel_key)
 
 
 def _commit():
@@ -330,7 +341,10 @@ def cpu_baseline(rows, base, reps=3, cfg=None):
 
     log("cpu baseline: %d timesteps on %d threads" % (P * H, cores))
     try:
-        one(max(H, (P * H // 10) // H * H))
+        # warm-up at the full sample size: the first update at a new size pays the
+        # first touch of its multi-GB temporaries (round 5's first full rep: 50.8 s
+        # against 35.7 / 36.1 s after a warm-up on a tenth)
+        one(P * H)
         ts = []
         for i in range(reps):
             ts.append(one(P * H))
@@ -445,21 +459,24 @@ def e2e_timeline(paths, eng, th, base, upd, device):
              "device H2D span and summed copy time, the update after the staging (device events)")
 
 
+def fvp_kernel_key(path, split, mp, np_, h0, h1):
+    """(name, demangled rocprof instantiation) of the FVP accumulate kernel: the
+    template arguments as kx.h / ks.h instantiate it (k_kx<MP, KG, MODE = 1 (FVP),
+    PACK = false>, k_ks<MP, KG, 1, false>)."""
+    if path == 0:
+        return "k_rows<%d,%d,%d,FVP>+k_wgrad" % (h0, h1, mp), "k_rows<%d, %d, %d, 1>" % (h0, h1, mp)
+    if path == 2 and split:
+        return "k_kx<%d,%d,FVP>" % (mp, np_ // 32), "k_kx<%d, %d, 1, false>" % (mp, np_ // 32)
+    if path == 2:
+        return "k_ks<%d,%d,FVP>" % (mp, np_ // 32), "k_ks<%d, %d, 1, false>" % (mp, np_ // 32)
+    return "k_fused<%d,%d,%d,FVP>" % (h0, h1, mp), "k_fused<%d, %d, %d, " % (h0, h1, mp)
+
+
 def kernel_names(eng, cfg):
     """(name, rocprof key, flops/row) of the FVP accumulate step and of the gather."""
     fl = flops_per_row(cfg["n"], cfg["m"], *cfg["hidden"])
-    path = eng.accumulate_path()
-    np_, mp = eng.shape.np, eng.shape.mp
     h0, h1 = cfg["hidden"]
-    if path == 0:   # row-chain kernel then split-K weight-gradient kernel, both inside the accumulate step
-        return ("k_rows<%d,%d,%d,FVP>+k_wgrad" % (h0, h1, mp), "k_rows<", fl["rows_fvp"] + fl["weight_grads"],
-                "k_gather", "k_gather", 0)
-    if path == 2 and eng.split:
-        acc = ("k_kx<%d,%d,FVP>" % (mp, np_ // 32), "k_kx<%d, %d, 1>" % (mp, np_ // 32))
-    elif path == 2:
-        acc = ("k_ks<%d,%d,FVP>" % (mp, np_ // 32), "k_ks<%d, %d, 1, false>" % (mp, np_ // 32))
-    else:
-        acc = ("k_fused<%d,%d,%d,FVP>" % (h0, h1, mp), "k_fused<")
+    acc = fvp_kernel_key(eng.accumulate_path(), eng.split, eng.shape.mp, eng.shape.np, eng.shape.h0, eng.shape.h1)
     return acc + (fl["rows_fvp"] + fl["weight_grads"], "k_gather", "k_gather", 0)
 
 
@@ -567,10 +584,17 @@ def main():
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
     log("timed region: %d steps, %.3f ms per step" % (args.steps, elapsed / args.steps * 1e3))
+    per_rank = [dict(rank=rank, rows=batch.T, ms_per_step=round(elapsed / args.steps * 1e3, 3))]
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
+        # every rank's own rows and time (so the line shows the shards and how far
+        # apart the ranks finished), then the max over ranks as the job's time
+        t = torch.tensor([float(rank), float(batch.T), elapsed], dtype=torch.float64,
+                         device=device if args.backend == "nccl" else "cpu")
+        allt = [torch.zeros_like(t) for _ in range(world)]
+        torch.distributed.all_gather(allt, t)
+        per_rank = [dict(rank=int(a[0]), rows=int(a[1]), ms_per_step=round(float(a[2]) / args.steps * 1e3, 3))
+                    for a in (x.cpu().numpy() for x in allt)]
+        elapsed = max(float(x[2].item()) for x in allt)
 
     # dominant-kernel roofline from live HIP events on the launch stream, recorded
     # around every FVP of eager steps: the timed region's when it ran eager, else
@@ -606,7 +630,10 @@ def main():
     kern = {acc_name: dict(avg_ms=t_acc * 1e3, tflops=acc_fl * rows_rank / t_acc / 1e12),
             gat_name: dict(avg_ms=t_gat * 1e3, tflops=gat_fl * rows_rank / t_gat / 1e12)}
     dom = max(kern, key=lambda k: kern[k]["avg_ms"])
-    traffic, tsrc = pmc_traffic(acc_key if dom == acc_name else gat_key) if args.config == "c4" else (None, None)
+    traffic, tsrc, terr = pmc_traffic(acc_key if dom == acc_name else gat_key) if args.config == "c4" \
+        else (None, None, None)
+    if terr is not None:
+        log("WARNING: roofline.traffic unavailable: " + terr)
     if traffic is not None and rows_rank != N_PATHS * HORIZON:
         # the committed PMC pass is the default 1-GPU launch (1M rows); scale per row
         traffic = traffic * rows_rank / (N_PATHS * HORIZON)
@@ -626,7 +653,7 @@ def main():
         roof = dict(bound="mfma", kernel=dom, achieved=round(flops_dom / t_dom / 1e12, 3), peak=peak_mm,
                     unit="TFLOP/s", frac=round(flops_dom / t_dom / 1e12 / peak_mm, 4))
     roof.update(traffic=None if traffic is None else round(traffic),
-                traffic_unit="bytes/launch (HBM, PMC)", traffic_source=tsrc,
+                traffic_unit="bytes/launch (HBM, PMC)", traffic_source=tsrc, traffic_error=terr,
                 traffic_GBps=None if traffic is None else round(traffic / t_dom / 1e9, 1),
                 flops_per_timestep=acc_fl if dom == acc_name else gat_fl, rows_per_launch=rows_rank,
                 mfma_form="split-f16 (3 x v_mfma_f32_16x16x32_f16 per f32 product), peak %.1f TFLOP/s f32-equivalent"
@@ -684,6 +711,9 @@ def main():
                                comm=type(eng.comm).__name__ + (" (one rank, sharded code path)"
                                                                if args.sharded_path and world == 1 else "")),
                    commit=_commit(),
+                   ranks=per_rank,
+                   comm_world_size=int(eng.comm.world_size),
+                   comm_backend=(torch.distributed.get_backend() if world > 1 else None),
                    hipgraph=bool(graphed), eager_ms_per_step=None if eager_ms is None else round(eager_ms, 3),
                    f32_ms_per_step=None if f32_ms is None else round(f32_ms, 3),
                    roofline=roof)

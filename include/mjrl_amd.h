@@ -182,6 +182,16 @@ int mjrl_linear_baseline_residual(const double* obs, const double* returns, int6
 int mjrl_linear_baseline_residual_f32(const float* obs, const double* returns, int64_t T, int32_t n,
                                       const int64_t* path_off, int64_t P, const double* coeffs,
                                       double* scratch, double* out, void* stream);
+/* Both from observations staged as an f32 pair, obs = hi + lo (mjrl_host_stage_paths_f64x
+ * rows + mjrl_host_stage_lo_paths_f64 low halves): the features are formed in fp64 from
+ * (double)hi + (double)lo, i.e. from the sampler's f64 values to 2^-48, so the fit
+ * matches LinearBaseline.fit on observations that are not float32s. */
+int mjrl_linear_baseline_gram_f32x2(const float* obs, const float* obs_lo, const double* returns, int64_t T,
+                                    int32_t n, const int64_t* path_off, int64_t P, double* scratch, double* out,
+                                    void* stream);
+int mjrl_linear_baseline_residual_f32x2(const float* obs, const float* obs_lo, const double* returns, int64_t T,
+                                        int32_t n, const int64_t* path_off, int64_t P, const double* coeffs,
+                                        double* scratch, double* out, void* stream);
 
 /* ---- subsampled Fisher rows (npg_cg.py:58-62: obs[rand_idx], act[rand_idx]) ----
  * dst row i = src row idx[i] for i < n, rows of row_bytes bytes (a multiple of 4);
@@ -403,6 +413,26 @@ int mjrl_host_stage_f32(const float* src, int64_t rows, int32_t n, float* dst, f
  * written one after another into dst: one call per chunk of paths. */
 int mjrl_host_stage_paths_f64(const double* const* srcs, const int64_t* rows, int32_t count, int32_t n, float* dst,
                               float* cmin, float* cmax);
+/* The same pass with LinearBaseline.predict's input taken from the sampler's own f64
+ * values (baselines/linear_baseline.py:10-18, 46-49; process_samples.py:23): for the
+ * first npred arrays (the RL paths; demonstration paths follow them) pred receives,
+ * one path after another, [clip(x, +-10), a, a^2, a^3, 1] . coeffs[n+4] in fp64
+ * (a = row index in the path / 1000) when coeffs / pred are given (both or neither),
+ * and *inexact (nullable) is set to 1 when any value is not exactly a float32 (the
+ * caller then stages the low halves below for the device fit).  The block's source
+ * is re-read from the core's cache, not DRAM. */
+int mjrl_host_stage_paths_f64x(const double* const* srcs, const int64_t* rows, int32_t count, int32_t n, float* dst,
+                               float* cmin, float* cmax, const double* coeffs, double* pred, int32_t npred,
+                               int32_t* inexact);
+/* dst = float(x - double(float(x))) for `count` arrays one after another: with the
+ * f32 rows above, hi + lo carries every observation to 2^-48 relative (lo = 0 where
+ * float(x) overflows).  The input of mjrl_linear_baseline_gram_f32x2. */
+int mjrl_host_stage_lo_paths_f64(const double* const* srcs, const int64_t* rows, int32_t count, int32_t n,
+                                 float* dst);
+/* The extras of mjrl_host_stage_paths_f64x for one array through the portable loop
+ * (tests compare it with the vector path). */
+int mjrl_host_extras_portable(const double* src, int64_t rows, int32_t n, const double* coeffs, double* pred,
+                              int32_t* inexact);
 /* The portable (non-AVX-512) path of mjrl_host_stage_f64, whatever the CPU, and
  * whether the CPU runs the AVX-512 path (1) or not (0); both for tests.  All the
  * mjrl_host_stage_* entry points are also in the host-only lib/libmjrl_stage.so. */

@@ -71,9 +71,14 @@ class BatchREINFORCE:
     env_factory = None
     num_envs = 64
     # dtype the sampled observations / actions are staged to HBM in: float32 (the
-    # policy's own input precision, half the PCIe bytes) or float64 (the device
-    # LinearBaseline then predicts / fits from the sampler's exact values)
-    staging_dtype = np.float32
+    # policy's own input precision, half the PCIe bytes) or float64; None = auto
+    # (staging_obs_dtype): float32, except float64 when the baseline is an
+    # MLPBaseline that predicts from the staged rows (its features are
+    # float32(clip(x) / 10) of the f64 x, mlp_baseline.py:37-56, which float32
+    # rows cannot reproduce bit for bit).  With float32 rows a LinearBaseline still
+    # sees the f64 values: the staging pass computes its predictions from them and
+    # the device fit reads their low halves (DeviceBatch.obs_lo).
+    staging_dtype = None
     # whether MJRL_AMD_DEVICES / devices= may hand the update to the GPU worker pool
     # (an algorithm whose update does not shard, PPO, runs in this process)
     _poolable = True
@@ -104,6 +109,13 @@ class BatchREINFORCE:
         if not isinstance(d.get("_comm"), (LocalComm, type(None))):
             d["_comm"] = None     # a process group does not pickle; re-resolved on use
         return d
+
+    def staging_obs_dtype(self):
+        """The dtype observations / actions of sampled paths are staged in (see
+        staging_dtype)."""
+        if self.staging_dtype is not None:
+            return np.dtype(self.staging_dtype)
+        return np.dtype(np.float64 if hasattr(self.baseline, "predict_device") else np.float32)
 
     def engine(self):
         if self._engine is None:
@@ -311,7 +323,10 @@ class BatchREINFORCE:
         comm = self.comm()
         if batch is not None and type(self.baseline).__name__ == "LinearBaseline" \
                 and hasattr(self.baseline, "_reg_coeff") and batch.T == sum(len(p["rewards"]) for p in paths):
-            return self.engine().fit_linear_baseline(batch, self.baseline, return_errors=return_errors)
+            # float32 rows of values that are not float32s: the fit reads their low
+            # halves too (staged now from the f64 paths), i.e. the sampler's values
+            return self.engine().fit_linear_baseline(batch, self.baseline, return_errors=return_errors,
+                                                     obs_lo=batch.obs_lo(paths))
         if comm.world_size > 1:
             return _fit_sharded(self.baseline, paths, comm, return_errors)
         return self.baseline.fit(paths, return_errors=return_errors) if return_errors else self.baseline.fit(paths)
@@ -323,7 +338,8 @@ class BatchREINFORCE:
         advantages into the path dicts like the reference does."""
         eng = self.engine()
         batch = DeviceBatch.from_paths(paths, eng.device, baseline=self.baseline, demo_paths=self._demo_paths(),
-                                       obs_dtype=self.staging_dtype, reuse=True, pre=self.__dict__.pop("_pre", None))
+                                       obs_dtype=self.staging_obs_dtype(), reuse=True,
+                                       pre=self.__dict__.pop("_pre", None))
         ret, adv = eng.returns_advantages(batch, gamma, gae_lambda)
         ret, adv = ret.cpu().numpy(), adv.cpu().numpy()
         base = batch.baseline.cpu().numpy()
@@ -342,7 +358,8 @@ class BatchREINFORCE:
             return self._apply_pool(pool.step(self, paths, "paths"), paths)
         eng = self.engine()
         batch = DeviceBatch.from_paths(paths, eng.device, use_advantages=True, demo_paths=self._demo_paths(),
-                                       obs_dtype=self.staging_dtype, reuse=True, pre=self.__dict__.pop("_pre", None))
+                                       obs_dtype=self.staging_obs_dtype(), reuse=True,
+                                       pre=self.__dict__.pop("_pre", None))
         return self._update(batch, paths)
 
     # ---- hooks for subclasses ---------------------------------------------------

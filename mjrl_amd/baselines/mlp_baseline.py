@@ -316,14 +316,26 @@ class MLPBaseline:
         RL rows first), path_off (device i64 [P+1]), lengths (host [P]) -> f64
         device [T].  Features as _features (f64, then f32), one forward."""
         st = self._predict_state()
-        dev = st["device"]
-        T = int(np.sum(lengths))
-        o = obs[:T].to(torch.float64).clamp(-10.0, 10.0) / 10.0
-        start = torch.repeat_interleave(path_off[:-1], torch.from_numpy(np.asarray(lengths, np.int64)).to(dev))
-        al = (torch.arange(T, device=dev, dtype=torch.int64) - start).to(torch.float64) / 1000.0
-        feat = torch.cat([o, al[:, None], (al ** 2)[:, None], (al ** 3)[:, None], (al ** 4)[:, None]], 1)
+        feat = self.features_device(obs, path_off, lengths)
         with torch.no_grad():
-            return st["model"](feat.to(torch.float32)).to(torch.float64).reshape(-1)
+            return st["model"](feat).to(torch.float64).reshape(-1)
+
+    def features_device(self, obs, path_off, lengths):
+        """_features(paths).astype('float32') (mlp_baseline.py:37-56, 108) of the
+        staged rows, on obs's device: f32 [T][n + 4]."""
+        dev = obs.device
+        lengths = np.asarray(lengths, np.int64)
+        T = int(np.sum(lengths))
+        # float32(clip(x, +-10) / 10) with clip and division in f64 (np.clip(o) / 10.0
+        # then .astype('float32')): bit for bit the reference's features when obs
+        # holds the sampler's f64 values (BatchREINFORCE stages f64 for this baseline)
+        o = (obs[:T].to(torch.float64).clamp(-10.0, 10.0) / 10.0).to(torch.float32)
+        # the time features depend on the row's index in its path only: one f32
+        # table from numpy's own al ** (j + 1) (torch's pow takes other roundings)
+        al = np.arange(int(lengths.max()) if len(lengths) else 0) / 1000.0
+        tab = torch.from_numpy(np.stack([al ** (j + 1) for j in range(4)], 1).astype(np.float32)).to(dev)
+        start = torch.repeat_interleave(path_off[:-1], torch.from_numpy(lengths).to(dev))
+        return torch.cat([o, tab[torch.arange(T, device=dev, dtype=torch.int64) - start]], 1)
 
     def predict(self, path):
         """mlp_baseline.py:107-115: one forward of the f32 features (on the GPU

@@ -246,21 +246,33 @@ def _group_comm(group=None):
     import torch.distributed as dist
     if dist.get_backend(group) == "nccl" and os.environ.get("MJRL_AMD_COMM", "rccl") != "torch":
         dev = torch.device("cuda", torch.cuda.current_device())
-        key = (id(group) if group is not None else None, dev.index)
-        c = _RCCL_CACHE.get(key)
-        if c is None or getattr(c, "_comm", None) is None:
+        # the entry holds the group object itself (the default group: the live
+        # WORLD object), its rank and size: a group destroyed and created again
+        # (even one reusing a freed object's id) gets a new communicator instead
+        # of the old world's
+        pg = group if group is not None else dist.group.WORLD
+        key = (id(pg), dev.index)
+        ent = _RCCL_CACHE.get(key)
+        live = (dist.get_rank(group), dist.get_world_size(group))
+        if ent is not None and (ent[1] is not pg or ent[2] != live or getattr(ent[0], "_comm", None) is None):
+            try:
+                ent[0].close()
+            except Exception:
+                pass
+            ent = None
+        if ent is None:
             if not _RCCL_CACHE:
                 import atexit
                 atexit.register(release_comms)
-            c = _RCCL_CACHE[key] = RcclComm(dev, group=group)
-        return c
+            ent = _RCCL_CACHE[key] = (RcclComm(dev, group=group), pg, live)
+        return ent[0]
     return DistComm(group)
 
 
 def release_comms():
     """Destroys the cached RCCL communicators (at exit, or before the process
     group is destroyed)."""
-    for c in list(_RCCL_CACHE.values()):
+    for c, _, _ in list(_RCCL_CACHE.values()):
         try:
             c.close()
         except Exception:

@@ -6,6 +6,10 @@
 // The T x k products are the whole cost (Humanoid 1M: k = 380, 2 T k^2 = 289
 // GFLOP fp64); the k x k solve stays on the host, exactly as the reference runs it.
 //
+// Observations staged as f32 rows can come with their low halves (an f32 pair,
+// hi + lo = the sampler's f64 value to 2^-48): the features are then formed from
+// both, so the fit is the reference's on observations that are not float32s.
+//
 // k_gram computes the Gram matrix of the augmented rows [f_t, y_t] (k+1 = n+5
 // columns: F^T F, F^T y and y^T y in one pass) with v_mfma_f64_16x16x4_f64:
 //   - output 64 x 64 tiles of the upper triangle; workgroup = 4 waves, each wave
@@ -43,12 +47,20 @@ __global__ void __launch_bounds__(256) k_path_time(const int64_t* __restrict__ o
     }
 }
 
+// observation k of row `row` in fp64: the staged value, or hi + lo for an f32 pair
+// (the low halves of mjrl_host_stage_lo_paths_f64; lo is null otherwise)
+template <typename TO>
+__device__ __forceinline__ double obs_at(const TO* __restrict__ obs, const float* __restrict__ lo, int64_t i) {
+    return lo ? (double)obs[i] + (double)lo[i] : (double)obs[i];
+}
+
 // feature g of row `row` (linear_baseline.py:10-18), the return as feature n + 4, zero pad
 template <typename TO>
-__device__ __forceinline__ double feat(const TO* __restrict__ obs, const double* __restrict__ y,
-                                       const double* __restrict__ al, int64_t row, int g, int n) {
+__device__ __forceinline__ double feat(const TO* __restrict__ obs, const float* __restrict__ lo,
+                                       const double* __restrict__ y, const double* __restrict__ al, int64_t row,
+                                       int g, int n) {
     if (g < n) {
-        const double o = (double)obs[row * n + g];
+        const double o = obs_at(obs, lo, row * n + g);
         return o < -10.0 ? -10.0 : (o > 10.0 ? 10.0 : o);
     }
     const double a = al[row];
@@ -65,6 +77,7 @@ __device__ __forceinline__ double feat(const TO* __restrict__ obs, const double*
 template <typename TO>
 struct GramArgs {
     const TO* obs;
+    const float* lo;   // low halves of an f32 pair, or null
     const double* y;
     const double* al;
     int64_t T;
@@ -99,8 +112,8 @@ __global__ void __launch_bounds__(GTHREADS, 2) k_gram(GramArgs<TO> a) {
         const bool in = row < r1;
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            vi[u] = in ? feat(a.obs, a.y, a.al, row, ti * GT + lc + u, a.n) : 0.0;
-            vj[u] = in ? feat(a.obs, a.y, a.al, row, tj * GT + lc + u, a.n) : 0.0;
+            vi[u] = in ? feat(a.obs, a.lo, a.y, a.al, row, ti * GT + lc + u, a.n) : 0.0;
+            vj[u] = in ? feat(a.obs, a.lo, a.y, a.al, row, tj * GT + lc + u, a.n) : 0.0;
         }
     };
     auto lstore = [&](int buf) {
@@ -179,7 +192,8 @@ __global__ void __launch_bounds__(256) k_gram_reduce(const double* __restrict__ 
 
 // r_t = y_t - [clip(o_t), a, a^2, a^3, 1] . c  (fit(return_errors=True)'s residuals)
 template <typename TO>
-__global__ void __launch_bounds__(256) k_linear_residual(const TO* __restrict__ obs, const double* __restrict__ y,
+__global__ void __launch_bounds__(256) k_linear_residual(const TO* __restrict__ obs, const float* __restrict__ lo,
+                                                         const double* __restrict__ y,
                                                          const double* __restrict__ al, int64_t T, int n,
                                                          const double* __restrict__ coef, double* __restrict__ out) {
     const int lane = threadIdx.x & 63;
@@ -187,7 +201,7 @@ __global__ void __launch_bounds__(256) k_linear_residual(const TO* __restrict__ 
     for (int64_t row = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; row < T; row += nw) {
         double acc = 0.0;
         for (int j = lane; j < n; j += 64) {
-            double o = (double)obs[row * n + j];
+            double o = obs_at(obs, lo, row * n + j);
             o = o < -10.0 ? -10.0 : (o > 10.0 ? 10.0 : o);
             acc += o * coef[j];
         }
@@ -222,8 +236,8 @@ int mjrl_linear_baseline_gram_scratch(int32_t n, int64_t T, int64_t* doubles) {
 
 extern "C++" {
 template <typename TO>
-static int linear_baseline_gram(const TO* obs, const double* returns, int64_t T, int32_t n, const int64_t* path_off,
-                                int64_t P, double* scratch, double* out, void* stream) {
+static int linear_baseline_gram(const TO* obs, const float* lo, const double* returns, int64_t T, int32_t n,
+                                const int64_t* path_off, int64_t P, double* scratch, double* out, void* stream) {
     if (n <= 0 || T < 0 || P < 0 || !out || !scratch || (T > 0 && (!obs || !returns || !path_off)))
         return MJRL_EINVAL;
     hipStream_t st = (hipStream_t)stream;
@@ -235,7 +249,7 @@ static int linear_baseline_gram(const TO* obs, const double* returns, int64_t T,
         const int64_t g = (P + 3) / 4;
         hipLaunchKernelGGL(k_path_time, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, st, path_off, P, al);
     }
-    GramArgs<TO> ga{obs, returns, al, T, n, ntile, npair, slab};
+    GramArgs<TO> ga{obs, lo, returns, al, T, n, ntile, npair, slab};
     const int groups = (GSLICES + 7) / 8;   // slices per XCD
     hipLaunchKernelGGL(k_gram<TO>, dim3(8 * groups * npair), dim3(GTHREADS), 0, st, ga);
     const int64_t ne = (int64_t)npair * GT * GT;
@@ -247,7 +261,7 @@ static int linear_baseline_gram(const TO* obs, const double* returns, int64_t T,
 
 extern "C++" {
 template <typename TO>
-static int linear_baseline_residual(const TO* obs, const double* returns, int64_t T, int32_t n,
+static int linear_baseline_residual(const TO* obs, const float* lo, const double* returns, int64_t T, int32_t n,
                                     const int64_t* path_off, int64_t P, const double* coeffs, double* scratch,
                                     double* out, void* stream) {
     if (n <= 0 || T < 0 || P < 0 || (T > 0 && (!obs || !returns || !path_off || !coeffs || !scratch || !out)))
@@ -262,7 +276,7 @@ static int linear_baseline_residual(const TO* obs, const double* returns, int64_
         hipLaunchKernelGGL(k_path_time, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, st, path_off, P, al);
     }
     const int64_t g = (T + 3) / 4;
-    hipLaunchKernelGGL(k_linear_residual<TO>, dim3((unsigned)(g < 16384 ? g : 16384)), dim3(256), 0, st, obs,
+    hipLaunchKernelGGL(k_linear_residual<TO>, dim3((unsigned)(g < 16384 ? g : 16384)), dim3(256), 0, st, obs, lo,
                        returns, al, T, n, coeffs, out);
     return err(hipGetLastError());
 }
@@ -270,24 +284,40 @@ static int linear_baseline_residual(const TO* obs, const double* returns, int64_
 
 int mjrl_linear_baseline_gram(const double* obs, const double* returns, int64_t T, int32_t n,
                               const int64_t* path_off, int64_t P, double* scratch, double* out, void* stream) {
-    return linear_baseline_gram(obs, returns, T, n, path_off, P, scratch, out, stream);
+    return linear_baseline_gram(obs, (const float*)nullptr, returns, T, n, path_off, P, scratch, out, stream);
 }
 
 int mjrl_linear_baseline_gram_f32(const float* obs, const double* returns, int64_t T, int32_t n,
                                   const int64_t* path_off, int64_t P, double* scratch, double* out, void* stream) {
-    return linear_baseline_gram(obs, returns, T, n, path_off, P, scratch, out, stream);
+    return linear_baseline_gram(obs, (const float*)nullptr, returns, T, n, path_off, P, scratch, out, stream);
 }
 
 int mjrl_linear_baseline_residual(const double* obs, const double* returns, int64_t T, int32_t n,
                                   const int64_t* path_off, int64_t P, const double* coeffs, double* scratch,
                                   double* out, void* stream) {
-    return linear_baseline_residual(obs, returns, T, n, path_off, P, coeffs, scratch, out, stream);
+    return linear_baseline_residual(obs, (const float*)nullptr, returns, T, n, path_off, P, coeffs, scratch, out,
+                                    stream);
 }
 
 int mjrl_linear_baseline_residual_f32(const float* obs, const double* returns, int64_t T, int32_t n,
                                       const int64_t* path_off, int64_t P, const double* coeffs, double* scratch,
                                       double* out, void* stream) {
-    return linear_baseline_residual(obs, returns, T, n, path_off, P, coeffs, scratch, out, stream);
+    return linear_baseline_residual(obs, (const float*)nullptr, returns, T, n, path_off, P, coeffs, scratch, out,
+                                    stream);
+}
+
+int mjrl_linear_baseline_gram_f32x2(const float* obs, const float* obs_lo, const double* returns, int64_t T,
+                                    int32_t n, const int64_t* path_off, int64_t P, double* scratch, double* out,
+                                    void* stream) {
+    if (T > 0 && !obs_lo) return MJRL_EINVAL;
+    return linear_baseline_gram(obs, obs_lo, returns, T, n, path_off, P, scratch, out, stream);
+}
+
+int mjrl_linear_baseline_residual_f32x2(const float* obs, const float* obs_lo, const double* returns, int64_t T,
+                                        int32_t n, const int64_t* path_off, int64_t P, const double* coeffs,
+                                        double* scratch, double* out, void* stream) {
+    if (T > 0 && !obs_lo) return MJRL_EINVAL;
+    return linear_baseline_residual(obs, obs_lo, returns, T, n, path_off, P, coeffs, scratch, out, stream);
 }
 
 }  // extern "C"

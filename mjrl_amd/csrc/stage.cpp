@@ -22,6 +22,7 @@
 //     slab displaced the source from the caches, so the conversion, not the PCIe
 //     copy, set the end-to-end time.
 //   portable: the same one-pass loop, auto-vectorised for the build's baseline ISA.
+#include <cmath>
 #include <cstdint>
 #include <cstring>
 
@@ -32,8 +33,9 @@
 namespace {
 
 template <typename S>
-int stage_portable(const S* __restrict__ src, int64_t rows, int32_t n, float* __restrict__ dst,
-                   float* __restrict__ cmin, float* __restrict__ cmax) {
+__attribute__((always_inline)) inline int portable_body(const S* __restrict__ src, int64_t rows, int32_t n,
+                                                        float* __restrict__ dst, float* __restrict__ cmin,
+                                                        float* __restrict__ cmax) {
     const int64_t ne = rows * (int64_t)n;
     if (!cmin) {
         for (int64_t i = 0; i < ne; ++i) dst[i] = (float)src[i];
@@ -50,6 +52,58 @@ int stage_portable(const S* __restrict__ src, int64_t rows, int32_t n, float* __
             cmax[k] = v > hi ? v : hi;
         }
     }
+    return MJRL_OK;
+}
+
+// the loop auto-vectorised for the build's baseline ISA (SSE2), and again for AVX2
+// hosts without AVX-512 (Zen 2 / 3), chosen at run time like the AVX-512 path
+template <typename S>
+int stage_portable(const S* src, int64_t rows, int32_t n, float* dst, float* cmin, float* cmax) {
+    return portable_body(src, rows, n, dst, cmin, cmax);
+}
+template <typename S>
+__attribute__((target("avx2,fma"))) int stage_portable_avx2(const S* src, int64_t rows, int32_t n, float* dst,
+                                                            float* cmin, float* cmax) {
+    return portable_body(src, rows, n, dst, cmin, cmax);
+}
+
+bool have_avx2() {
+    static const int ok = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma");
+    return ok;
+}
+
+// LinearBaseline extras of the f64 pass (baselines/linear_baseline.py:10-18, 46-49):
+// pred[r] = [clip(x_r, +-10), a, a^2, a^3, 1] . coeffs (a = r / 1000, the row's index in
+// its path) in fp64 from the sampler's own values, and a flag raised when a value
+// is not a float32 (its f32 image then differs from what the reference reads).
+struct Extras {
+    const double* coeffs;   // n + 4, or null (no prediction)
+    double* pred;           // rows, or null
+    int32_t* inexact;       // set to 1 on the first value with (double)(float)x != x, or null
+};
+
+inline double clip10(double x) {   // np.clip(x, -10, 10): NaN stays NaN
+    return x < -10.0 ? -10.0 : (x > 10.0 ? 10.0 : x);
+}
+
+inline double time_terms(int64_t r, const double* c, int32_t n) {
+    const double a = (double)r / 1000.0;   // np.arange(l) / 1000.0
+    return a * c[n] + (a * a) * c[n + 1] + std::pow(a, 3.0) * c[n + 2] + c[n + 3];
+}
+
+int extras_portable(const double* __restrict__ src, int64_t rows, int32_t n, const Extras& x) {
+    bool bad = false;
+    for (int64_t r = 0; r < rows; ++r) {
+        const double* __restrict__ s = src + r * n;
+        double acc = 0.0;
+        for (int32_t k = 0; k < n; ++k) {
+            const double v = s[k];
+            bad |= !((double)(float)v == v);
+            if (x.coeffs) acc += clip10(v) * x.coeffs[k];
+        }
+        if (x.pred) x.pred[r] = acc + time_terms(r, x.coeffs, n);
+    }
+    if (bad && x.inexact) *x.inexact = 1;
     return MJRL_OK;
 }
 
@@ -126,14 +180,43 @@ MJRL_AVX512 inline void strip(const S* __restrict__ src, int64_t r0, int64_t r1,
     }
 }
 
-template <typename S, bool RANGE, bool PREFETCH = true>
+// The extras of rows r0 .. r1 - 1, right after the strips converted them: the
+// block's source (rb rows, ~64 KB) is still in the core's L2, so this second look
+// at it costs no DRAM traffic.  8 doubles per step: the float round trip compared
+// with the value (NEQ_UQ: a NaN counts as inexact), clip as max(-10, x) then
+// min(10, .) with x the SECOND operand of each (vmaxpd / vminpd return it when
+// either is NaN: NaN stays NaN, as np.clip), fused multiply-add with the coefficients.
+MJRL_AVX512 void extras_avx512(const double* __restrict__ src, int64_t r0, int64_t r1, int32_t n, const Extras& x) {
+    const __m512d lo = _mm512_set1_pd(-10.0), hi = _mm512_set1_pd(10.0);
+    __mmask8 bad = 0;
+    for (int64_t r = r0; r < r1; ++r) {
+        const double* s = src + r * n;
+        __m512d acc = _mm512_setzero_pd();
+        for (int32_t k = 0; k < n; k += 8) {
+            const __mmask8 m = n - k >= 8 ? (__mmask8)0xff : (__mmask8)((1u << (n - k)) - 1);
+            const __m512d v = _mm512_maskz_loadu_pd(m, s + k);
+            bad |= _mm512_cmp_pd_mask(_mm512_cvtps_pd(_mm512_cvtpd_ps(v)), v, _CMP_NEQ_UQ);
+            if (x.coeffs)
+                acc = _mm512_fmadd_pd(_mm512_min_pd(hi, _mm512_max_pd(lo, v)), _mm512_maskz_loadu_pd(m, x.coeffs + k),
+                                      acc);
+        }
+        if (x.pred) x.pred[r] = _mm512_reduce_add_pd(acc) + time_terms(r, x.coeffs, n);
+    }
+    if (bad && x.inexact) *x.inexact = 1;
+}
+
+template <typename S, bool RANGE>
 MJRL_AVX512 int stage_avx512(const S* __restrict__ src, int64_t rows, int32_t n, float* __restrict__ dst,
-                             float* __restrict__ cmin, float* __restrict__ cmax) {
+                             float* __restrict__ cmin, float* __restrict__ cmax, const Extras* xt = nullptr) {
     constexpr int BUF = 8192;   // floats of the block buffer (32 KB: stays in L1 / L2)
     constexpr int NCH = 12;     // 16-column chunks per strip: 24 range registers of the 32
     alignas(64) float buf[BUF + 16];
     const int64_t rb = n <= BUF ? BUF / n : 0;
-    if (rb == 0) return stage_portable(src, rows, n, dst, cmin, cmax);
+    if (rb == 0) {
+        if constexpr (sizeof(S) == 8)
+            if (xt) extras_portable(src, rows, n, *xt);
+        return stage_portable(src, rows, n, dst, cmin, cmax);
+    }
     const int nc = (n + 15) / 16;
     const __mmask16 tail = (__mmask16)(n % 16 ? (1u << (n % 16)) - 1 : 0xffff);
     for (int64_t r0 = 0; r0 < rows; r0 += rb) {
@@ -142,7 +225,7 @@ MJRL_AVX512 int stage_avx512(const S* __restrict__ src, int64_t rows, int32_t n,
         // rows), so the strips below find them in L2: the strips' short strided
         // pieces (rb rows x 192 columns) are not a stream the hardware prefetcher
         // follows
-        if (PREFETCH && r1 < rows) {
+        if (r1 < rows) {
             const char* p = reinterpret_cast<const char*>(src + r1 * n);
             const int64_t nb = ((r1 + rb < rows ? r1 + rb : rows) - r1) * n * (int64_t)sizeof(S);
             for (int64_t o = 0; o < nb; o += 64) _mm_prefetch(p + o, _MM_HINT_T1);
@@ -150,6 +233,8 @@ MJRL_AVX512 int stage_avx512(const S* __restrict__ src, int64_t rows, int32_t n,
         // strip by strip over the block: the block's source (rb rows) stays in the
         // core's caches between strips, the ranges in registers within one
         for (int c0 = 0; c0 < n; c0 += 16 * NCH) strip<S, RANGE, NCH>(src, r0, r1, n, c0, nc, tail, buf, cmin, cmax);
+        if constexpr (sizeof(S) == 8)
+            if (xt) extras_avx512(src, r0, r1, n, *xt);
         stream_out(dst + r0 * n, buf, (r1 - r0) * n);
     }
     _mm_sfence();   // the streamed lines are globally visible before the caller's H2D copy
@@ -163,14 +248,32 @@ bool have_avx512() {
 }
 
 template <typename S>
-int stage_rows(const S* src, int64_t rows, int32_t n, float* dst, float* cmin, float* cmax) {
+int stage_rows(const S* src, int64_t rows, int32_t n, float* dst, float* cmin, float* cmax,
+               const Extras* xt = nullptr) {
     if (rows < 0 || n <= 0 || (rows > 0 && (!src || !dst))) return MJRL_EINVAL;
     if ((cmin == nullptr) != (cmax == nullptr)) return MJRL_EINVAL;
     if (rows == 0) return MJRL_OK;
     if (have_avx512())
-        return cmin ? stage_avx512<S, true>(src, rows, n, dst, cmin, cmax)
-                    : stage_avx512<S, false>(src, rows, n, dst, cmin, cmax);
-    return stage_portable(src, rows, n, dst, cmin, cmax);
+        return cmin ? stage_avx512<S, true>(src, rows, n, dst, cmin, cmax, xt)
+                    : stage_avx512<S, false>(src, rows, n, dst, cmin, cmax, xt);
+    if constexpr (sizeof(S) == 8)
+        if (xt) extras_portable(src, rows, n, *xt);
+    return have_avx2() ? stage_portable_avx2(src, rows, n, dst, cmin, cmax) : stage_portable(src, rows, n, dst, cmin, cmax);
+}
+
+// lo = float(x - double(float(x))): with hi = float(x), hi + lo carries x to 2^-48
+// relative (x - hi is exact in f64; its float rounding keeps 24 of its <= 29 bits).
+// A value past the float range (hi = +-inf) gets lo = 0, so hi + lo stays the
+// infinity the clip at +-10 maps to the same feature; NaN stays NaN.
+int stage_lo_rows(const double* __restrict__ src, int64_t rows, int32_t n, float* __restrict__ dst) {
+    if (rows < 0 || n <= 0 || (rows > 0 && (!src || !dst))) return MJRL_EINVAL;
+    const int64_t ne = rows * (int64_t)n;
+    for (int64_t i = 0; i < ne; ++i) {
+        const double v = src[i];
+        const float h = (float)v;
+        dst[i] = std::isinf(h) ? 0.0f : (float)(v - (double)h);
+    }
+    return MJRL_OK;
 }
 
 }  // namespace
@@ -199,6 +302,46 @@ int mjrl_host_stage_paths_f64(const double* const* srcs, const int64_t* rows, in
     return MJRL_OK;
 }
 
+// mjrl_host_stage_paths_f64 with the LinearBaseline extras: the first npred arrays
+// (the RL paths of the chunk; demonstration paths follow them) get their fp64
+// predictions written one after another into pred when coeffs is given, and
+// *inexact is set to 1 when any value of the chunk is not a float32.
+int mjrl_host_stage_paths_f64x(const double* const* srcs, const int64_t* rows, int32_t count, int32_t n, float* dst,
+                               float* cmin, float* cmax, const double* coeffs, double* pred, int32_t npred,
+                               int32_t* inexact) {
+    if (count < 0 || (count > 0 && (!srcs || !rows))) return MJRL_EINVAL;
+    if ((coeffs == nullptr) != (pred == nullptr) || npred < 0) return MJRL_EINVAL;
+    for (int32_t i = 0; i < count; ++i) {
+        const Extras xt{i < npred ? coeffs : nullptr, i < npred ? pred : nullptr, inexact};
+        const int rc = stage_rows(srcs[i], rows[i], n, dst, cmin, cmax, &xt);
+        if (rc != MJRL_OK) return rc;
+        dst += rows[i] * (int64_t)n;
+        if (i < npred && pred) pred += rows[i];
+    }
+    return MJRL_OK;
+}
+
+// The low halves of `count` f64 arrays (stage_lo_rows), one after another into dst:
+// with the f32 rows of the pass above, the device LinearBaseline fit reads every
+// observation to 2^-48 (mjrl_linear_baseline_gram_f32x2).
+int mjrl_host_stage_lo_paths_f64(const double* const* srcs, const int64_t* rows, int32_t count, int32_t n,
+                                 float* dst) {
+    if (count < 0 || (count > 0 && (!srcs || !rows))) return MJRL_EINVAL;
+    for (int32_t i = 0; i < count; ++i) {
+        const int rc = stage_lo_rows(srcs[i], rows[i], n, dst);
+        if (rc != MJRL_OK) return rc;
+        dst += rows[i] * (int64_t)n;
+    }
+    return MJRL_OK;
+}
+
+// The extras alone through the portable loop, whatever the CPU (tests compare the paths).
+int mjrl_host_extras_portable(const double* src, int64_t rows, int32_t n, const double* coeffs, double* pred,
+                              int32_t* inexact) {
+    if (rows < 0 || n <= 0 || (rows > 0 && !src) || (coeffs == nullptr) != (pred == nullptr)) return MJRL_EINVAL;
+    return extras_portable(src, rows, n, Extras{coeffs, pred, inexact});
+}
+
 // The portable loop, callable whatever the CPU (tests compare the two paths).
 int mjrl_host_stage_f64_portable(const double* src, int64_t rows, int32_t n, float* dst, float* cmin, float* cmax) {
     if (rows < 0 || n <= 0 || (rows > 0 && (!src || !dst))) return MJRL_EINVAL;
@@ -221,15 +364,6 @@ int mjrl_host_gather(const void* const* srcs, const int64_t* nbytes, int32_t cou
         d += nbytes[i];
     }
     return MJRL_OK;
-}
-
-// The AVX-512 path without the next-block prefetch (tools/stage_convert_probe.py A/B).
-int mjrl_host_stage_f64_nopf(const double* src, int64_t rows, int32_t n, float* dst, float* cmin, float* cmax) {
-    if (rows < 0 || n <= 0 || (rows > 0 && (!src || !dst))) return MJRL_EINVAL;
-    if ((cmin == nullptr) != (cmax == nullptr)) return MJRL_EINVAL;
-    if (rows == 0 || !have_avx512()) return stage_portable(src, rows, n, dst, cmin, cmax);
-    return cmin ? stage_avx512<double, true, false>(src, rows, n, dst, cmin, cmax)
-                : stage_avx512<double, false, false>(src, rows, n, dst, cmin, cmax);
 }
 
 }  // extern "C"

@@ -79,13 +79,20 @@ def _host_threads(cap=16):
     return max(1, min(int(cap), n))
 
 
-def host_stage(arrs, view, offs, a0, a1, lo=None, hi=None):
+def host_stage(arrs, view, offs, a0, a1, lo=None, hi=None, extras=None):
     """Arrays a0 .. a1 - 1 of `arrs` into their rows offs[i]:offs[i+1] of `view`
     (a pinned host array), converted to view's dtype; with lo / hi (float32 [n])
     the column ranges of what was written are folded in.  f64 / f32 arrays go
     through the native one-pass convert-and-range loop (mjrl_host_stage_* of the
     host-only lib/libmjrl_stage.so: AVX-512 with streaming stores; ctypes
-    releases the GIL), anything else through numpy."""
+    releases the GIL), anything else through numpy.
+
+    extras (float32 2-D views only): dict(coeffs=f64 [n+4] or None, pred=f64
+    host array over the rows of the first `npred` arrays, npred=, flag=int32 [1])
+    — the LinearBaseline prediction of every row of arrays < npred, in fp64 from
+    the sampler's own values, and flag[0] = 1 when any value is not a float32
+    (mjrl_host_stage_paths_f64x).  Sources that are not C-contiguous f64 are
+    converted to it first, so the extras always come from the values as given."""
     fns = None
     if view.dtype == np.float32 and view.ndim == 2:
         L = _lib.stage_lib()
@@ -94,17 +101,29 @@ def host_stage(arrs, view, offs, a0, a1, lo=None, hi=None):
         # width: one native call for the whole chunk
         srcs = [np.asarray(arrs[i]) for i in range(a0, a1)]
         n = view.shape[1]
+        if extras is not None:
+            srcs = [np.ascontiguousarray(a.reshape(a.shape[0], -1) if a.ndim > 2 else a, dtype=np.float64)
+                    for a in srcs]
         if srcs and all(a.dtype == np.float64 and a.ndim == 2 and a.shape[1] == n and a.flags.c_contiguous
                         and a.shape[0] == offs[i + 1] - offs[i] for i, a in zip(range(a0, a1), srcs)):
             k = len(srcs)
             ptrs = (C.c_void_p * k)(*[a.ctypes.data for a in srcs])
             rows = (C.c_int64 * k)(*[a.shape[0] for a in srcs])
             dst = view[offs[a0]:offs[a1]]
-            if dst.shape[0]:
-                _lib.check(L.mjrl_host_stage_paths_f64(ptrs, rows, k, n, dst.ctypes.data,
-                                                       None if lo is None else lo.ctypes.data,
-                                                       None if hi is None else hi.ctypes.data), "mjrl_host_stage")
+            rng = (None if lo is None else lo.ctypes.data, None if hi is None else hi.ctypes.data)
+            if dst.shape[0] and extras is None:
+                _lib.check(L.mjrl_host_stage_paths_f64(ptrs, rows, k, n, dst.ctypes.data, *rng), "mjrl_host_stage")
+            elif dst.shape[0]:
+                npred = max(0, min(a1, int(extras["npred"])) - a0)
+                c = extras.get("coeffs")
+                withp = c is not None and npred > 0
+                _lib.check(L.mjrl_host_stage_paths_f64x(
+                    ptrs, rows, k, n, dst.ctypes.data, *rng, c.ctypes.data if withp else None,
+                    extras["pred"][offs[a0]:].ctypes.data if withp else None, npred if withp else 0,
+                    extras["flag"].ctypes.data), "mjrl_host_stage")
             return
+        if extras is not None:
+            raise ValueError("host_stage extras: observation arrays of a path do not match the staged width %d" % n)
     elif a1 > a0:
         # other slots (1-D rewards / offsets / flags, f64 observations): one
         # numpy concatenate per chunk (a copyto per path cost ~25 us each: 25 ms
@@ -142,6 +161,21 @@ def host_stage(arrs, view, offs, a0, a1, lo=None, hi=None):
         if lo is not None:
             np.fmin(lo, np.nanmin(dst, axis=0) if dst.shape[0] else lo, out=lo)
             np.fmax(hi, np.nanmax(dst, axis=0) if dst.shape[0] else hi, out=hi)
+
+
+def host_stage_lo(arrs, view, offs, a0, a1):
+    """The low halves float32(x - float32(x)) of arrays a0 .. a1 - 1 (f64 [rows, n])
+    into their rows of `view` (float32 [R, n]): mjrl_host_stage_lo_paths_f64."""
+    srcs = [np.ascontiguousarray(np.asarray(arrs[i]).reshape(len(arrs[i]), -1), dtype=np.float64)
+            for i in range(a0, a1)]
+    dst = view[offs[a0]:offs[a1]]
+    if not srcs or not dst.shape[0]:
+        return
+    k = len(srcs)
+    ptrs = (C.c_void_p * k)(*[a.ctypes.data for a in srcs])
+    rows = (C.c_int64 * k)(*[a.shape[0] for a in srcs])
+    _lib.check(_lib.stage_lib().mjrl_host_stage_lo_paths_f64(ptrs, rows, k, view.shape[1], dst.ctypes.data),
+               "mjrl_host_stage_lo_paths_f64")
 
 
 class _PinnedStaging:
@@ -232,12 +266,19 @@ class _PinnedStaging:
         if ev is not None:
             ev.synchronize()
 
-    def stage(self, slot, arrs, ncols, dtype, device, reuse=False, ranges=False):
+    def stage(self, slot, arrs, ncols, dtype, device, reuse=False, ranges=False, extras=None, low=False):
         """Concatenation of `arrs` (each [rows] or [rows, ncols]) as a device
         tensor [R] / [R, ncols] of `dtype` (np.float32 / np.float64 / np.int64 /
         np.uint8).  ranges=True (float32 [R, ncols] slots): also the per-column
         (min, max) of the staged values, taken in the same conversion pass, as
-        self.last_range (two float32 [ncols] arrays)."""
+        self.last_range (two float32 [ncols] arrays).  extras (float32 [R, ncols]
+        slots of f64 observations): dict(coeffs=LinearBaseline coefficients or
+        None, npred=number of leading arrays to predict) — the same pass also
+        computes their fp64 baseline predictions (staged to the device slot
+        'base', after the rows) and whether every value was a float32:
+        self.last_extras = dict(pred=device f64 [rows of the first npred arrays]
+        or None, inexact=bool).  low=True (float32 [R, ncols] of f64 arrays): the
+        rows' low halves instead (host_stage_lo), for the device fit's f32 pair."""
         dtype = np.dtype(dtype)
         rows = [int(a.shape[0]) for a in arrs]
         R = sum(rows)
@@ -265,6 +306,8 @@ class _PinnedStaging:
         if R == 0:
             if ranges and ncols:
                 self.last_range = (np.full(width, np.inf, np.float32), np.full(width, -np.inf, np.float32))
+            if extras is not None:
+                self.last_extras = dict(pred=None, inexact=False)
             return out
         cur = torch.cuda.current_stream(device)
         cs = self._copy_stream(device)
@@ -292,10 +335,28 @@ class _PinnedStaging:
 
         tr = self.trace
         fill_t = [None] * nchunk
+        xs = None
+        if extras is not None:
+            c = extras.get("coeffs")
+            npred = int(extras["npred"])
+            Tp = int(offs[npred])
+            pv = None
+            if c is not None and Tp:
+                hp = self._host.get(slot + ":pred")
+                if hp is None or hp.numel() < Tp * 8:
+                    hp = self._host[slot + ":pred"] = torch.empty(Tp * 8, dtype=torch.uint8, pin_memory=True)
+                pv = hp[:Tp * 8].numpy().view(np.float64)
+            flags = np.zeros((nchunk, 1), np.int32)
+            xs = [dict(coeffs=None if pv is None else np.ascontiguousarray(c, dtype=np.float64), pred=pv,
+                       npred=npred, flag=flags[k]) for k in range(nchunk)]
 
         def fill(k):
             t0 = time.perf_counter() if tr is not None else 0.0
-            host_stage(arrs, view, offs, bounds[k], bounds[k + 1], *((rng[k, 0], rng[k, 1]) if ranges else ()))
+            if low:
+                host_stage_lo(arrs, view, offs, bounds[k], bounds[k + 1])
+            else:
+                host_stage(arrs, view, offs, bounds[k], bounds[k + 1],
+                           *((rng[k, 0], rng[k, 1]) if ranges else (None, None)), extras=None if xs is None else xs[k])
             if tr is not None:
                 fill_t[k] = (t0, time.perf_counter())
 
@@ -317,6 +378,16 @@ class _PinnedStaging:
                         e1.record(cs)
                         tr.append(dict(slot=slot, bytes=int(b1 - b0), fill=fill_t[k], issue=time.perf_counter(),
                                        ev=(e0, e1)))
+            if xs is not None:
+                pred = None
+                if xs[0]["pred"] is not None:
+                    pv = xs[0]["pred"]
+                    if reuse:
+                        pred = self.device_slot("base", pv.shape[0], np.float64, device)
+                    else:
+                        pred = torch.empty(pv.shape[0], dtype=torch.float64, device=device)
+                    pred.copy_(torch.from_numpy(pv), non_blocking=True)
+                self.last_extras = dict(pred=pred, inexact=bool(flags.any()))
         ev = torch.cuda.Event()
         ev.record(cs)
         self._ev[slot] = ev
@@ -397,6 +468,9 @@ class DeviceBatch:
         self.rewards, self.baseline = rewards, baseline
         self.path_off, self.terminated = path_off, terminated
         self.advantages = advantages
+        # True when obs holds float32 images of values that are not all float32s
+        # (set by from_paths; the device LinearBaseline fit then reads obs_lo too)
+        self.obs_inexact = False
         self.T_demo = int(T_demo)
         self.T = int(obs.shape[0]) - self.T_demo
         self.P = int(path_off.shape[0]) - 1
@@ -442,14 +516,29 @@ class DeviceBatch:
         # pipeline for all three slots measured 52 ms against 32.5 ms this way,
         # tools/staging_ab.py, profiles/r03f/staging_ab.txt)
         orange = None
+        coeffs = _linear_coeffs(baseline, n) if not use_advantages else False
+        hpred, inexact = None, False
         if pre is not None and not demo_paths and pre["obs"].dtype == obs_dtype and pre["obs"].shape == (T, n):
             obs = _STAGING.stage_host("obs", pre["obs"], device, reuse)
             act = _STAGING.stage_host("act", pre["act"], device, reuse)
             if obs_dtype == np.float32 and pre.get("obs_range") is not None:
                 orange = stage("orange", [np.stack(pre["obs_range"]).astype(np.float32)], n, np.float32)
+            # a pool controller's fill (pool._fill_shard) made the same f64 predictions
+            # and exactness check as the extras below
+            inexact = bool(pre.get("inexact", False))
+            if pre.get("pred") is not None and coeffs is not False and coeffs is not None:
+                hpred = stage("base", [pre["pred"]], 0)
         else:
+            # f32 rows of f64 sampler observations: the same pass computes the
+            # LinearBaseline predictions from the f64 values (a4, fp64 as the
+            # reference) and notes whether any value is not a float32 (the fit then
+            # stages the low halves, DeviceBatch.obs_lo)
+            xt = dict(coeffs=coeffs if coeffs is not False else None, npred=len(paths)) \
+                if obs_dtype == np.float32 else None
             obs = stage("obs", [p["observations"] for p in paths] + [p["observations"] for p in demo_paths or []], n,
-                        obs_dtype, ranges=obs_dtype == np.float32)
+                        obs_dtype, ranges=obs_dtype == np.float32, extras=xt)
+            if xt is not None:
+                hpred, inexact = _STAGING.last_extras["pred"], _STAGING.last_extras["inexact"]
             if obs_dtype == np.float32:
                 orange = stage("orange", [np.stack(_STAGING.last_range)], n, np.float32)
             act = stage("act", [p["actions"] for p in paths] + [p["actions"] for p in demo_paths or []], m,
@@ -461,9 +550,12 @@ class DeviceBatch:
         if use_advantages:
             base = None
             adv = stage("adv", [p["advantages"] for p in paths], 0)
-        elif _linear_coeffs(baseline, n) is not False:
+        elif coeffs is not False and hpred is not None:
+            base = hpred   # the host pass's fp64 predictions (linear_baseline.py:46-49)
+            adv = None
+        elif coeffs is not False:
             # LinearBaseline.predict on the device (a4), reading the staged obs
-            coeffs = _linear_coeffs(baseline, n)
+            # (f64 staging: the sampler's values; before the first fit: zeros)
             base = _STAGING.device_slot("base", T, np.float64, device) if reuse else \
                 torch.empty(T, dtype=torch.float64, device=device)
             base.zero_()
@@ -487,7 +579,34 @@ class DeviceBatch:
             adv = None
         b = cls(obs, act, rew, base, off, term, advantages=adv, T_demo=T_demo, obs_range=orange)
         b.lengths = lengths
+        b.obs_inexact = inexact
+        if pre is not None and pre.get("obs_lo") is not None and inexact:
+            b._obs_lo = pre["obs_lo"]   # the controller's low halves, copied on first use
         return b
+
+    def obs_lo(self, paths=None, reuse=True):
+        """The low halves float32(x - float32(x)) of the RL rows' observations
+        (float32 [T, n] on the device) when they were staged as float32 from
+        values that are not all float32s, else None: with obs they give the
+        device LinearBaseline fit the sampler's f64 values to 2^-48.  Staged on
+        first use from `paths` (the batch's own RL paths) on the staging threads."""
+        if not self.obs_inexact or self.obs.dtype != torch.float32:
+            return None
+        lo = getattr(self, "_obs_lo_dev", None)
+        if lo is not None:
+            return lo
+        src = getattr(self, "_obs_lo", None)
+        dev = self.obs.device
+        with torch.cuda.device(dev):
+            if src is not None:   # host float32 [T, n] (a pool segment)
+                lo = _STAGING.stage_host("obs_lo", src, dev, reuse)
+            else:
+                if paths is None or sum(len(p["rewards"]) for p in paths) != self.T:
+                    raise ValueError("DeviceBatch.obs_lo needs the batch's RL paths")
+                lo = _STAGING.stage("obs_lo", [p["observations"] for p in paths], self.obs.shape[1], np.float32, dev,
+                                    reuse, low=True)
+        self._obs_lo_dev = lo
+        return lo
 
 
 # the forward pass assembles the split rows itself where it can (UpdateEngine._fused_pack)
@@ -1261,14 +1380,16 @@ class UpdateEngine:
         return h[0].numpy().copy(), h[1].numpy().copy(), h[2].numpy().copy()
 
     @_on_device
-    def fit_linear_baseline(self, batch, baseline, returns=None, return_errors=False):
+    def fit_linear_baseline(self, batch, baseline, returns=None, return_errors=False, obs_lo=None):
         """LinearBaseline.fit (baselines/linear_baseline.py:20-44) on the batch's
         RL rows already in HBM: the Gram products [F y]^T [F y] on the device
         (mjrl_linear_baseline_gram, all-reduced when sharded), then the
         reference's own lstsq retry loop on the k x k system.  `returns`: f64
         device [T] (default: the returns of the last GAE scan).  Sets
         baseline._coeffs; with return_errors, returns (error_before, error_after)
-        computed from device residuals as the reference does."""
+        computed from device residuals as the reference does.  obs_lo: the low
+        halves of f32-staged observations (DeviceBatch.obs_lo): the features are
+        then formed from hi + lo, the sampler's f64 values to 2^-48."""
         L = self.lib
         st = _lib.stream_ptr()
         n, T, P = int(batch.obs.shape[1]), batch.T, batch.P
@@ -1280,16 +1401,24 @@ class UpdateEngine:
         scratch = torch.empty(max(nd.value, 1), **f64)
         gram = torch.zeros((k + 1, k + 1), **f64)
         f32 = batch.obs.dtype == torch.float32
-        gram_fn = L.mjrl_linear_baseline_gram_f32 if f32 else L.mjrl_linear_baseline_gram
-        res_fn = L.mjrl_linear_baseline_residual_f32 if f32 else L.mjrl_linear_baseline_residual
-        _lib.check(gram_fn(_lib.ptr(batch.obs), _lib.ptr(y), T, n, _lib.ptr(batch.path_off), P,
+        if f32 and obs_lo is not None:
+            if obs_lo.dtype != torch.float32 or obs_lo.shape[0] < T or obs_lo.shape[1] != n:
+                raise ValueError("fit_linear_baseline: obs_lo must be float32 [T, n]")
+            gram_fn = functools.partial(L.mjrl_linear_baseline_gram_f32x2, _lib.ptr(batch.obs))
+            res_fn = functools.partial(L.mjrl_linear_baseline_residual_f32x2, _lib.ptr(batch.obs))
+            obs_arg = _lib.ptr(obs_lo)
+        else:
+            gram_fn = L.mjrl_linear_baseline_gram_f32 if f32 else L.mjrl_linear_baseline_gram
+            res_fn = L.mjrl_linear_baseline_residual_f32 if f32 else L.mjrl_linear_baseline_residual
+            obs_arg = _lib.ptr(batch.obs)
+        _lib.check(gram_fn(obs_arg, _lib.ptr(y), T, n, _lib.ptr(batch.path_off), P,
                            _lib.ptr(scratch), _lib.ptr(gram), st), "mjrl_linear_baseline_gram")
         self.comm.allreduce_sum(gram)
 
         def sse(coeffs):
             r = torch.empty(max(T, 1), **f64)
             c = torch.from_numpy(np.ascontiguousarray(coeffs, dtype=np.float64)).to(self.device)
-            _lib.check(res_fn(_lib.ptr(batch.obs), _lib.ptr(y), T, n, _lib.ptr(batch.path_off), P, _lib.ptr(c),
+            _lib.check(res_fn(obs_arg, _lib.ptr(y), T, n, _lib.ptr(batch.path_off), P, _lib.ptr(c),
                               _lib.ptr(scratch), _lib.ptr(r), st), "mjrl_linear_baseline_residual")
             out = torch.zeros(8, **f64)
             part = torch.empty(4 * 256, **f64)

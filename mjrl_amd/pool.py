@@ -91,7 +91,15 @@ class _Layout:
         f32, f64, i64 = np.dtype(np.float32), np.dtype(np.float64), np.dtype(np.int64)
         off = 0
         self.fields = {}
+        x = dt == f32 and not with_adv
+        # float32 layouts of sampled paths also carry the controller's f64
+        # LinearBaseline predictions ('pred_in'), the low halves of the
+        # observations ('obs_lo', written only when some value is not a float32:
+        # the untouched pages of a shared segment cost no memory) and two flags
+        # ('xflags': [inexact, predictions present])
         for name, count, ft in (("obs", T * n, dt), ("act", T * m, dt), ("orange", 2 * n if dt == f32 else 0, f32),
+                                ("pred_in", T if x else 0, f64), ("obs_lo", T * n if x else 0, f32),
+                                ("xflags", 2 if x else 0, i64),
                                 ("rew", T, f64), ("lengths", P, i64), ("term", P, i64),
                                 ("adv_in", T if with_adv else 0, f64), ("ret", T, f64), ("base", T, f64),
                                 ("adv", T, f64)):
@@ -111,12 +119,13 @@ def _segment_dtype(agent):
     Otherwise float64: MLPBaseline builds its features from the path
     observations on the host (clip(o) / 10 in f64, mlp_baseline.py:37-56), which
     float32 views of a segment would round first."""
-    f32 = np.dtype(getattr(agent, "staging_dtype", np.float64)) == np.float32
+    f32 = (agent.staging_obs_dtype() if hasattr(agent, "staging_obs_dtype")
+           else np.dtype(getattr(agent, "staging_dtype", np.float64))) == np.float32
     dev_fit = type(getattr(agent, "baseline", None)).__name__ == "LinearBaseline"
     return np.float32 if (f32 and dev_fit) else np.float64
 
 
-def _fill_shard(buf, L, sh, lengths, ex=None, chunk_rows=None, threads=1):
+def _fill_shard(buf, L, sh, lengths, ex=None, chunk_rows=None, threads=1, coeffs=None):
     """The shard's paths `sh` into its segment.  float32 layouts: the native
     convert-and-range pass (engine.host_stage, the staging path's own) writes
     obs / act and the per-column (min, max) of obs into 'orange'.  ex: a thread
@@ -124,7 +133,10 @@ def _fill_shard(buf, L, sh, lengths, ex=None, chunk_rows=None, threads=1):
     (default: two chunks per pool thread, `threads` of them, at least 1024 rows;
     a fixed 64k rows left half of 16 threads idle on a 500k-row shard), converted in parallel
     (ctypes releases the GIL), their ranges folded; the 1-D slots go through the
-    same native gather as the staging path's."""
+    same native gather as the staging path's.  Layouts with the 'pred_in' field:
+    the same pass makes the f64 LinearBaseline predictions from `coeffs` (None:
+    before the first fit) and the exactness check of the staging path
+    (engine.host_stage extras), and a second pass the low halves when needed."""
     lengths = np.asarray(lengths, dtype=np.int64)
     offs = np.concatenate([[0], np.cumsum(lengths)])
     if chunk_rows is None:
@@ -141,12 +153,17 @@ def _fill_shard(buf, L, sh, lengths, ex=None, chunk_rows=None, threads=1):
     rng[:, 0], rng[:, 1] = np.inf, -np.inf
     obs_v, act_v = L.view(buf, "obs").reshape(L.T, L.n), L.view(buf, "act").reshape(L.T, L.m)
     if f32:
-        from .engine import host_stage
+        from .engine import host_stage, host_stage_lo
+    xt = L.fields["pred_in"][1] > 0
+    flags = np.zeros((max(nchunk, 1), 1), np.int32)
+    pred_v = L.view(buf, "pred_in") if xt else None
+    cf = None if coeffs is None else np.ascontiguousarray(coeffs, dtype=np.float64)
 
     def conv(k):
         a0, a1 = bounds[k], bounds[k + 1]
         if f32:
-            host_stage([p["observations"] for p in sh], obs_v, offs, a0, a1, rng[k, 0], rng[k, 1])
+            host_stage([p["observations"] for p in sh], obs_v, offs, a0, a1, rng[k, 0], rng[k, 1],
+                       extras=dict(coeffs=cf, pred=pred_v, npred=len(sh), flag=flags[k]) if xt else None)
             host_stage([p["actions"] for p in sh], act_v, offs, a0, a1)
         else:
             for i in range(a0, a1):
@@ -158,6 +175,19 @@ def _fill_shard(buf, L, sh, lengths, ex=None, chunk_rows=None, threads=1):
     else:
         for k in range(nchunk):
             conv(k)
+    if xt:
+        inexact = bool(flags.any())
+        L.view(buf, "xflags")[:] = (int(inexact), int(cf is not None))
+        if inexact:
+            lo_v = L.view(buf, "obs_lo").reshape(L.T, L.n)
+
+            def low(k):
+                host_stage_lo([p["observations"] for p in sh], lo_v, offs, bounds[k], bounds[k + 1])
+            if ex is not None and nchunk > 1:
+                list(ex.map(low, range(nchunk)))
+            else:
+                for k in range(nchunk):
+                    low(k)
     if sh:
         from .engine import host_stage
         if f32:
@@ -368,6 +398,9 @@ class DevicePool:
                              % (len(paths), self.world))
         with_adv = mode == "paths"
         dtype = _segment_dtype(agent)
+        from .engine import _linear_coeffs
+        c = _linear_coeffs(getattr(agent, "baseline", None), n) if not with_adv else False
+        coeffs = None if c is False or c is None else c
         try:
             t0 = time.perf_counter()
             state = self._state(agent)
@@ -382,7 +415,7 @@ class DevicePool:
                 p0, p1 = parts[r]
                 L = _Layout(int(lengths[p0:p1].sum()), p1 - p0, n, m, with_adv, dtype)
                 _fill_shard(self._segment(r, L.nbytes).buf, L, paths[p0:p1], lengths[p0:p1], self._fill_pool(),
-                            threads=self._fill_threads)
+                            threads=self._fill_threads, coeffs=coeffs)
                 layouts.append(L)
                 self._conns[r].send(("step", dict(state=state, shm=self._shm[r].name, T=L.T, P=L.P, n=n, m=m,
                                                   dtype=L.dtype.str, mode=mode, gamma=gamma, gae_lambda=gae_lambda,
@@ -512,6 +545,10 @@ def _worker_main(args):
                 # the segment is the staged batch: copied to HBM as it is
                 agent._pre = dict(obs=L.view(shm.buf, "obs").reshape(L.T, L.n),
                                   act=L.view(shm.buf, "act").reshape(L.T, L.m), obs_range=(rng[0], rng[1]))
+                if L.fields["xflags"][1]:
+                    inexact, has_pred = (bool(v) for v in L.view(shm.buf, "xflags"))
+                    agent._pre.update(inexact=inexact, pred=L.view(shm.buf, "pred_in") if has_pred else None,
+                                      obs_lo=L.view(shm.buf, "obs_lo").reshape(L.T, L.n) if inexact else None)
             key = (agent.policy.n, agent.policy.m, agent.policy.hidden)
             agent._engine = engines.get(key)
             np.random.set_state(a["rng"])
@@ -543,6 +580,7 @@ def _worker_main(args):
             from .engine import _STAGING
             _STAGING.wait_host("obs")
             _STAGING.wait_host("act")
+            _STAGING.wait_host("obs_lo")
             conn.send(("ok", out))
         except Exception:
             conn.send(("error", traceback.format_exc()))

@@ -422,6 +422,37 @@ def regen_inputs(seed, n, m, lengths, col_scale=None, spiky=None, act_scale=None
     return np.concatenate(obs), np.concatenate(act), np.concatenate(rew)
 
 
+def regen_f64obs(seed, n, lengths, col_scale=None, spiky=None):
+    """The f64-observation fixtures' inputs (tests/golden/make_golden.py:f64obs_case)
+    replayed from np.random.RandomState(seed): per path obs randn(H, n) (spiky
+    columns zeroed where |draw| <= 1.5, times the column scales) kept in f64, then
+    rewards randn(H).  Returns the per-path lists (obs, rewards)."""
+    rs = np.random.RandomState(int(seed))
+    obs, rew = [], []
+    for H in lengths:
+        o = rs.randn(int(H), n)
+        if spiky is not None:
+            o[:, spiky] *= np.abs(o[:, spiky]) > 1.5
+        if col_scale is not None:
+            o = o * col_scale
+        obs.append(o)
+        rew.append(rs.randn(int(H)))
+    return obs, rew
+
+
+def load_f64obs(path):
+    """An f64-observation fixture with its inputs regenerated and checked against
+    the stored checksum: dict of the .npz arrays plus obs_paths / rew_paths."""
+    z = np.load(path, allow_pickle=False)
+    c = {k: z[k] for k in z.files}
+    obs, rew = regen_f64obs(c["gen_seed"], int(c["n"]), c["lengths"], col_scale=c.get("col_scale"),
+                            spiky=c["spiky"].astype(bool) if "spiky" in c else None)
+    if _sha(np.concatenate(obs), np.concatenate(rew)) != str(c["inputs_sha256"]):
+        raise ValueError("%s: regenerated inputs do not match the fixture's checksum" % path)
+    c["obs_paths"], c["rew_paths"] = obs, rew
+    return c
+
+
 def _sha(*arrs):
     import hashlib
     return hashlib.sha256(b"".join(np.ascontiguousarray(a).tobytes() for a in arrs)).hexdigest()

@@ -554,6 +554,88 @@ def mlp_baseline_case():
     print("mlp_baseline errors", out["err0"], out["err1"])
 
 
+def f64obs_case(name, n, lengths, terminated, seed, col_scale=None, spiky=None, gamma=0.995, gae_lambda=0.97):
+    """The baseline / GAE chain on observations that are NOT float32s (MuJoCo's are
+    f64): obs = randn(H, n) (spiky columns zeroed where |draw| <= 1.5, times the
+    column scales) kept in f64, then rewards randn(H), per path from
+    RandomState(seed) (oracle.npg_cpu.regen_f64obs replays it; the inputs are not
+    stored, their SHA-256 is).  Reference calls: LinearBaseline.fit on the first
+    half of the paths (coeffs0: the previous iteration's baseline,
+    linear_baseline.py:20-44), compute_returns + compute_advantages with it on all
+    paths (process_samples.py:3-35, predict :23), then fit(return_errors=True) on
+    all paths (coeffs1, err); MLPBaseline._features(paths).astype('float32')
+    (mlp_baseline.py:37-56, 64), stored as a checksum and its first rows."""
+    import hashlib
+    saved = {k: os.environ.get(k) for k in ("CUDA_VISIBLE_DEVICES", "CUDA_DEVICE_ORDER", "MKL_THREADING_LAYER")}
+    from mjrl.baselines.mlp_baseline import MLPBaseline as RefMLP   # sets CUDA_VISIBLE_DEVICES at import
+    for k, v in saved.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
+    rs = np.random.RandomState(seed)
+    paths = []
+    for H, term in zip(lengths, terminated):
+        obs = rs.randn(H, n)
+        if spiky is not None:
+            obs[:, spiky] *= np.abs(obs[:, spiky]) > 1.5
+        if col_scale is not None:
+            obs = obs * col_scale
+        paths.append(dict(observations=obs, rewards=rs.randn(H), terminated=bool(term)))
+    obs = concat(paths, "observations")
+    assert np.mean(obs.astype(np.float32).astype(np.float64) != obs) > 0.5   # genuinely f64
+    spec = EnvSpec(n, 1, max(lengths), 1)
+    process_samples.compute_returns(paths, gamma)
+    lin = LinearBaseline(spec)
+    lin.fit(paths[: len(paths) // 2])
+    coeffs0 = lin._coeffs.copy()
+    process_samples.compute_advantages(paths, lin, gamma, gae_lambda)
+    err = lin.fit(paths, return_errors=True)
+    # the reference's own sensitivity of that fit to the order its paths arrive in
+    # (two path permutations: the normal equations summed in another order); at
+    # Humanoid column scales the k x k system is ill-conditioned enough that this,
+    # not the 1e-10 of a well-conditioned fit, is the attainable bar
+    spread = 0.0
+    for ps in (1, 2):
+        order = np.random.RandomState(ps).permutation(len(paths))
+        alt = LinearBaseline(spec)
+        alt.fit([paths[i] for i in order])
+        spread = max(spread, float(np.linalg.norm(alt._coeffs - lin._coeffs)))
+    feat = RefMLP(spec)._features(paths).astype("float32")
+    sha = lambda *arrs: hashlib.sha256(b"".join(np.ascontiguousarray(a).tobytes() for a in arrs)).hexdigest()
+    out = dict(n=np.int64(n), lengths=np.array(lengths, np.int64), terminated=np.array(terminated, np.uint8),
+               gen_seed=np.int64(seed), gamma=np.float64(gamma), gae_lambda=np.float64(gae_lambda),
+               inputs_sha256=np.array(sha(obs, concat(paths, "rewards"))), coeffs0=coeffs0,
+               baseline=concat(paths, "baseline"), returns=concat(paths, "returns"),
+               advantages=concat(paths, "advantages"), coeffs1=lin._coeffs.copy(), err=np.array(err, np.float64),
+               coeffs1_spread=np.float64(spread),
+               mlp_feat_sha256=np.array(sha(feat)), mlp_feat_head=feat[:64])
+    if col_scale is not None:
+        out["col_scale"] = col_scale
+    if spiky is not None:
+        out["spiky"] = np.asarray(spiky, np.uint8)
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), **out)
+    print("%-22s T=%-6d n=%-4d inexact %.3f err %s fit spread %.3g" % (
+        name, obs.shape[0], n, np.mean(obs.astype(np.float32).astype(np.float64) != obs), err,
+        spread / np.linalg.norm(lin._coeffs)))
+
+
+def f64obs_cases():
+    # Swimmer width, ragged lengths with terminated paths, values past the +-10 clip
+    rs = np.random.RandomState(606)
+    lengths = [500] * 20 + list(rs.randint(1, 500, size=5))
+    term = [False] * 20 + [True, False, True, True, False]
+    f64obs_case("f64obs_swimmer", 8, lengths, term, seed=607, col_scale=np.array([1, 3, 12, 0.5, 8, 2, 30, 0.1]))
+    # Humanoid width with Humanoid-like columns: scales 10^U(-4, 3), every 7th
+    # column contact-force-like (mostly zero), so many values sit past the clip
+    crs = np.random.RandomState(608)
+    col_scale = 10.0 ** crs.uniform(-4, 3, size=376)
+    spiky = np.zeros(376, bool)
+    spiky[::7] = True
+    f64obs_case("f64obs_humanoid", 376, [1000] * 8 + [517, 1, 1000, 250], [False] * 8 + [True, True, False, True],
+                seed=609, col_scale=col_scale, spiky=spiky)
+
+
 def bc_case():
     """Reference BC (behavior_cloning.py:11-68): MLE of expert actions by minibatch
     Adam, minibatches from np.random.choice after np.random.seed(17); the
@@ -613,6 +695,10 @@ def ppo_case():
 
 
 if __name__ == "__main__":
+    if not ONLY or "f64obs" in ONLY:
+        f64obs_cases()
+    if ONLY == {"f64obs"}:
+        sys.exit(0)
     main()
     if not ONLY or "baselines" in ONLY:
         baselines_case()

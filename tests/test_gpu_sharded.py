@@ -199,3 +199,62 @@ def test_sharded_graph_replay_is_bit_identical(rccl, name):
         assert np.array_equal(eng.vec["theta_new"].cpu().numpy(), th_eager)
         assert r["base_stats"] == r_eager["base_stats"]
         assert r["kl_dist"] == r_eager["kl_dist"] and r["alpha"] == r_eager["alpha"]
+
+
+@pytest.fixture(scope="module")
+def torch_nccl():
+    """A one-rank torch.distributed group on the nccl (= RCCL) backend in this
+    process: the fallback comm of an N-GPU run (MJRL_AMD_COMM=torch: torch's own
+    collectives, eager)."""
+    import socket
+    import torch.distributed as dist
+    if dist.is_initialized():
+        pytest.skip("a process group is already initialised in this process")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1,
+                            device_id=DEV)
+    try:
+        yield dist
+    finally:
+        from mjrl_amd.comm import release_comms
+        release_comms()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name", ["c4_humanoid", "c3_halfcheetah_trpo"])
+def test_sharded_path_torch_collectives_eager(torch_nccl, monkeypatch, name):
+    """The escape hatch if the captured RCCL path misbehaves at N > 1:
+    MJRL_AMD_COMM=torch selects torch.distributed's collectives on the nccl group
+    (comm.DistComm), the sharded schedule runs eager (graphs off), and the update
+    equals the one-process update bit for bit."""
+    from mjrl_amd.comm import DistComm, LocalComm, _group_comm
+    monkeypatch.setenv("MJRL_AMD_COMM", "torch")
+    comm = _group_comm()
+    assert type(comm) is DistComm and torch_nccl.get_backend() == "nccl"
+    comm = DistComm(force_sharded=True)
+    c = _case(name)
+    th0 = _t(c["theta0"].astype(np.float32))
+    res, th = {}, {}
+    for key, cm in (("local", LocalComm()), ("torch", comm)):
+        eng = _engine(c, cm)
+        eng.graphs = False
+        res[key] = eng.update(_batch(c), th0, **_args(c))
+        th[key] = eng.vec["theta_new"].cpu().numpy()
+    assert np.array_equal(th["torch"], th["local"])
+    assert res["torch"]["base_stats"] == res["local"]["base_stats"]
+    assert res["torch"]["kl_dist"] == res["local"]["kl_dist"] and res["torch"]["alpha"] == res["local"]["alpha"]
+
+
+def test_rccl_cache_rebuilds_for_a_new_group(torch_nccl, monkeypatch):
+    """comm._group_comm's cached RcclComm belongs to the live group: the same
+    object while the group lives, a new one for another group object."""
+    from mjrl_amd.comm import RcclComm, _group_comm
+    monkeypatch.setenv("MJRL_AMD_COMM", "rccl")
+    a = _group_comm()
+    assert isinstance(a, RcclComm) and _group_comm() is a
+    g2 = torch_nccl.new_group([0])
+    b = _group_comm(g2)
+    assert b is not a and _group_comm(g2) is b

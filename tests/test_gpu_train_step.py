@@ -52,7 +52,8 @@ def _steps(agent, k=2):
         out.append(dict(stats=stats, seed=agent.seed, theta0=th0, theta=agent.policy.get_param_values(),
                         g=agent.engine().vec["g"].cpu().numpy(),
                         coeffs0=coeffs0, coeffs=agent.baseline._coeffs.copy(),
-                        paths=[{k: p[k] for k in ("observations", "actions", "rewards", "terminated", "returns")}
+                        paths=[{k: p[k] for k in ("observations", "actions", "rewards", "terminated", "returns",
+                                                  "baseline", "advantages")}
                                for p in stub_samplers.LAST],
                         log={k: list(v) for k, v in agent.logger.log.items()}))
     return out
@@ -76,6 +77,19 @@ def test_train_step_one_gpu_matches_oracle(linear):
         base = O.linear_baseline_predict(r["coeffs0"], obs, lengths)
         ret, adv = O.returns_and_advantages(rew, base, lengths, term, 0.99, 0.95)
         assert np.array_equal(np.concatenate([p["returns"] for p in paths]), ret)   # written back, bit-exact
+        # the stub's observations are f64 randn (not float32s): the default f32
+        # staging still predicts from the f64 values (1e-12 of the fp64
+        # LinearBaseline.predict), and the written-back advantages are the GAE of
+        # those predictions bit for bit
+        got_base = np.concatenate([p["baseline"] for p in paths])
+        if r["coeffs0"] is not None:
+            bound = np.concatenate([np.abs(O.linear_baseline_features(o)).dot(np.abs(r["coeffs0"]))
+                                    for o in O.split(obs, lengths)])
+            assert np.all(np.abs(got_base - base) <= 1e-12 * bound)
+        else:
+            assert np.array_equal(got_base, base)
+        _, adv_given = O.returns_and_advantages(rew, got_base, lengths, term, 0.99, 0.95)
+        assert np.array_equal(np.concatenate([p["advantages"] for p in paths]), adv_given)
         np.testing.assert_allclose(r["stats"][:4], O.path_return_stats(rew, lengths), rtol=1e-12)
         pol = O.Policy(N_OBS, N_ACT, None if linear else HID, r["theta0"].astype(np.float64), None)
         ref = O.update(pol, obs, act, adv, rew, lengths, algo="npg", n_step_size=0.05)
@@ -85,8 +99,8 @@ def test_train_step_one_gpu_matches_oracle(linear):
         # the device LinearBaseline fit (all-reduced Gram + the reference's lstsq loop)
         host = LinearBaseline(EnvSpec(N_OBS, N_ACT, 100, 1))
         host.fit([dict(p) for p in paths])
-        # the device fit reads the f32-staged observations (BatchREINFORCE.staging_dtype)
-        np.testing.assert_allclose(r["coeffs"], host._coeffs, rtol=1e-5, atol=1e-8)
+        # the device fit reads the f32-staged rows AND their low halves (the f64 values)
+        assert np.linalg.norm(r["coeffs"] - host._coeffs) <= 1e-10 * np.linalg.norm(host._coeffs)
     for k in ("time_sampling", "time_VF", "VF_error_before", "VF_error_after", "alpha", "kl_dist",
               "stoc_pol_mean", "running_score"):
         assert len(res[-1]["log"][k]) == 2, k

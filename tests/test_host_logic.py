@@ -232,3 +232,15 @@ def test_mlp_baseline_device_mirror_tracks_cpu_parameters():
     p.data = p.data.clone()
     assert b._cpu_key() != k1
     assert b._cpu_key() == b._cpu_key()
+
+
+def test_bench_pmc_key_matches_committed_summary():
+    """bench.py's roofline.traffic comes from the newest committed PMC summary:
+    the key it builds for the default workload's FVP kernel (k_kx<32, 12, 1,
+    false> at Humanoid: MP 32, NP 384) must name an entry of that file (round 5
+    printed traffic: null after the kernel gained a template argument)."""
+    import bench
+    name, key = bench.fvp_kernel_key(2, True, 32, 384, 64, 64)
+    assert key == "k_kx<32, 12, 1, false>"
+    b, src, err = bench.pmc_traffic(key)
+    assert err is None and b > 2.0e9, (src, err)

@@ -154,3 +154,124 @@ def test_moment_records_combine_to_global_moments(sizes):
     if len(sizes) == 1:
         rec = O.moments_record(x)
         assert out[9] == rec[9] and out[8] == rec[8]
+
+
+F64OBS = ["f64obs_swimmer", "f64obs_humanoid"]
+
+
+def _f64obs(name):
+    import os
+    from oracle import npg_cpu as O
+    return O.load_f64obs(os.path.join(os.path.dirname(__file__), "golden", name + ".npz"))
+
+
+def _pred_bound(coeffs, obs_paths):
+    """|f . c| summed termwise: the scale a 1e-12 relative bound on a dot product
+    of these features is taken against (a prediction near zero by cancellation
+    carries the rounding of its large terms)."""
+    from oracle import npg_cpu as O
+    return np.concatenate([np.abs(O.linear_baseline_features(o)).dot(np.abs(coeffs)) for o in obs_paths])
+
+
+@pytest.mark.parametrize("name", F64OBS)
+def test_oracle_pinned_on_f64_observations(name):
+    """The oracle's returns / GAE and LinearBaseline predict / fit against what the
+    reference computed on observations that are not float32s."""
+    from oracle import npg_cpu as O
+    c = _f64obs(name)
+    obs, rew, lengths = np.concatenate(c["obs_paths"]), np.concatenate(c["rew_paths"]), c["lengths"]
+    term = c["terminated"].astype(bool)
+    pred = O.linear_baseline_predict(c["coeffs0"], obs, lengths)
+    assert np.all(np.abs(pred - c["baseline"]) <= 1e-12 * _pred_bound(c["coeffs0"], c["obs_paths"]))
+    ret, adv = O.returns_and_advantages(rew, c["baseline"], lengths, term, float(c["gamma"]), float(c["gae_lambda"]))
+    assert np.array_equal(ret, c["returns"]) and np.array_equal(adv, c["advantages"])
+    coeffs = O.linear_baseline_fit(obs, c["returns"], lengths)
+    assert np.linalg.norm(coeffs - c["coeffs1"]) <= fit_bound(c)
+
+
+def fit_bound(c):
+    """Bound on ||coeffs - reference's||: 1e-10 relative, or 3x the reference's
+    own spread over path orders where its normal equations are ill-conditioned
+    (Humanoid column scales: cond ~1e10, the spread ~5e-7 relative)."""
+    return max(1e-10 * np.linalg.norm(c["coeffs1"]), 3.0 * float(c["coeffs1_spread"]))
+
+
+@pytest.mark.parametrize("name", F64OBS)
+def test_host_stage_extras_on_f64_observations(lib, name):
+    """The staging pass's LinearBaseline extras (mjrl_host_stage_paths_f64x): the
+    fp64 predictions from the sampler's own values within 1e-12 of the
+    reference's LinearBaseline.predict, the advantages the GAE makes of them
+    within the same bound of the reference's, the inexact flag raised, and the
+    low halves carrying every value to 2^-48 (the device fit's f32 pair)."""
+    from oracle import npg_cpu as O
+    from mjrl_amd.engine import host_stage, host_stage_lo
+    c = _f64obs(name)
+    arrs, lengths = c["obs_paths"], c["lengths"]
+    n = int(c["n"])
+    offs = np.concatenate([[0], np.cumsum(lengths)])
+    T = int(offs[-1])
+    view = np.empty((T, n), np.float32)
+    lo, hi = np.full(n, np.inf, np.float32), np.full(n, -np.inf, np.float32)
+    pred, flag = np.full(T, np.nan), np.zeros(1, np.int32)
+    mid = len(arrs) // 2   # two chunks, as the staging threads cut them
+    for a0, a1 in ((0, mid), (mid, len(arrs))):
+        host_stage(arrs, view, offs, a0, a1, lo, hi, extras=dict(coeffs=c["coeffs0"], pred=pred, npred=len(arrs),
+                                                                 flag=flag))
+    obs = np.concatenate(arrs)
+    assert np.array_equal(view, obs.astype(np.float32))
+    assert flag[0] == 1
+    bound = 1e-12 * _pred_bound(c["coeffs0"], arrs)
+    assert np.all(np.abs(pred - c["baseline"]) <= bound)
+    _, adv = O.returns_and_advantages(np.concatenate(c["rew_paths"]), pred, lengths, c["terminated"].astype(bool),
+                                      float(c["gamma"]), float(c["gae_lambda"]))
+    np.testing.assert_allclose(adv, c["advantages"], rtol=0, atol=1e-10 * np.abs(c["advantages"]).max())
+    low = np.empty_like(view)
+    host_stage_lo(arrs, low, offs, 0, len(arrs))
+    rec = view.astype(np.float64) + low
+    assert np.all(np.abs(rec - obs) <= 2.0 ** -48 * np.abs(obs))
+    # the fit from hi + lo (the device Gram's input) matches the reference's fit
+    assert np.linalg.norm(O.linear_baseline_fit(rec, c["returns"], lengths) - c["coeffs1"]) <= fit_bound(c)
+
+
+def test_host_stage_extras_portable_and_specials(lib):
+    """The AVX-512 extras equal the portable loop's (NaN propagates through the
+    clip as np.clip does, values past the float range, masked column tails), the
+    flag stays 0 for float32-representable input, demo arrays (past npred) get no
+    prediction, and a value past the float range gets a zero low half."""
+    from mjrl_amd import _lib
+    from mjrl_amd.engine import host_stage, host_stage_lo
+    from oracle import npg_cpu as O
+    L = _lib.stage_lib()
+    rs = np.random.RandomState(8)
+    for n in (1, 7, 8, 9, 37, 376):
+        arrs = [rs.standard_normal((H, n)) * 6 for H in (3, 250, 1)]
+        arrs[1][5, 0] = np.nan
+        arrs[1][6, n - 1] = 1e39
+        coeffs = rs.standard_normal(n + 4)
+        offs = np.concatenate([[0], np.cumsum([len(a) for a in arrs])])
+        view = np.empty((offs[-1], n), np.float32)
+        pred, flag = np.full(offs[2], -7.0), np.zeros(1, np.int32)
+        host_stage(arrs, view, offs, 0, 3, extras=dict(coeffs=coeffs, pred=pred, npred=2, flag=flag))
+        ref = O.linear_baseline_predict(coeffs, np.concatenate(arrs[:2]), [3, 250])
+        assert np.array_equal(np.isnan(pred), np.isnan(ref))
+        ok = ~np.isnan(ref)
+        assert np.all(np.abs(pred[ok] - ref[ok]) <= 1e-12 * _pred_bound(coeffs, arrs[:2])[ok])
+        assert flag[0] == 1
+        import ctypes as C
+        for a, o0 in zip(arrs[:2], offs[:2]):
+            pp, fl = np.zeros(len(a)), np.zeros(1, np.int32)
+            assert L.mjrl_host_extras_portable(a.ctypes.data, len(a), n, coeffs.ctypes.data, pp.ctypes.data,
+                                               fl.ctypes.data) == 0
+            got = pred[o0:o0 + len(a)]
+            assert np.array_equal(np.isnan(pp), np.isnan(got))
+            m = ~np.isnan(pp)
+            assert np.all(np.abs(pp[m] - got[m]) <= 1e-13 * (np.abs(got[m]) + 1))
+        low = np.empty_like(view)
+        host_stage_lo(arrs, low, offs, 0, 3)
+        assert low[offs[1] + 6, n - 1] == 0.0 and np.isinf(view[offs[1] + 6, n - 1])
+        exact = [a.astype(np.float32).astype(np.float64) for a in arrs[:1]] + [np.zeros((4, n))]
+        eoffs = np.concatenate([[0], np.cumsum([len(a) for a in exact])])
+        flag[0] = 0
+        host_stage(exact, np.empty((eoffs[-1], n), np.float32), eoffs, 0, 2,
+                   extras=dict(coeffs=None, pred=None, npred=2, flag=flag))
+        assert flag[0] == 0

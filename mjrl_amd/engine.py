@@ -508,8 +508,8 @@ class DeviceBatch:
         dlen = [len(p["observations"]) for p in (demo_paths or [])]
         T_demo = int(sum(dlen))
 
-        def stage(slot, arrs, ncols, dtype=np.float64, ranges=False):
-            return _STAGING.stage(slot, arrs, ncols, dtype, device, reuse, ranges=ranges)
+        def stage(slot, arrs, ncols, dtype=np.float64, ranges=False, extras=None):
+            return _STAGING.stage(slot, arrs, ncols, dtype, device, reuse, ranges=ranges, extras=extras)
 
         # slot after slot: each stage() returns once its copies are issued, so the
         # next slot's conversion overlaps the previous slot's H2D tail (one chunked

@@ -17,7 +17,7 @@ __global__ void __launch_bounds__(64) k_chain(const double* __restrict__ in, dou
     const int lane = threadIdx.x;
     for (int i = lane; i < 2048; i += 64) src[i] = in[i];
     __syncthreads();
-    if (lane < 3) {
+    if (lane < (MODE == 8 ? 64 : 3)) {
         double acc = 0.0;
         double xv[GU];
 #pragma unroll
@@ -56,6 +56,29 @@ __global__ void __launch_bounds__(64) k_chain(const double* __restrict__ in, dou
             } else if (MODE == 4) {   // fused multiply-add (NOT the reference's rounding: latency only)
 #pragma unroll
                 for (int u = 0; u < GU; ++u) acc = __fma_rn(c, acc, xv[u]);
+            } else if (MODE == 6) {   // outputs of batch j - 1 stored while batch j's chain runs
+                double o[GU];
+#pragma unroll
+                for (int u = 0; u < GU; ++u) {
+                    acc = __dadd_rn(xv[u], __dmul_rn(c, acc));
+                    o[u] = acc;
+                    if (u % 8 == 7) {
+#pragma unroll
+                        for (int q = u - 7; q <= u; ++q) dst[((base + q) & 1023)] = o[q];
+                    }
+                }
+            } else if (MODE == 7) {   // outputs to global memory, one batch of stores
+                double o[GU];
+#pragma unroll
+                for (int u = 0; u < GU; ++u) {
+                    acc = __dadd_rn(xv[u], __dmul_rn(c, acc));
+                    o[u] = acc;
+                }
+#pragma unroll
+                for (int u = 0; u < GU; ++u) out[64 + ((base + u) & 1023) * 4 + lane] = o[u];
+            } else if (MODE == 8) {   // mul -> add with every lane active (lane count)
+#pragma unroll
+                for (int u = 0; u < GU; ++u) acc = __dadd_rn(xv[u], __dmul_rn(c, acc));
             } else if (MODE == 5) {   // two independent chains interleaved (latency vs issue)
                 double acc2 = acc;
 #pragma unroll
@@ -66,7 +89,7 @@ __global__ void __launch_bounds__(64) k_chain(const double* __restrict__ in, dou
                 acc += acc2;
             }
         }
-        out[lane] = acc + dst[lane];
+        out[lane] = acc + dst[lane & 1023];
     }
 }
 
@@ -88,15 +111,17 @@ float run(const double* in, double* out, int nb, int reps) {
 int main() {
     double *in, *out;
     hipMalloc(&in, 2048 * sizeof(double));
-    hipMalloc(&out, 64 * sizeof(double));
+    hipMalloc(&out, (64 + 4096) * sizeof(double));
     double h[2048];
     for (int i = 0; i < 2048; ++i) h[i] = 0.001 * (i % 97) - 0.03;
     hipMemcpy(in, h, sizeof(h), hipMemcpyHostToDevice);
     const int nb = 4096;   // 131072 steps per launch
     const char* names[] = {"mul->add registers", "+ LDS store per step", "+ next batch LDS reads (k_gae)",
                            "outputs in registers, one store batch", "fma (latency only)",
-                           "two chains interleaved (per chain step)"};
-    float t[6];
+                           "two chains interleaved (per chain step)", "outputs stored every 8 steps",
+                           "outputs to global, one store batch", "mul->add, all 64 lanes active"};
+    constexpr int NM = 9;
+    float t[NM];
     for (int pass = 0; pass < 2; ++pass) {
         t[0] = run<0>(in, out, nb, 5);
         t[1] = run<1>(in, out, nb, 5);
@@ -104,11 +129,14 @@ int main() {
         t[3] = run<3>(in, out, nb, 5);
         t[4] = run<4>(in, out, nb, 5);
         t[5] = run<5>(in, out, nb, 5);
+        t[6] = run<6>(in, out, nb, 5);
+        t[7] = run<7>(in, out, nb, 5);
+        t[8] = run<8>(in, out, nb, 5);
     }
     int clk = 0;
     hipDeviceGetAttribute(&clk, hipDeviceAttributeClockRate, 0);
     printf("gfx950 serial fp64 chain, one wave, %d steps per launch, shader clock %.0f MHz\n", nb * GU, clk / 1e3);
-    for (int i = 0; i < 6; ++i) {
+    for (int i = 0; i < NM; ++i) {
         const double ns = t[i] * 1e6 / (nb * GU);
         printf("%-42s %7.3f ns/step  %6.1f cycles/step\n", names[i], ns, ns * clk / 1e6);
     }

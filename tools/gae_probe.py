@@ -48,6 +48,7 @@ def run(P, H, reps=20):
 
 
 if __name__ == "__main__":
-    for P, H in ((125, 1000), (1000, 1000), (25, 500), (100, 1000), (200, 200)):
+    for P, H in ((125, 1000), (1000, 1000), (25, 500), (100, 1000), (200, 200), (1, 1000), (125, 250), (125, 500),
+                 (125, 1024), (125, 2000), (125, 4000), (1, 4000)):
         o = run(P, H)
         print("P %5d H %5d  gae %7.2f us  gae_scan %7.2f us" % (P, H, o["mjrl_gae"], o["mjrl_gae_scan"]), flush=True)

@@ -1,13 +1,14 @@
 #!/bin/bash
-# Round 6, first GPU pass: the serial-step microbenchmark, the new / changed
-# parity tests (f64 observations, train_step, torch-collective sharded path),
-# the whole GPU suite + smoke, the bench line, then the PMC passes at this commit.
-TAG=${1:-r06a}
+# Round 6, GPU pass b: GAE microbenchmarks, the new / changed parity tests, the
+# whole GPU suite + smoke, the bench line, the PMC passes at this commit.
+TAG=${1:-r06b}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 60 ./tools/gae_latency > $OUT/gae_latency.txt 2>&1 || { echo "GAE_LATENCY FAILED"; cat $OUT/gae_latency.txt; exit 1; }
 cat $OUT/gae_latency.txt
+timeout -k 10 120 python3 -u tools/gae_probe.py > $OUT/gae_probe.txt 2>&1 || { echo "GAE_PROBE FAILED"; tail $OUT/gae_probe.txt; exit 1; }
+cat $OUT/gae_probe.txt
 timeout -k 10 400 python3 -u -m pytest tests/test_gpu_f64obs.py tests/test_gpu_train_step.py tests/test_gpu_sharded.py -x -v -m gpu -p no:cacheprovider --timeout 200 --timeout-method thread > $OUT/new_tests.log 2>&1 || { echo "NEW TESTS FAILED"; grep -E "PASS|FAIL|Error" $OUT/new_tests.log | tail -40; exit 1; }
 grep -cE "PASSED" $OUT/new_tests.log
 bash tools/gpu_suite.sh $TAG/suite || exit 1

@@ -429,6 +429,16 @@ int mjrl_host_stage_paths_f64x(const double* const* srcs, const int64_t* rows, i
  * float(x) overflows).  The input of mjrl_linear_baseline_gram_f32x2. */
 int mjrl_host_stage_lo_paths_f64(const double* const* srcs, const int64_t* rows, int32_t count, int32_t n,
                                  float* dst);
+/* Rows bound for different places (the vectorised sampler's streaming sink: one row
+ * per environment per step, each into its trajectory's pinned slab): row i of src
+ * (rows x n f64, contiguous) converted into dst_rows[i] (n f32), folded into cmin /
+ * cmax (nullable, both or neither), with pred[i] = its LinearBaseline prediction at
+ * path index tidx[i] when coeffs is given (coeffs / pred / tidx together), and
+ * *inexact (nullable) raised as above: the same per-row arithmetic as
+ * mjrl_host_stage_paths_f64x, so a batch built row by row is bit-identical. */
+int mjrl_host_stage_rows_f64x(const double* src, int64_t rows, int32_t n, float* const* dst_rows, float* cmin,
+                              float* cmax, const double* coeffs, const int64_t* tidx, double* pred,
+                              int32_t* inexact);
 /* The extras of mjrl_host_stage_paths_f64x for one array through the portable loop
  * (tests compare it with the vector path). */
 int mjrl_host_extras_portable(const double* src, int64_t rows, int32_t n, const double* coeffs, double* pred,

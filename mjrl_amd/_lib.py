@@ -104,6 +104,7 @@ SIGNATURES = {
     "mjrl_host_stage_paths_f64x": [P, P, I32, I32, P, P, P, P, P, I32, P],
     "mjrl_host_stage_lo_paths_f64": [P, P, I32, I32, P],
     "mjrl_host_extras_portable": [P, I64, I32, P, P, P],
+    "mjrl_host_stage_rows_f64x": [P, I64, I32, P, P, P, P, P, P, P],
     "mjrl_host_stage_f64_portable": [P, I64, I32, P, P, P],
     "mjrl_host_stage_avx512": [],
     "mjrl_host_gather": [P, P, I32, P],
@@ -141,6 +142,7 @@ def load(path=None):
 STAGE_LIB_PATH = os.path.join(HERE, "lib", "libmjrl_stage.so")
 STAGE_FUNCS = ("mjrl_host_stage_f64", "mjrl_host_stage_f32", "mjrl_host_stage_paths_f64",
                "mjrl_host_stage_paths_f64x", "mjrl_host_stage_lo_paths_f64", "mjrl_host_extras_portable",
+               "mjrl_host_stage_rows_f64x",
                "mjrl_host_stage_f64_portable", "mjrl_host_stage_avx512", "mjrl_host_gather")
 _STAGE = None
 

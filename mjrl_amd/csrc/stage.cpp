@@ -91,17 +91,26 @@ inline double time_terms(int64_t r, const double* c, int32_t n) {
     return a * c[n] + (a * a) * c[n + 1] + std::pow(a, 3.0) * c[n + 2] + c[n + 3];
 }
 
+// One row s (n values, index t in its path): its prediction when c is given (else
+// 0), and whether any value is not a float32.  Every staging entry point computes
+// a row's prediction through the row function of the CPU's path (row_extras), so
+// the block pass, the per-row pass of the streaming sink and the tests agree bit
+// for bit.
+inline double row_extras_portable(const double* __restrict__ s, int64_t t, int32_t n, const double* c, bool& bad) {
+    double acc = 0.0;
+    for (int32_t k = 0; k < n; ++k) {
+        const double v = s[k];
+        bad |= !((double)(float)v == v);
+        if (c) acc += clip10(v) * c[k];
+    }
+    return c ? acc + time_terms(t, c, n) : 0.0;
+}
+
 int extras_portable(const double* __restrict__ src, int64_t rows, int32_t n, const Extras& x) {
     bool bad = false;
     for (int64_t r = 0; r < rows; ++r) {
-        const double* __restrict__ s = src + r * n;
-        double acc = 0.0;
-        for (int32_t k = 0; k < n; ++k) {
-            const double v = s[k];
-            bad |= !((double)(float)v == v);
-            if (x.coeffs) acc += clip10(v) * x.coeffs[k];
-        }
-        if (x.pred) x.pred[r] = acc + time_terms(r, x.coeffs, n);
+        const double p = row_extras_portable(src + r * n, r, n, x.coeffs, bad);
+        if (x.pred) x.pred[r] = p;
     }
     if (bad && x.inexact) *x.inexact = 1;
     return MJRL_OK;
@@ -186,21 +195,24 @@ MJRL_AVX512 inline void strip(const S* __restrict__ src, int64_t r0, int64_t r1,
 // with the value (NEQ_UQ: a NaN counts as inexact), clip as max(-10, x) then
 // min(10, .) with x the SECOND operand of each (vmaxpd / vminpd return it when
 // either is NaN: NaN stays NaN, as np.clip), fused multiply-add with the coefficients.
-MJRL_AVX512 void extras_avx512(const double* __restrict__ src, int64_t r0, int64_t r1, int32_t n, const Extras& x) {
+MJRL_AVX512 double row_extras_avx512(const double* __restrict__ s, int64_t t, int32_t n, const double* c,
+                                     __mmask8& bad) {
     const __m512d lo = _mm512_set1_pd(-10.0), hi = _mm512_set1_pd(10.0);
+    __m512d acc = _mm512_setzero_pd();
+    for (int32_t k = 0; k < n; k += 8) {
+        const __mmask8 m = n - k >= 8 ? (__mmask8)0xff : (__mmask8)((1u << (n - k)) - 1);
+        const __m512d v = _mm512_maskz_loadu_pd(m, s + k);
+        bad |= _mm512_cmp_pd_mask(_mm512_cvtps_pd(_mm512_cvtpd_ps(v)), v, _CMP_NEQ_UQ);
+        if (c) acc = _mm512_fmadd_pd(_mm512_min_pd(hi, _mm512_max_pd(lo, v)), _mm512_maskz_loadu_pd(m, c + k), acc);
+    }
+    return c ? _mm512_reduce_add_pd(acc) + time_terms(t, c, n) : 0.0;
+}
+
+MJRL_AVX512 void extras_avx512(const double* __restrict__ src, int64_t r0, int64_t r1, int32_t n, const Extras& x) {
     __mmask8 bad = 0;
     for (int64_t r = r0; r < r1; ++r) {
-        const double* s = src + r * n;
-        __m512d acc = _mm512_setzero_pd();
-        for (int32_t k = 0; k < n; k += 8) {
-            const __mmask8 m = n - k >= 8 ? (__mmask8)0xff : (__mmask8)((1u << (n - k)) - 1);
-            const __m512d v = _mm512_maskz_loadu_pd(m, s + k);
-            bad |= _mm512_cmp_pd_mask(_mm512_cvtps_pd(_mm512_cvtpd_ps(v)), v, _CMP_NEQ_UQ);
-            if (x.coeffs)
-                acc = _mm512_fmadd_pd(_mm512_min_pd(hi, _mm512_max_pd(lo, v)), _mm512_maskz_loadu_pd(m, x.coeffs + k),
-                                      acc);
-        }
-        if (x.pred) x.pred[r] = _mm512_reduce_add_pd(acc) + time_terms(r, x.coeffs, n);
+        const double p = row_extras_avx512(src + r * n, r, n, x.coeffs, bad);
+        if (x.pred) x.pred[r] = p;
     }
     if (bad && x.inexact) *x.inexact = 1;
 }
@@ -332,6 +344,41 @@ int mjrl_host_stage_lo_paths_f64(const double* const* srcs, const int64_t* rows,
         if (rc != MJRL_OK) return rc;
         dst += rows[i] * (int64_t)n;
     }
+    return MJRL_OK;
+}
+
+// Rows that are not contiguous in their destination (the streaming sink of the
+// vectorised sampler: one row per environment per step, each to its trajectory's
+// pinned slab): row i of src goes to dst_rows[i] as f32, folded into the column
+// ranges, with its prediction at path index tidx[i] (when coeffs is given) and
+// the exactness flag, through the same per-row arithmetic as the block pass.
+int mjrl_host_stage_rows_f64x(const double* src, int64_t rows, int32_t n, float* const* dst_rows, float* cmin,
+                              float* cmax, const double* coeffs, const int64_t* tidx, double* pred,
+                              int32_t* inexact) {
+    if (rows < 0 || n <= 0 || (rows > 0 && (!src || !dst_rows))) return MJRL_EINVAL;
+    if ((cmin == nullptr) != (cmax == nullptr) || (coeffs == nullptr) != (pred == nullptr)) return MJRL_EINVAL;
+    if (coeffs && !tidx) return MJRL_EINVAL;
+    const bool vec = have_avx512();
+    bool bad = false;
+    __mmask8 badv = 0;
+    for (int64_t i = 0; i < rows; ++i) {
+        const double* s = src + i * n;
+        float* d = dst_rows[i];
+        if (!d) return MJRL_EINVAL;
+        for (int32_t k = 0; k < n; ++k) {
+            const float v = (float)s[k];
+            d[k] = v;
+            if (cmin) {
+                const float lo = cmin[k], hi = cmax[k];
+                cmin[k] = v < lo ? v : lo;   // a NaN compares false: skipped (as the block pass)
+                cmax[k] = v > hi ? v : hi;
+            }
+        }
+        const int64_t t = tidx ? tidx[i] : 0;
+        const double p = vec ? row_extras_avx512(s, t, n, coeffs, badv) : row_extras_portable(s, t, n, coeffs, bad);
+        if (pred) pred[i] = p;
+    }
+    if ((bad || badv) && inexact) *inexact = 1;
     return MJRL_OK;
 }
 

@@ -1,0 +1,182 @@
+"""Sampler-fed staging ("have the samplers fill pinned fp32
+per-path slabs ... and overlap the H2D with" the rest of sampling).
+
+The reference concatenates the finished f64 paths (npg_cg.py:87-89) and the
+policy casts them to f32 on every forward (gaussian_mlp.py:103); the staging
+path of engine.DeviceBatch.from_paths does that conversion once, but only after
+sampling has finished, so the update waits for a ~3 GB f64 read and a 1.5 GB
+PCIe copy at Humanoid 1M.  StreamSink moves that work INTO the
+sampling loop of samplers/vector_sampler.py:
+
+  - every lock step, the observation rows of the live environments go through
+    ONE native call (mjrl_host_stage_rows_f64x) straight into their
+    trajectories' pinned f32 slabs (one double-buffered slab per environment
+    slot), folded into the column ranges, with the LinearBaseline prediction of
+    each row computed from its f64 values (the coefficients are fixed while a
+    batch is sampled: baseline.fit runs after the update) and the exactness
+    flag; the actions likewise (f32);
+  - when a trajectory ends, its rows are copied to HBM on the staging copy
+    stream at the trajectory's fixed position ep * H of a padded device slab,
+    while the other environments keep stepping;
+  - after sampling, batch() compacts the padded slabs into the contiguous
+    layout with one device gather (mjrl_gather_rows) and stages the 1-D slots
+    (rewards, offsets, flags, predictions: 24 bytes a row).
+
+The DeviceBatch it returns is bit-identical to DeviceBatch.from_paths on the
+same paths (the same f32 rounding, the same per-row prediction arithmetic,
+ranges that give the same column scales): tests/test_gpu_stream_staging.py.
+What remains after the last environment step is one trajectory's copy, the
+gather, the 1-D slots and the update itself (bench.py e2e_stream).
+"""
+import ctypes as C
+
+import numpy as np
+import torch
+
+from .. import _lib
+from ..engine import DeviceBatch, _STAGING, _linear_coeffs
+
+
+class StreamSink:
+    """Receives rows from the vectorised sampler and stages them as they come.
+
+    n, m: observation / action widths; horizon: the longest trajectory; N: the
+    number of trajectories; baseline: the agent's value baseline (a
+    LinearBaseline's coefficients are used for the predictions, as fixed while
+    the batch is sampled); nslots: the sampler's environment slots."""
+
+    NBUF = 2   # slabs per environment slot: a slot starts its next trajectory while the last one's copy runs
+
+    def __init__(self, n, m, horizon, N, device, baseline=None, nslots=64):
+        self.n, self.m, self.H, self.N = int(n), int(m), int(horizon), int(N)
+        self.device = torch.device(device)
+        c = _linear_coeffs(baseline, self.n)
+        self.linear = c is not False
+        self.coeffs = None if c is False or c is None else np.ascontiguousarray(c, dtype=np.float64)
+        self.L = _lib.stage_lib()
+        S, B, H = int(nslots), self.NBUF, self.H
+        # pinned per-slot slabs: [slot][buf][H][n] f32 observations, [..][m] actions, [..] f64 predictions
+        self._obs = torch.empty((S, B, H, self.n), dtype=torch.float32, pin_memory=True)
+        self._act = torch.empty((S, B, H, self.m), dtype=torch.float32, pin_memory=True)
+        self.obs_h, self.act_h = self._obs.numpy(), self._act.numpy()
+        self.pred_h = np.zeros((S, B, H), np.float64)
+        self._row_ptr0 = self.obs_h.ctypes.data
+        self._ev = [[None] * B for _ in range(S)]
+        self.buf = np.zeros(S, np.int64)
+        self.ep = np.full(S, -1, np.int64)
+        self.lo = np.full(self.n, np.inf, np.float32)
+        self.hi = np.full(self.n, -np.inf, np.float32)
+        self.flag = np.zeros(1, np.int32)
+        self.lengths = np.zeros(self.N, np.int64)
+        self.pred = [None] * self.N
+        with torch.cuda.device(self.device):
+            self.obs_pad = _STAGING.device_slot("stream_obs", self.N * H * self.n, np.float32, self.device) \
+                .view(self.N * H, self.n)
+            self.act_pad = _STAGING.device_slot("stream_act", self.N * H * self.m, np.float32, self.device) \
+                .view(self.N * H, self.m)
+            self.cs = _STAGING._copy_stream(self.device)
+            # the padded slabs may still be read by work queued on the current stream
+            self.cs.wait_stream(torch.cuda.current_stream(self.device))
+        self.done = False
+
+    # ---- sampler side -------------------------------------------------------
+    def begin(self, slot, ep):
+        """Slot `slot` starts trajectory `ep`: it writes into its other slab, once
+        that slab's previous copy has completed."""
+        b = (self.buf[slot] + 1) % self.NBUF
+        ev = self._ev[slot][b]
+        if ev is not None:
+            ev.synchronize()
+            self._ev[slot][b] = None
+        self.buf[slot] = b
+        self.ep[slot] = ep
+
+    def rows(self, slots, obs, t):
+        """Observation rows obs [E, n] (f64) of environments `slots` at path
+        indices t (the row each trajectory records at this step)."""
+        obs = np.ascontiguousarray(obs, dtype=np.float64)
+        slots = np.asarray(slots, np.int64)
+        t = np.ascontiguousarray(t, dtype=np.int64)
+        E = len(slots)
+        if E == 0:
+            return
+        b = self.buf[slots]
+        stride_b, stride_s = self.H * self.n * 4, self.NBUF * self.H * self.n * 4
+        ptrs = (C.c_void_p * E)(*(self._row_ptr0 + slots * stride_s + b * stride_b + t * self.n * 4).tolist())
+        pred = np.empty(E, np.float64) if self.coeffs is not None else None
+        _lib.check(self.L.mjrl_host_stage_rows_f64x(
+            obs.ctypes.data, E, self.n, ptrs, self.lo.ctypes.data, self.hi.ctypes.data,
+            None if pred is None else self.coeffs.ctypes.data, t.ctypes.data, None if pred is None else pred.ctypes.data,
+            self.flag.ctypes.data), "mjrl_host_stage_rows_f64x")
+        if pred is not None:
+            self.pred_h[slots, b, t] = pred
+
+    def actions(self, slots, act, t):
+        """Action rows act [E, m] of environments `slots` at path indices t."""
+        slots = np.asarray(slots, np.int64)
+        self.act_h[slots, self.buf[slots], np.asarray(t, np.int64)] = np.asarray(act, dtype=np.float64)
+
+    def finish(self, slot, length):
+        """Slot `slot`'s trajectory ended after `length` rows: its rows leave for
+        HBM now, on the copy stream, while sampling continues."""
+        ep, b, Lr = int(self.ep[slot]), int(self.buf[slot]), int(length)
+        self.lengths[ep] = Lr
+        self.pred[ep] = self.pred_h[slot, b, :Lr].copy() if self.coeffs is not None else None
+        if Lr:
+            with torch.cuda.stream(self.cs):
+                self.obs_pad[ep * self.H: ep * self.H + Lr].copy_(self._obs[slot, b, :Lr], non_blocking=True)
+                self.act_pad[ep * self.H: ep * self.H + Lr].copy_(self._act[slot, b, :Lr], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.cs)
+            self._ev[slot][b] = ev
+        self.ep[slot] = -1
+
+    # ---- update side -------------------------------------------------------
+    def batch(self, paths, reuse=True):
+        """The DeviceBatch of the sampled paths (those this sink received, in
+        trajectory order), as DeviceBatch.from_paths would stage them."""
+        with torch.cuda.device(self.device):
+            return self._batch(paths, reuse)
+
+    def _batch(self, paths, reuse):
+        N, H, dev = self.N, self.H, self.device
+        lengths = np.array([len(p["rewards"]) for p in paths], dtype=np.int64)
+        if len(paths) != N or not np.array_equal(lengths, self.lengths):
+            raise ValueError("StreamSink.batch: the paths are not the ones the sink received")
+        T = int(lengths.sum())
+        cur = torch.cuda.current_stream(dev)
+        cur.wait_stream(self.cs)   # every trajectory's copy
+        idx = np.concatenate([ep * H + np.arange(L, dtype=np.int64) for ep, L in enumerate(lengths)]) \
+            if T else np.zeros(0, np.int64)
+        idx_d = torch.from_numpy(idx).to(dev, non_blocking=False)
+        obs = _STAGING.device_slot("obs", T * self.n, np.float32, dev).view(T, self.n) if reuse else \
+            torch.empty((T, self.n), dtype=torch.float32, device=dev)
+        act = _STAGING.device_slot("act", T * self.m, np.float32, dev).view(T, self.m) if reuse else \
+            torch.empty((T, self.m), dtype=torch.float32, device=dev)
+        L = _lib.lib()
+        st = _lib.stream_ptr()
+        if T:
+            _lib.check(L.mjrl_gather_rows(_lib.ptr(self.obs_pad), 4 * self.n, _lib.ptr(idx_d), T, _lib.ptr(obs), st),
+                       "mjrl_gather_rows")
+            _lib.check(L.mjrl_gather_rows(_lib.ptr(self.act_pad), 4 * self.m, _lib.ptr(idx_d), T, _lib.ptr(act), st),
+                       "mjrl_gather_rows")
+
+        def stage(slot, arrs, ncols, dtype=np.float64):
+            return _STAGING.stage(slot, arrs, ncols, dtype, dev, reuse)
+
+        orange = stage("orange", [np.stack([self.lo, self.hi])], self.n, np.float32)
+        rew = stage("rew", [p["rewards"] for p in paths], 0)
+        off = stage("off", [np.concatenate([[0], np.cumsum(lengths)]).astype(np.int64)], 0, np.int64)
+        term = stage("term", [np.array([bool(p.get("terminated", False)) for p in paths], dtype=np.uint8)], 0,
+                     np.uint8)
+        if self.coeffs is not None:
+            base = stage("base", self.pred, 0)
+        else:
+            base = _STAGING.device_slot("base", T, np.float64, dev) if reuse else \
+                torch.empty(T, dtype=torch.float64, device=dev)
+            base.zero_()
+        b = DeviceBatch(obs, act, rew, base, off, term, obs_range=orange)
+        b.lengths = lengths
+        b.obs_inexact = bool(self.flag[0])
+        self.done = True
+        return b

@@ -414,6 +414,58 @@ def e2e_from_host(paths_range, eng, th0, base, upd, device, cfg, reps=3):
                      "median of %d (staging_ms: the staging alone, synchronised)" % (host_threads(), reps))
 
 
+def e2e_stream(paths_range, eng, th0, base, upd, device, cfg, nslots=64):
+    """train_step's post-sampling critical path with the sampler feeding the
+    staging (samplers/stream_staging.StreamSink): the
+    vectorised sampler's per-step calls are replayed on the synthetic paths
+    (nslots lock-stepped slots, each observation / action row handed over at
+    its step, each trajectory copied to HBM when it ends), then from the last
+    hand-over: the device batch (gather + 1-D slots) -> update -> readback.
+    Reported beside `value` (never as it)."""
+    from mjrl_amd.samplers.stream_staging import StreamSink
+    p0, p1 = paths_range
+    obs, act, rew = make_paths(p0, p1, cfg=cfg)
+    paths = [dict(observations=o.astype(np.float64), actions=a.astype(np.float64), rewards=r, terminated=False)
+             for o, a, r in zip(obs, act, rew)]
+    del obs, act
+    N, H = len(paths), cfg["horizon"]
+    T = N * H
+
+    def one(th):
+        sink = StreamSink(cfg["n"], cfg["m"], H, N, device, baseline=base, nslots=nslots)
+        tf = 0.0
+        for g0 in range(0, N, nslots):   # lock-stepped rounds of nslots trajectories
+            grp = list(range(g0, min(N, g0 + nslots)))
+            for j, ep in enumerate(grp):
+                sink.begin(j, ep)
+            slots = list(range(len(grp)))
+            f0 = time.perf_counter()
+            for t in range(H):
+                ts = [t] * len(grp)
+                sink.rows(slots, np.stack([paths[ep]["observations"][t] for ep in grp]), ts)
+                sink.actions(slots, np.stack([paths[ep]["actions"][t] for ep in grp]), ts)
+            for j in slots:
+                sink.finish(j, H)
+            tf += time.perf_counter() - f0
+        t0 = time.perf_counter()
+        b = sink.batch(paths)
+        eng.update(b, th, **upd)
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) * 1e3, tf * 1e3
+
+    one(th0.clone())
+    runs = [one(th0.clone()) for _ in range(2)]
+    crit = float(np.median([r[0] for r in runs]))
+    feed = float(np.median([r[1] for r in runs]))
+    return dict(post_sampling_ms=round(crit, 2), feed_ms=round(feed, 1), feed_us_per_row=round(feed * 1e3 / T, 3),
+                timesteps=T, slots=nslots,
+                note="StreamSink fed per lock step as the vectorised sampler feeds it (observation rows through "
+                     "mjrl_host_stage_rows_f64x into pinned per-slot slabs, each trajectory copied to HBM when it "
+                     "ends); post_sampling_ms = from the last trajectory's hand-over to the update's readback "
+                     "(gather of the padded slabs, 1-D slots, update); feed_ms = the sampler-side cost of the "
+                     "hand-overs (spread over sampling, timed without environments); median of 2")
+
+
 def e2e_timeline(paths, eng, th, base, upd, device):
     """One more end-to-end update with the staging traced (engine._PinnedStaging
     .trace): host conversion spans per chunk, each chunk's H2D copy timed with
@@ -721,6 +773,8 @@ def main():
             th = th0.clone()
             log("end-to-end from host paths")
             out["e2e_from_host"] = e2e_from_host((p0, p1), eng, th, base, upd, device, cfg)
+            log("end-to-end with the sampler feeding the staging")
+            out["e2e_stream"] = e2e_stream((p0, p1), eng, th0, base, upd, device, cfg)
         if world == 1 and not args.no_cpu_baseline:
             rows = T_total if (args.cpu_full or not args.cpu_rows) else min(args.cpu_rows, T_total)
             reps = args.cpu_reps or (3 if args.config == "c4" else 10)

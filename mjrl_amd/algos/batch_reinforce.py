@@ -70,6 +70,9 @@ class BatchREINFORCE:
     sampler = None
     env_factory = None
     num_envs = 64
+    # with the "vector" sampler: stage each trajectory to HBM while sampling goes on
+    # (samplers/stream_staging.py; float32 staging, no demonstration rows)
+    stream_staging = True
     # dtype the sampled observations / actions are staged to HBM in: float32 (the
     # policy's own input precision, half the PCIe bytes) or float64; None = auto
     # (staging_obs_dtype): float32, except float64 when the baseline is an
@@ -105,6 +108,7 @@ class BatchREINFORCE:
         d = dict(self.__dict__)
         d["_engine"] = None
         d["_last_batch"] = None   # device tensors
+        d.pop("_stream", None)    # pinned slabs / device slots of the streaming sink
         d.pop("_pre", None)       # views of a pool worker's shared segment
         if not isinstance(d.get("_comm"), (LocalComm, type(None))):
             d["_comm"] = None     # a process group does not pickle; re-resolved on use
@@ -219,9 +223,21 @@ class BatchREINFORCE:
                 raise ValueError("the vector sampler runs the policy on a GPU; with devices=... the controller "
                                  "process keeps off the GPUs: use the reference samplers there")
             from ..samplers.vector_sampler import sample_paths_vectorized
+            sinks = []
+            if self.stream_staging and self.staging_obs_dtype() == np.float32 and self._demo_paths() is None:
+                from ..samplers.stream_staging import StreamSink
+
+                def sink(n_paths, horizon, nslots):
+                    sinks.append(StreamSink(self.policy.n, self.policy.m, horizon, n_paths, self.engine().device,
+                                            baseline=self.baseline, nslots=nslots))
+                    return sinks[-1]
+            else:
+                sink = None
             paths = sample_paths_vectorized(N, self.policy, T, env=self.env_factory, env_name=env_name,
                                             pegasus_seed=self.seed, num_envs=self.num_envs,
-                                            device=self.engine().device)
+                                            device=self.engine().device, sink=sink)
+            if sinks:
+                self._stream = sinks[0]
         elif sample_mode == "trajectories":
             paths = trajectory_sampler.sample_paths_parallel(N, self.policy, T, env_name, self.seed, num_cpu)
         else:
@@ -337,9 +353,13 @@ class BatchREINFORCE:
         train_from_paths, fused on the device.  Writes returns / baseline /
         advantages into the path dicts like the reference does."""
         eng = self.engine()
-        batch = DeviceBatch.from_paths(paths, eng.device, baseline=self.baseline, demo_paths=self._demo_paths(),
-                                       obs_dtype=self.staging_obs_dtype(), reuse=True,
-                                       pre=self.__dict__.pop("_pre", None))
+        stream = self.__dict__.pop("_stream", None)
+        if stream is not None:   # staged while sampling (vector sampler + StreamSink)
+            batch = stream.batch(paths)
+        else:
+            batch = DeviceBatch.from_paths(paths, eng.device, baseline=self.baseline, demo_paths=self._demo_paths(),
+                                           obs_dtype=self.staging_obs_dtype(), reuse=True,
+                                           pre=self.__dict__.pop("_pre", None))
         ret, adv = eng.returns_advantages(batch, gamma, gae_lambda)
         ret, adv = ret.cpu().numpy(), adv.cpu().numpy()
         base = batch.baseline.cpu().numpy()

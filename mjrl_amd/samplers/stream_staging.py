@@ -37,6 +37,9 @@ from .. import _lib
 from ..engine import DeviceBatch, _STAGING, _linear_coeffs
 
 
+_SLABS = {}
+
+
 class StreamSink:
     """Receives rows from the vectorised sampler and stages them as they come.
 
@@ -50,18 +53,25 @@ class StreamSink:
     def __init__(self, n, m, horizon, N, device, baseline=None, nslots=64):
         self.n, self.m, self.H, self.N = int(n), int(m), int(horizon), int(N)
         self.device = torch.device(device)
+        self.baseline = baseline
         c = _linear_coeffs(baseline, self.n)
         self.linear = c is not False
         self.coeffs = None if c is False or c is None else np.ascontiguousarray(c, dtype=np.float64)
         self.L = _lib.stage_lib()
         S, B, H = int(nslots), self.NBUF, self.H
-        # pinned per-slot slabs: [slot][buf][H][n] f32 observations, [..][m] actions, [..] f64 predictions
-        self._obs = torch.empty((S, B, H, self.n), dtype=torch.float32, pin_memory=True)
-        self._act = torch.empty((S, B, H, self.m), dtype=torch.float32, pin_memory=True)
+        # pinned per-slot slabs, [slot][buf][H][n] f32 observations, [..][m] actions
+        # and [..] f64 predictions, kept across batches (a training loop builds one
+        # sink per iteration) with the copy events that guard them
+        key = (S, B, H, self.n, self.m)
+        ent = _SLABS.get(key)
+        if ent is None:
+            _SLABS.clear()   # one shape at a time
+            ent = _SLABS[key] = dict(obs=torch.empty((S, B, H, self.n), dtype=torch.float32, pin_memory=True),
+                                     act=torch.empty((S, B, H, self.m), dtype=torch.float32, pin_memory=True),
+                                     pred=np.zeros((S, B, H), np.float64), ev=[[None] * B for _ in range(S)])
+        self._obs, self._act, self.pred_h, self._ev = ent["obs"], ent["act"], ent["pred"], ent["ev"]
         self.obs_h, self.act_h = self._obs.numpy(), self._act.numpy()
-        self.pred_h = np.zeros((S, B, H), np.float64)
         self._row_ptr0 = self.obs_h.ctypes.data
-        self._ev = [[None] * B for _ in range(S)]
         self.buf = np.zeros(S, np.int64)
         self.ep = np.full(S, -1, np.int64)
         self.lo = np.full(self.n, np.inf, np.float32)
@@ -171,6 +181,10 @@ class StreamSink:
                      np.uint8)
         if self.coeffs is not None:
             base = stage("base", self.pred, 0)
+        elif not self.linear and self.baseline is not None:
+            # another baseline: its own predict per path, as DeviceBatch.from_paths
+            # (process_samples.py:23)
+            base = stage("base", [self.baseline.predict(p) for p in paths], 0)
         else:
             base = _STAGING.device_slot("base", T, np.float64, dev) if reuse else \
                 torch.empty(T, dtype=torch.float64, device=dev)

@@ -86,15 +86,20 @@ def _stack(dicts):
 
 
 class _Slot:
-    __slots__ = ("env", "ep", "rs", "o", "t", "obs", "act", "rew", "ainfo", "einfo")
+    __slots__ = ("env", "ep", "rs", "o", "t", "obs", "act", "rew", "ainfo", "einfo", "idx")
 
 
 def sample_paths_vectorized(N, policy, T=1e6, env=None, env_name=None, pegasus_seed=None, num_envs=64,
-                            device=None):
+                            device=None, sink=None):
     """N trajectories on min(num_envs, N) lock-stepped environments.
 
     env: an environment factory (called once per slot) or None with env_name
-    (mjrl.utils.get_environment, the reference's registry)."""
+    (mjrl.utils.get_environment, the reference's registry).  sink: a
+    samplers.stream_staging.StreamSink (built with nslots >= min(num_envs, N)
+    and horizon >= the trajectories' length) that receives every observation /
+    action row as it is produced and stages each trajectory to HBM when it ends
+    (sink.batch(paths) afterwards), or a factory sink(N, horizon, slots) that
+    builds one.  The paths returned are the same either way."""
     if env is None:
         if env_name is None:
             raise ValueError("sample_paths_vectorized needs env (a factory) or env_name")
@@ -111,6 +116,13 @@ def sample_paths_vectorized(N, policy, T=1e6, env=None, env_name=None, pegasus_s
         s.env = env()
         slots.append(s)
     horizon = min(T, slots[0].env.horizon)
+    if callable(sink):   # a factory: sink(N, horizon, slots)
+        sink = sink(N, int(horizon), len(slots))
+    if sink is not None and (sink.N != N or sink.H < horizon or len(sink.buf) < len(slots)):
+        raise ValueError("StreamSink sized for %d paths x %d steps on %d slots; sampling %d x %d on %d"
+                         % (sink.N, sink.H, len(sink.buf), N, horizon, len(slots)))
+    for i, s in enumerate(slots):
+        s.idx = i
     paths = [None] * N
     last_state = [None]
     next_ep = [0]
@@ -134,8 +146,12 @@ def sample_paths_vectorized(N, policy, T=1e6, env=None, env_name=None, pegasus_s
         np.random.set_state(saved)
         s.t = 0
         s.obs, s.act, s.rew, s.ainfo, s.einfo = [], [], [], [], []
+        if sink is not None:
+            sink.begin(s.idx, ep)
 
     def finish(s, done):
+        if sink is not None:
+            sink.finish(s.idx, s.t)
         paths[s.ep] = dict(observations=np.array(s.obs), actions=np.array(s.act), rewards=np.array(s.rew),
                            agent_infos=_stack(s.ainfo), env_infos=_stack(s.einfo), terminated=done)
         if s.ep == N - 1:
@@ -148,9 +164,16 @@ def sample_paths_vectorized(N, policy, T=1e6, env=None, env_name=None, pegasus_s
         live = [s for s in slots if s.ep is not None]
         if not live:
             break
-        means = bp.means(np.stack([np.asarray(s.o, dtype=np.float64).ravel() for s in live]))
-        for s, mean in zip(live, means):
-            a = mean + scale * s.rs.randn(m)
+        O = np.stack([np.asarray(s.o, dtype=np.float64).ravel() for s in live])
+        means = bp.means(O)
+        # every slot's action from its own stream (the draw order within a slot is
+        # the reference's), then the environments step
+        acts = [mean + scale * s.rs.randn(m) for s, mean in zip(live, means)]
+        if sink is not None:
+            idx, ts = [s.idx for s in live], [s.t for s in live]
+            sink.rows(idx, O, ts)
+            sink.actions(idx, np.stack(acts), ts)
+        for s, mean, a in zip(live, means, acts):
             next_o, r, done, info = s.env.step(a)
             s.obs.append(s.o)
             s.act.append(a)

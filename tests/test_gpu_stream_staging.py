@@ -1,0 +1,79 @@
+"""Sampler-fed staging (samplers/stream_staging.StreamSink):
+the vectorised sampler hands every observation / action row to the sink as it
+is produced and each trajectory is copied to HBM when it ends.  The device batch
+must be bit-identical to DeviceBatch.from_paths on the same paths (rows, 1-D
+slots, LinearBaseline predictions, column ranges, exactness flag), the paths
+unchanged, and train_step's update identical with the sink on and off."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _same_batch(a, b):
+    for k in ("obs", "act", "rewards", "baseline", "path_off", "terminated"):
+        x, y = getattr(a, k), getattr(b, k)
+        assert x.dtype == y.dtype and x.shape == y.shape, k
+        assert torch.equal(x, y), k
+    assert torch.equal(a.obs_range, b.obs_range)
+    assert a.obs_inexact == b.obs_inexact and np.array_equal(a.lengths, b.lengths)
+
+
+@pytest.mark.parametrize("fitted", [False, True])
+def test_stream_batch_equals_from_paths(fitted):
+    from mjrl_amd.baselines.linear_baseline import LinearBaseline
+    from mjrl_amd.engine import DeviceBatch
+    from mjrl_amd.policies.gaussian_mlp import MLP
+    from mjrl_amd.samplers.stream_staging import StreamSink
+    from mjrl_amd.samplers.vector_sampler import sample_paths_vectorized
+    from mjrl_amd.utils.gym_env import EnvSpec
+    from stub_env import StubEnv
+    dev = torch.device("cuda:0")
+    spec = EnvSpec(6, 2, 40, 1)
+    policy = MLP(spec, hidden_sizes=(32, 32), seed=4, init_log_std=-0.5)
+    base = LinearBaseline(spec)
+    if fitted:
+        base._coeffs = np.random.RandomState(1).randn(6 + 4)
+    sinks = []
+
+    def make(N, H, S):
+        sinks.append(StreamSink(6, 2, H, N, dev, baseline=base, nslots=S))
+        return sinks[-1]
+    plain = sample_paths_vectorized(37, policy, 1e6, env=StubEnv, pegasus_seed=7, num_envs=8)
+    paths = sample_paths_vectorized(37, policy, 1e6, env=StubEnv, pegasus_seed=7, num_envs=8, sink=make)
+    for p, q in zip(paths, plain):
+        assert np.array_equal(p["observations"], q["observations"]) and np.array_equal(p["actions"], q["actions"])
+        assert p["terminated"] == q["terminated"]
+    lengths = [len(p["rewards"]) for p in paths]
+    assert len(set(lengths)) > 1   # ragged: terminations moved the offsets
+    ref = DeviceBatch.from_paths(paths, dev, baseline=base, reuse=False)
+    got = sinks[0].batch(paths, reuse=False)
+    torch.cuda.synchronize()
+    _same_batch(got, ref)
+    assert got.obs_inexact   # the stub's observations are f64
+
+
+def test_train_step_stream_on_equals_off():
+    """Two iterations of train_step with the vector sampler, the sink on and off:
+    bit-identical parameters, baseline coefficients and statistics (the second
+    iteration stages predictions of the fitted baseline)."""
+    from mjrl_amd.algos.npg_cg import NPG
+    from mjrl_amd.baselines.linear_baseline import LinearBaseline
+    from mjrl_amd.policies.gaussian_mlp import MLP
+    from mjrl_amd.utils.gym_env import EnvSpec
+    from stub_env import StubEnv
+
+    class Env:
+        env_id = "stub-v0"
+    out = []
+    for stream in (True, False):
+        spec = EnvSpec(6, 2, 40, 1)
+        agent = NPG(Env(), MLP(spec, hidden_sizes=(64, 64), seed=3, init_log_std=-1.0), LinearBaseline(spec),
+                    normalized_step_size=0.05, seed=200, save_logs=True)
+        agent.sampler, agent.env_factory, agent.num_envs, agent.stream_staging = "vector", StubEnv, 16, stream
+        stats = [agent.train_step(N=60, gamma=0.99, gae_lambda=0.95) for _ in range(2)]
+        out.append((stats, agent.policy.get_param_values(), agent.baseline._coeffs.copy()))
+    (s1, th1, c1), (s0, th0, c0) = out
+    assert s1 == s0
+    assert np.array_equal(th1, th0) and np.array_equal(c1, c0)

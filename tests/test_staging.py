@@ -275,3 +275,45 @@ def test_host_stage_extras_portable_and_specials(lib):
         host_stage(exact, np.empty((eoffs[-1], n), np.float32), eoffs, 0, 2,
                    extras=dict(coeffs=None, pred=None, npred=2, flag=flag))
         assert flag[0] == 0
+
+
+def test_rows_entry_equals_block_pass(lib):
+    """mjrl_host_stage_rows_f64x (one row per environment per step, scattered into
+    the trajectories' slabs: the streaming sink's call) writes the same floats,
+    predictions (bit for bit: the same per-row arithmetic), ranges and flag as
+    the block pass over the finished paths."""
+    import ctypes as C
+    from mjrl_amd import _lib
+    from mjrl_amd.engine import host_stage
+    L = _lib.stage_lib()
+    rs = np.random.RandomState(12)
+    for n in (6, 17, 376):
+        lengths = [5, 40, 1, 33]
+        arrs = [rs.standard_normal((H, n)) * 7 for H in lengths]
+        arrs[1][3, 2] = np.nan
+        coeffs = rs.standard_normal(n + 4)
+        offs = np.concatenate([[0], np.cumsum(lengths)])
+        T = int(offs[-1])
+        view = np.empty((T, n), np.float32)
+        lo, hi = np.full(n, np.inf, np.float32), np.full(n, -np.inf, np.float32)
+        pred, flag = np.zeros(T), np.zeros(1, np.int32)
+        host_stage(arrs, view, offs, 0, len(arrs), lo, hi, extras=dict(coeffs=coeffs, pred=pred, npred=len(arrs),
+                                                                       flag=flag))
+        # the same rows handed over step by step, the live paths of each step at once
+        dst = np.full((T, n), -1.0, np.float32)
+        lo2, hi2 = np.full(n, np.inf, np.float32), np.full(n, -np.inf, np.float32)
+        pred2, flag2 = np.zeros(T), np.zeros(1, np.int32)
+        for t in range(max(lengths)):
+            live = [i for i, H in enumerate(lengths) if t < H]
+            src = np.ascontiguousarray(np.stack([arrs[i][t] for i in live]))
+            ptrs = (C.c_void_p * len(live))(*[dst[offs[i] + t:].ctypes.data for i in live])
+            tidx = np.full(len(live), t, np.int64)
+            pr = np.zeros(len(live))
+            assert L.mjrl_host_stage_rows_f64x(src.ctypes.data, len(live), n, ptrs, lo2.ctypes.data, hi2.ctypes.data,
+                                               coeffs.ctypes.data, tidx.ctypes.data, pr.ctypes.data,
+                                               flag2.ctypes.data) == 0
+            for j, i in enumerate(live):
+                pred2[offs[i] + t] = pr[j]
+        assert np.array_equal(dst, view, equal_nan=True)
+        assert np.array_equal(pred2, pred, equal_nan=True)
+        assert np.array_equal(lo2, lo) and np.array_equal(hi2, hi) and flag2[0] == flag[0] == 1

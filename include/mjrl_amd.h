@@ -141,6 +141,12 @@ int mjrl_gae(const double* rew, const double* base, const int64_t* path_off,
              const uint8_t* terminated, int64_t P, double gamma, double gae_lambda,
              int32_t use_gae, double* ret, double* adv, double* path_ret, void* stream);
 
+/* The same outputs (bit for bit) by the one-wave-per-path kernel of rounds 1-5
+ * (mjrl_gae now runs 32 paths per workgroup, lanes = paths); kept for A/B. */
+int mjrl_gae_wave(const double* rew, const double* base, const int64_t* path_off,
+                  const uint8_t* terminated, int64_t P, double gamma, double gae_lambda,
+                  int32_t use_gae, double* ret, double* adv, double* path_ret, void* stream);
+
 /* The same outputs by a wave-parallel scan (one wave per path, 64 lane chunks per
  * window of 1024 steps composed with wave shuffles): not bit-identical to
  * discount_sum — the products are regrouped — but within ~1e-14 of each path's

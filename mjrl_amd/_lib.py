@@ -59,6 +59,7 @@ SIGNATURES = {
     "mjrl_pack_batch_split_f32": [P, P, I64, SP, P, P, P, P, P, P, P],
     "mjrl_split_supported": [SP],
     "mjrl_gae": [P, P, P, P, I64, F64, F64, I32, P, P, P, P],
+    "mjrl_gae_wave": [P, P, P, P, I64, F64, F64, I32, P, P, P, P],
     "mjrl_gae_scan": [P, P, P, P, I64, F64, F64, I32, P, P, P, P],
     "mjrl_linear_baseline": [P, I64, I32, P, I64, P, P, P],
     "mjrl_linear_baseline_f32": [P, I64, I32, P, I64, P, P, P],

@@ -534,6 +534,146 @@ __global__ void __launch_bounds__(64 * GAE_WAVES) k_gae(const double* __restrict
     }
 }
 
+// Lanes = paths (round 6): the serial recurrences of LP_PATHS paths run side by side
+// in ONE instruction stream each, one wave per chain — wave 0 the returns
+// (discount_sum(rewards, gamma)), wave 1 the advantages (discount_sum(td, gamma
+// lambda), or nothing without GAE), wave 2 the path-return sum (front to back) —
+// each lane one path; wave 3 only loads and stores.  A dependent fp64 multiply -> add costs ~10 cycles of issue
+// per step for the whole wave (tools/gae_latency.hip), so 32 paths advance for the
+// price k_gae paid for one.  The paths' steps come through LDS in windows of LP_W
+// steps per path (backward windows aligned at each path's end, forward windows at
+// its start): all four waves load window j + 1 into registers (each instruction 8
+// paths' runs of 8 consecutive steps) while the chains consume window j, then store it (td formed on
+// the way) after a barrier; the chains write their outputs in place, and the
+// window leaves for HBM with coalesced writes.  Bit-identical to k_gae: the same
+// __dmul_rn / __dadd_rn / __dsub_rn per step in the same order.
+constexpr int LP_PATHS = 32;              // paths per workgroup (lanes 0..31 of each chain wave)
+constexpr int LP_W = 128;                 // steps per window
+constexpr int LP_LD = LP_W + 1;           // LDS row stride (doubles): chain lanes conflict-free
+constexpr int LP_T = 256;                 // 4 waves: three chain waves, all four load / store
+constexpr int LP_PER = LP_PATHS * LP_W / LP_T;   // window elements per thread per array
+static_assert(LP_PATHS * LP_W % LP_T == 0 && LP_W % 64 == 0, "window split");
+
+__global__ void __launch_bounds__(LP_T) k_gae_lp(const double* __restrict__ rew, const double* __restrict__ base,
+                                                 const int64_t* __restrict__ off, const uint8_t* __restrict__ term,
+                                                 int64_t P, double gamma, double gl, int use_gae,
+                                                 double* __restrict__ ret, double* __restrict__ adv,
+                                                 double* __restrict__ path_ret) {
+    __shared__ double RB[LP_PATHS * LP_LD];   // backward rewards -> returns (in place)
+    __shared__ double TD[LP_PATHS * LP_LD];   // td -> advantages (in place); no GAE: the baseline
+    __shared__ double RF[LP_PATHS * LP_LD];   // forward rewards
+    __shared__ int64_t sb[LP_PATHS], se[LP_PATHS];
+    __shared__ double sbl[LP_PATHS];          // b1's last entry: 0 if terminated else b[-1]
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int64_t p0 = (int64_t)blockIdx.x * LP_PATHS;
+    const int np = (int)(P - p0 < LP_PATHS ? P - p0 : LP_PATHS);
+    if (tid < LP_PATHS) {
+        const bool ok = tid < np;
+        const int64_t b = ok ? off[p0 + tid] : 0, e = ok ? off[p0 + tid + 1] : 0;
+        sb[tid] = b;
+        se[tid] = e;
+        sbl[tid] = e > b ? (term[p0 + tid] ? 0.0 : base[e - 1]) : 0.0;
+    }
+    __syncthreads();
+    int64_t hmax = 0;
+    for (int i = 0; i < np; ++i) hmax = se[i] - sb[i] > hmax ? se[i] - sb[i] : hmax;
+    const int nwin = (int)((hmax + LP_W - 1) / LP_W);
+    // this thread's path (8 threads a path) and its steps u = (tid & 7) + 8 k of every
+    // window: each load instruction reads 8 paths' runs of 8 consecutive steps
+    const int mp = tid >> 3, mu = tid & 7;
+    // an empty path (or a lane past the last path) reads index 0: valid whenever a
+    // window exists, and never used (the chains and the drain skip its steps)
+    const int64_t pb = se[mp] > sb[mp] ? sb[mp] : 0, pe = se[mp] > sb[mp] ? se[mp] : 1;
+    const double pbl = sbl[mp];
+    double xr[LP_PER], xb[LP_PER], xn[LP_PER], xf[LP_PER];
+    auto load = [&](int j) {
+        // backward window: step t = e - (j + 1) W + u; forward window: t = b + j W + u;
+        // loads from clamped indices, unconditional (no exec-masked loads in the stream)
+#pragma unroll
+        for (int k = 0; k < LP_PER; ++k) {
+            const int u = mu + 8 * k;
+            int64_t tb = pe - (int64_t)(j + 1) * LP_W + u, tf = pb + (int64_t)j * LP_W + u;
+            tb = tb < pb ? pb : tb;
+            tf = tf < pe ? tf : pe - 1;
+            const int64_t tn = tb + 1 < pe ? tb + 1 : pe - 1;
+            xr[k] = rew[tb];
+            xb[k] = base[tb];
+            xn[k] = base[tn];
+            xf[k] = rew[tf];
+        }
+    };
+    auto put = [&](int j) {
+#pragma unroll
+        for (int k = 0; k < LP_PER; ++k) {
+            const int u = mu + 8 * k;
+            const int64_t tb = pe - (int64_t)(j + 1) * LP_W + u;
+            const double bn = tb + 1 < pe ? xn[k] : pbl;   // b1[t + 1] (process_samples.py:24-27)
+            RB[mp * LP_LD + u] = xr[k];
+            // GAE td = r + gamma * b1[t+1] - b1[t] (process_samples.py:28); plain: b
+            TD[mp * LP_LD + u] = use_gae ? __dsub_rn(__dadd_rn(xr[k], __dmul_rn(gamma, bn)), xb[k]) : xb[k];
+            RF[mp * LP_LD + u] = xf[k];
+        }
+    };
+    const int64_t db = sb[mp], de = se[mp];
+    auto drain = [&](int j) {   // window j's outputs (in RB / TD) to HBM
+#pragma unroll
+        for (int k = 0; k < LP_PER; ++k) {
+            const int u = mu + 8 * k;
+            const int64_t tb = de - (int64_t)(j + 1) * LP_W + u;
+            if (tb >= db) {
+                const double rr = RB[mp * LP_LD + u];
+                ret[tb] = rr;
+                adv[tb] = use_gae ? TD[mp * LP_LD + u] : __dsub_rn(rr, TD[mp * LP_LD + u]);   // plain: ret - b
+            }
+        }
+    };
+    // the chains: wave 0 returns, wave 1 advantages, wave 2 the path-return sum
+    const bool chain = lane < np && (w != 1 || use_gae);
+    const int64_t H = lane < LP_PATHS ? se[lane < np ? lane : 0] - sb[lane < np ? lane : 0] : 0;
+    const double c = w == 0 ? gamma : gl;
+    double* cw = w == 0 ? RB : (w == 1 ? TD : RF);
+    double acc = 0.0;
+    if (nwin > 0) {
+        load(0);
+        put(0);
+    }
+    __syncthreads();
+    for (int j = 0; j < nwin; ++j) {
+        if (j + 1 < nwin) load(j + 1);   // in flight under the chains
+        if (chain) {
+            double* row = cw + lane * LP_LD;
+            const int64_t s0 = (int64_t)j * LP_W;
+            if (w == 2) {
+                // front to back: Python's sum(p["rewards"]) (npg_cg.py:97); x + 1.0 * acc is
+                // x + acc exactly (k_gae's form)
+#pragma unroll 16
+                for (int u = 0; u < LP_W; ++u)
+                    if (s0 + u < H) acc = __dadd_rn(row[u], acc);
+            } else if (s0 + LP_W <= H) {
+                // a whole window of this path: the backward recurrence with no step mask
+#pragma unroll 16
+                for (int u = LP_W - 1; u >= 0; --u) {
+                    acc = __dadd_rn(row[u], __dmul_rn(c, acc));
+                    row[u] = acc;
+                }
+            } else {
+                // the path's first steps (a partial window): element u holds step
+                // t = e - (j + 1) W + u, valid for u >= (j + 1) W - H
+                const int u0 = (int)((int64_t)(j + 1) * LP_W - H);
+                for (int u = LP_W - 1; u >= (u0 > 0 ? u0 : 0); --u) {
+                    acc = __dadd_rn(row[u], __dmul_rn(c, acc));
+                    row[u] = acc;
+                }
+            }
+        }
+        __syncthreads();
+        drain(j);
+        if (j + 1 < nwin) put(j + 1);
+        __syncthreads();
+    }
+    if (w == 2 && lane < np) path_ret[p0 + lane] = acc;
+}
+
 // Moments pass 1: per-block partials of sum(x-c), sum((x-c)^2), min, max.
 template <typename T>
 __global__ void __launch_bounds__(MOM_THREADS) k_moments_part(const T* __restrict__ x, int64_t N,
@@ -1167,6 +1307,20 @@ int mjrl_gae(const double* rew, const double* base, const int64_t* path_off, con
         return MJRL_EINVAL;
     if (P == 0) return MJRL_OK;
     const double gl = gamma * gae_lambda;   // python: gamma*gae_lambda (process_samples.py:29)
+    const int64_t g = (P + LP_PATHS - 1) / LP_PATHS;
+    hipLaunchKernelGGL(k_gae_lp, dim3((unsigned)g), dim3(LP_T), 0, (hipStream_t)stream, rew, base, path_off,
+                       terminated, P, gamma, gl, use_gae, ret, adv, path_ret);
+    return err(hipGetLastError());
+}
+
+// The one-wave-per-path kernel (rounds 1-5), kept for A/B (tools/gae_probe.py).
+int mjrl_gae_wave(const double* rew, const double* base, const int64_t* path_off, const uint8_t* terminated,
+                  int64_t P, double gamma, double gae_lambda, int32_t use_gae, double* ret, double* adv,
+                  double* path_ret, void* stream) {
+    if (P < 0 || (P > 0 && (!rew || !base || !path_off || !terminated || !ret || !adv || !path_ret)))
+        return MJRL_EINVAL;
+    if (P == 0) return MJRL_OK;
+    const double gl = gamma * gae_lambda;
     const int64_t g = (P + GAE_WAVES - 1) / GAE_WAVES;
     hipLaunchKernelGGL(k_gae, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(64 * GAE_WAVES), 0, (hipStream_t)stream, rew,
                        base, path_off, terminated, P, gamma, gl, use_gae, ret, adv, path_ret);

@@ -302,6 +302,45 @@ def test_linear_baseline_predict_on_device():
 
 
 @pytest.mark.parametrize("use_gae", [1, 0])
+@pytest.mark.parametrize("fn", ["mjrl_gae", "mjrl_gae_wave"])
+def test_gae_kernel_ragged_many_paths(use_gae, fn):
+    """Both GAE kernels (lanes = paths, 32 paths per workgroup and 128-step
+    windows: mjrl_gae; one wave per path: mjrl_gae_wave) on 83 ragged paths
+    (empty, 1, window +-1, several windows, terminated or not; P not a multiple
+    of 32): bit-identical to the oracle's discount_sum chains."""
+    from mjrl_amd import _lib
+    from oracle import npg_cpu as O
+    L = _lib.lib()
+    rs = np.random.RandomState(23)
+    lengths = np.concatenate([[0, 1, 2, 127, 128, 129, 255, 256, 257, 1000, 0, 3001, 640],
+                              rs.randint(1, 700, size=70)])
+    T = int(lengths.sum())
+    rew = rs.randn(T) * 3.0
+    base = rs.randn(T)
+    term = (rs.rand(len(lengths)) < 0.5).astype(np.uint8)
+    off = np.concatenate([[0], np.cumsum(lengths)]).astype(np.int64)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    ret = torch.full((T,), np.nan, dtype=torch.float64, device="cuda")
+    adv = torch.full((T,), np.nan, dtype=torch.float64, device="cuda")
+    pret = torch.full((len(lengths),), np.nan, dtype=torch.float64, device="cuda")
+    gamma, lam = 0.99, 0.95
+    args = [t(rew), t(base), t(off), t(term)]
+    rc = getattr(L, fn)(*[_lib.ptr(a) for a in args], len(lengths), gamma, lam, use_gae, _lib.ptr(ret), _lib.ptr(adv),
+                        _lib.ptr(pret), _lib.stream_ptr())
+    assert rc == 0
+    torch.cuda.synchronize()
+    keep = lengths > 0
+    m = np.repeat(keep, lengths)
+    r_ref, a_ref = O.returns_and_advantages(rew[m], base[m], lengths[keep], term[keep].astype(bool), gamma,
+                                            lam if use_gae else None)
+    assert np.array_equal(ret.cpu().numpy(), r_ref)
+    assert np.array_equal(adv.cpu().numpy(), a_ref)
+    pr = pret.cpu().numpy()
+    assert np.array_equal(pr[keep], np.array([sum(r) for r in O.split(rew[m], lengths[keep])]))
+    assert np.all(pr[~keep] == 0.0)
+
+
+@pytest.mark.parametrize("use_gae", [1, 0])
 def test_gae_kernel_multiwindow_bitexact(use_gae):
     """mjrl_gae through the C-ABI on paths shorter than, equal to and longer
     than the kernel's 1024-step LDS window (and an empty path): returns,

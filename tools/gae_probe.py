@@ -25,7 +25,7 @@ def run(P, H, reps=20):
     pr = torch.empty(P, dtype=torch.float64, device=dev)
     st = _lib.stream_ptr()
     out = {}
-    for name in ("mjrl_gae", "mjrl_gae_scan"):
+    for name in ("mjrl_gae", "mjrl_gae_wave", "mjrl_gae_scan"):
         fn = getattr(L, name)
         args = (_lib.ptr(rew), _lib.ptr(base), _lib.ptr(off), _lib.ptr(term), P, 0.995, 0.97, 1, _lib.ptr(ret),
                 _lib.ptr(adv), _lib.ptr(pr), st)
@@ -38,7 +38,7 @@ def run(P, H, reps=20):
         e1.record()
         torch.cuda.synchronize()
         out[name] = e0.elapsed_time(e1) / reps * 1e3
-        if name == "mjrl_gae":
+        if name in ("mjrl_gae", "mjrl_gae_wave"):
             from oracle import npg_cpu as O
             r, b = rew.cpu().numpy(), base.cpu().numpy()
             lengths = np.full(P, H)
@@ -51,4 +51,5 @@ if __name__ == "__main__":
     for P, H in ((125, 1000), (1000, 1000), (25, 500), (100, 1000), (200, 200), (1, 1000), (125, 250), (125, 500),
                  (125, 1024), (125, 2000), (125, 4000), (1, 4000)):
         o = run(P, H)
-        print("P %5d H %5d  gae %7.2f us  gae_scan %7.2f us" % (P, H, o["mjrl_gae"], o["mjrl_gae_scan"]), flush=True)
+        print("P %5d H %5d  gae (lanes = paths) %7.2f us  gae_wave (round 5) %7.2f us  gae_scan %7.2f us"
+              % (P, H, o["mjrl_gae"], o["mjrl_gae_wave"], o["mjrl_gae_scan"]), flush=True)

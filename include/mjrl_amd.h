@@ -86,6 +86,15 @@ typedef struct mjrl_scratch {
  * Returns MJRL_ESHAPE if the kernels were not built for it. */
 int mjrl_shape_init(mjrl_shape* s, int32_t n, int32_t m, int32_t h0, int32_t h1);
 
+/* Build variant of the loaded library (bits): MJRL_BUILD_ABLATION = a timing-
+ * ablation build (tools/fvp_time.py; its results are wrong by construction: the
+ * engine refuses it unless MJRL_AMD_ALLOW_ABLATION=1), MJRL_BUILD_PROF = the
+ * phase-profiling build, MJRL_BUILD_CHECKS = the slab-guard debug build. */
+#define MJRL_BUILD_ABLATION 1
+#define MJRL_BUILD_PROF 2
+#define MJRL_BUILD_CHECKS 4
+int mjrl_build_flags(void);
+
 /* Scratch sizes (in elements) for T rows: *wpart_floats, *rpart_doubles; also
  * returns the T-slice count the kernels will use. */
 int mjrl_scratch_size(const mjrl_shape* s, int64_t T, int64_t* wpart_floats,

@@ -99,6 +99,7 @@ SIGNATURES = {
     "mjrl_linear_baseline_residual_f32x2": [P, P, P, I64, I32, P, I64, P, P, P, P],
     "mjrl_npg_step": [SP, P, P, P, I32, F32, F32, I32, F32, P, P, P, P],
     "mjrl_policy_mean": [SP, P, I64, P, P, P, P, P, P, P],
+    "mjrl_build_flags": [],
     "mjrl_host_stage_f64": [P, I64, I32, P, P, P],
     "mjrl_host_stage_f32": [P, I64, I32, P, P, P],
     "mjrl_host_stage_paths_f64": [P, P, I32, I32, P, P, P],
@@ -111,6 +112,7 @@ SIGNATURES = {
     "mjrl_host_gather": [P, P, I32, P],
 }
 
+BUILD_ABLATION, BUILD_PROF, BUILD_CHECKS = 1, 2, 4   # mjrl_build_flags()
 _LIB = None
 
 
@@ -136,6 +138,9 @@ def load(path=None):
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = C.c_int
+    if lib.mjrl_build_flags() & BUILD_ABLATION and os.environ.get("MJRL_AMD_ALLOW_ABLATION") != "1":
+        raise MjrlError("%s is a timing-ablation build (MJRL_KX_ABL_*: its results are wrong by construction); "
+                        "set MJRL_AMD_ALLOW_ABLATION=1 to load it for timing" % path)
     _LIB = lib
     return lib
 

@@ -1596,6 +1596,25 @@ int mjrl_debug_kx_prof(unsigned long long* out) {
 }
 #endif
 
+// What this library was built with (bits): a timing-ablation build (any
+// MJRL_KX_ABL_*: results wrong by construction), the phase-profiling build, the
+// device-checks (slab guard) build.  UpdateEngine refuses an ablation build unless
+// asked for one (tools/fvp_time.py).
+int mjrl_build_flags(void) {
+    int f = 0;
+#if defined(MJRL_KX_ABL_NOP1) || defined(MJRL_KX_ABL_NOP6) || defined(MJRL_KX_ABL_NOCHAIN) || \
+    defined(MJRL_KX_ABL_NOCOLS)
+    f |= MJRL_BUILD_ABLATION;
+#endif
+#ifdef MJRL_KX_PROF
+    f |= MJRL_BUILD_PROF;
+#endif
+#ifdef MJRL_DEVICE_CHECKS
+    f |= MJRL_BUILD_CHECKS;
+#endif
+    return f;
+}
+
 int mjrl_shape_init(mjrl_shape* s, int32_t n, int32_t m, int32_t h0, int32_t h1) {
     if (!s || n <= 0 || m <= 0 || h0 < 0 || h1 < 0) return MJRL_EINVAL;
     s->n = n;

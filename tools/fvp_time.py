@@ -2,6 +2,8 @@
 accumulate), FVP accumulate and EVAL at T rows of the Humanoid shape, HIP events
 on the launch stream, median of 20.  MJRL_AMD_LIB selects the library build.
     python tools/fvp_time.py [T] [precision]"""
+import os
+os.environ.setdefault("MJRL_AMD_ALLOW_ABLATION", "1")   # this tool times ablation builds
 import ctypes as C
 import os
 import sys

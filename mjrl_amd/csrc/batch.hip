@@ -550,6 +550,7 @@ __global__ void __launch_bounds__(64 * GAE_WAVES) k_gae(const double* __restrict
 constexpr int LP_PATHS = 32;              // paths per workgroup (lanes 0..31 of each chain wave)
 constexpr int LP_W = 128;                 // steps per window
 constexpr int LP_LD = LP_W + 1;           // LDS row stride (doubles): chain lanes conflict-free
+constexpr int LP_GB = 16;                 // chain steps per register batch
 constexpr int LP_T = 256;                 // 4 waves: three chain waves, all four load / store
 constexpr int LP_PER = LP_PATHS * LP_W / LP_T;   // window elements per thread per array
 static_assert(LP_PATHS * LP_W % LP_T == 0 && LP_W % 64 == 0, "window split");
@@ -628,7 +629,7 @@ __global__ void __launch_bounds__(LP_T) k_gae_lp(const double* __restrict__ rew,
         }
     };
     // the chains: wave 0 returns, wave 1 advantages, wave 2 the path-return sum
-    const bool chain = lane < np && (w != 1 || use_gae);
+    const bool chain = w < 3 && lane < np && (w != 1 || use_gae);
     const int64_t H = lane < LP_PATHS ? se[lane < np ? lane : 0] - sb[lane < np ? lane : 0] : 0;
     const double c = w == 0 ? gamma : gl;
     double* cw = w == 0 ? RB : (w == 1 ? TD : RF);
@@ -641,26 +642,57 @@ __global__ void __launch_bounds__(LP_T) k_gae_lp(const double* __restrict__ rew,
     for (int j = 0; j < nwin; ++j) {
         if (j + 1 < nwin) load(j + 1);   // in flight under the chains
         if (chain) {
+            // the window's steps come into registers in batches of LP_GB (the next
+            // batch's LDS reads issued before this batch's serial steps), so only the
+            // dependent fp64 multiply -> add is on the critical path
             double* row = cw + lane * LP_LD;
             const int64_t s0 = (int64_t)j * LP_W;
-            if (w == 2) {
+            const int64_t left = H - s0;   // this path's steps from this window on
+            if (w == 2 && left >= LP_W) {
                 // front to back: Python's sum(p["rewards"]) (npg_cg.py:97); x + 1.0 * acc is
                 // x + acc exactly (k_gae's form)
-#pragma unroll 16
-                for (int u = 0; u < LP_W; ++u)
-                    if (s0 + u < H) acc = __dadd_rn(row[u], acc);
-            } else if (s0 + LP_W <= H) {
-                // a whole window of this path: the backward recurrence with no step mask
-#pragma unroll 16
-                for (int u = LP_W - 1; u >= 0; --u) {
-                    acc = __dadd_rn(row[u], __dmul_rn(c, acc));
-                    row[u] = acc;
+                double x[LP_GB], xn2[LP_GB];
+#pragma unroll
+                for (int g = 0; g < LP_GB; ++g) x[g] = row[g];
+#pragma unroll
+                for (int u0 = 0; u0 < LP_W; u0 += LP_GB) {
+                    if (u0 + LP_GB < LP_W) {
+#pragma unroll
+                        for (int g = 0; g < LP_GB; ++g) xn2[g] = row[u0 + LP_GB + g];
+                    }
+#pragma unroll
+                    for (int g = 0; g < LP_GB; ++g) acc = __dadd_rn(x[g], acc);
+#pragma unroll
+                    for (int g = 0; g < LP_GB; ++g) x[g] = xn2[g];
                 }
-            } else {
+            } else if (w == 2) {
+                for (int u = 0; u < (int)(left > 0 ? left : 0); ++u) acc = __dadd_rn(row[u], acc);
+            } else if (left >= LP_W) {
+                // a whole window of this path: the backward recurrence with no step mask,
+                // outputs written back in place a batch at a time
+                double x[LP_GB], xn2[LP_GB];
+#pragma unroll
+                for (int g = 0; g < LP_GB; ++g) x[g] = row[LP_W - LP_GB + g];
+#pragma unroll
+                for (int u0 = LP_W - LP_GB; u0 >= 0; u0 -= LP_GB) {
+                    if (u0 >= LP_GB) {
+#pragma unroll
+                        for (int g = 0; g < LP_GB; ++g) xn2[g] = row[u0 - LP_GB + g];
+                    }
+#pragma unroll
+                    for (int g = LP_GB - 1; g >= 0; --g) {
+                        acc = __dadd_rn(x[g], __dmul_rn(c, acc));
+                        x[g] = acc;
+                    }
+#pragma unroll
+                    for (int g = 0; g < LP_GB; ++g) row[u0 + g] = x[g];
+#pragma unroll
+                    for (int g = 0; g < LP_GB; ++g) x[g] = xn2[g];
+                }
+            } else if (left > 0) {
                 // the path's first steps (a partial window): element u holds step
-                // t = e - (j + 1) W + u, valid for u >= (j + 1) W - H
-                const int u0 = (int)((int64_t)(j + 1) * LP_W - H);
-                for (int u = LP_W - 1; u >= (u0 > 0 ? u0 : 0); --u) {
+                // t = e - (j + 1) W + u, valid for u >= W - left
+                for (int u = LP_W - 1; u >= LP_W - (int)left; --u) {
                     acc = __dadd_rn(row[u], __dmul_rn(c, acc));
                     row[u] = acc;
                 }

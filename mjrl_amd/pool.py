@@ -407,7 +407,9 @@ class DevicePool:
             t1 = time.perf_counter()
             layouts = []
             rng = np.random.get_state()
+            shard_ms = []
             for r in range(self.world):
+                tf0 = time.perf_counter()
                 # every shard's conversion spread over the controller's thread pool
                 # (16 threads per GPU, within the process's CPU share), and the shard
                 # handed to its worker as soon as it is filled: worker r stages
@@ -417,6 +419,7 @@ class DevicePool:
                 _fill_shard(self._segment(r, L.nbytes).buf, L, paths[p0:p1], lengths[p0:p1], self._fill_pool(),
                             threads=self._fill_threads, coeffs=coeffs)
                 layouts.append(L)
+                shard_ms.append((time.perf_counter() - tf0) * 1e3)
                 self._conns[r].send(("step", dict(state=state, shm=self._shm[r].name, T=L.T, P=L.P, n=n, m=m,
                                                   dtype=L.dtype.str, mode=mode, gamma=gamma, gae_lambda=gae_lambda,
                                                   fit=fit, return_errors=return_errors, rng=rng,
@@ -427,7 +430,13 @@ class DevicePool:
         except BaseException:
             self._abort()
             raise
-        self.last_timing = dict(state_ms=(t1 - t0) * 1e3, fill_ms=(t2 - t1) * 1e3, workers_ms=(t3 - t2) * 1e3,
+        # shard r is handed to worker r as soon as it is filled, so the workers of the
+        # first shards compute while later shards fill: fill_ms is the controller's
+        # own conversion time (the sum of the per-shard fills), fill_span_ms the span
+        # from the first fill to the last hand-over (worker time overlaps it), and
+        # workers_ms the wait after the last hand-over only
+        self.last_timing = dict(state_ms=(t1 - t0) * 1e3, fill_ms=float(sum(shard_ms)), fill_shard_ms=shard_ms,
+                                fill_span_ms=(t2 - t1) * 1e3, workers_ms=(t3 - t2) * 1e3,
                                 worker_train_ms=[msg[1].get("train_ms") for msg in replies])
         if mode == "samples":
             for r in range(self.world):

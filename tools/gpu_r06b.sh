@@ -9,7 +9,7 @@ timeout -k 10 60 ./tools/gae_latency > $OUT/gae_latency.txt 2>&1 || { echo "GAE_
 cat $OUT/gae_latency.txt
 timeout -k 10 120 python3 -u tools/gae_probe.py > $OUT/gae_probe.txt 2>&1 || { echo "GAE_PROBE FAILED"; tail $OUT/gae_probe.txt; exit 1; }
 cat $OUT/gae_probe.txt
-timeout -k 10 400 python3 -u -m pytest tests/test_gpu_f64obs.py tests/test_gpu_stream_staging.py tests/test_gpu_train_step.py tests/test_gpu_sharded.py -x -v -m gpu -p no:cacheprovider --timeout 200 --timeout-method thread > $OUT/new_tests.log 2>&1 || { echo "NEW TESTS FAILED"; grep -E "PASS|FAIL|Error" $OUT/new_tests.log | tail -40; exit 1; }
+timeout -k 10 400 python3 -u -m pytest "tests/test_gpu_api.py::test_gae_kernel_ragged_many_paths" "tests/test_gpu_api.py::test_gae_kernel_multiwindow_bitexact" tests/test_gpu_f64obs.py tests/test_gpu_stream_staging.py tests/test_gpu_train_step.py tests/test_gpu_sharded.py -x -v -m gpu -p no:cacheprovider --timeout 200 --timeout-method thread > $OUT/new_tests.log 2>&1 || { echo "NEW TESTS FAILED"; grep -E "PASS|FAIL|Error" $OUT/new_tests.log | tail -40; exit 1; }
 grep -cE "PASSED" $OUT/new_tests.log
 bash tools/gpu_suite.sh $TAG/suite || exit 1
 timeout -k 10 400 python -u bench.py --no-cpu-baseline > $OUT/bench.json 2> $OUT/bench.err || { echo "BENCH FAILED"; tail -30 $OUT/bench.err; exit 1; }

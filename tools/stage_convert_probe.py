@@ -85,9 +85,8 @@ for _ in range(4):
 t = sorted(ts)[1]
 print("read-only pass (numpy sum, threads): %.1f ms (%.1f GB/s)" % (t * 1e3, R * n * 8 / t / 1e9), flush=True)
 res = {}
-SL.mjrl_host_stage_f64_nopf.argtypes = SL.mjrl_host_stage_f64.argtypes
 for name, fn in (("portable", SL.mjrl_host_stage_f64_portable), ("avx512", SL.mjrl_host_stage_f64),
-                 ("avx512-nopf", SL.mjrl_host_stage_f64_nopf)):
+                 ):
     for ranges in (True, False):
         ts = []
         for _ in range(4):

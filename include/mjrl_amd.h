@@ -340,6 +340,11 @@ int mjrl_fused_path(const mjrl_shape* s);
 #define MJRL_CG_STATE 4096
 int mjrl_cg_init(const mjrl_shape* s, const float* b, float* x, float* r, float* p,
                  float* packed_p, float* cg, int32_t* done, void* stream);
+/* mjrl_cg_init with b = float(double(gsum) * scale) formed in the same launch and
+ * written to g (the VPG's mean from its all-reduced sums: mjrl_scale_vec + mjrl_cg_init
+ * in one launch; npg_cg.py:118-125). */
+int mjrl_cg_init_scaled(const mjrl_shape* s, const float* gsum, double scale, float* g, float* x, float* r, float* p,
+                        float* packed_p, float* cg, int32_t* done, void* stream);
 int mjrl_cg_step(const mjrl_shape* s, const float* gsum, double inv_T, float damping,
                  const float* packed_theta, float* x, float* r, float* p, float* z,
                  float* packed_p, float* cg, int32_t* done, float residual_tol,

@@ -81,6 +81,7 @@ SIGNATURES = {
     "mjrl_gather_grads": [SP, C.POINTER(Rows), I64, C.POINTER(Scratch), I32, P, P, P],
     "mjrl_fused_path": [SP],
     "mjrl_cg_init": [SP, P, P, P, P, P, P, P, P],
+    "mjrl_cg_init_scaled": [SP, P, F64, P, P, P, P, P, P, P, P],
     "mjrl_cg_step": [SP, P, F64, F32, P, P, P, P, P, P, P, P, F32, P],
     "mjrl_gather_cg_z": [SP, C.POINTER(Rows), I64, C.POINTER(Scratch), P, P, F64, F32, P, P, P, P, P],
     "mjrl_cg_step_xr_p": [SP, P, P, P, P, P, P, P, P, F32, P],

@@ -539,7 +539,7 @@ __global__ void __launch_bounds__(64 * GAE_WAVES) k_gae(const double* __restrict
 // (discount_sum(rewards, gamma)), wave 1 the advantages (discount_sum(td, gamma
 // lambda), or nothing without GAE), wave 2 the path-return sum (front to back) —
 // each lane one path; wave 3 only loads and stores.  A dependent fp64 multiply -> add costs ~10 cycles of issue
-// per step for the whole wave (tools/gae_latency.hip), so 32 paths advance for the
+// per step for the whole wave (tools/gae_latency.hip), so LP_PATHS paths advance for the
 // price k_gae paid for one.  The paths' steps come through LDS in windows of LP_W
 // steps per path (backward windows aligned at each path's end, forward windows at
 // its start): all four waves load window j + 1 into registers (each instruction 8
@@ -547,8 +547,10 @@ __global__ void __launch_bounds__(64 * GAE_WAVES) k_gae(const double* __restrict
 // the way) after a barrier; the chains write their outputs in place, and the
 // window leaves for HBM with coalesced writes.  Bit-identical to k_gae: the same
 // __dmul_rn / __dadd_rn / __dsub_rn per step in the same order.
-constexpr int LP_PATHS = 32;              // paths per workgroup (lanes 0..31 of each chain wave)
-constexpr int LP_W = 128;                 // steps per window
+constexpr int LP_PATHS = 8;               // paths per workgroup (lanes 0..7 of each chain wave)
+constexpr int LP_W = 512;                 // steps per window: a window's chain (~2.5 us) covers the
+                                          // HBM latency of the next window's loads (128-step windows of
+                                          // 32 paths waited ~5 us a window on them, r06b/gae_probe.txt)
 constexpr int LP_LD = LP_W + 1;           // LDS row stride (doubles): chain lanes conflict-free
 constexpr int LP_GB = 16;                 // chain steps per register batch
 constexpr int LP_T = 256;                 // 4 waves: three chain waves, all four load / store
@@ -579,9 +581,10 @@ __global__ void __launch_bounds__(LP_T) k_gae_lp(const double* __restrict__ rew,
     int64_t hmax = 0;
     for (int i = 0; i < np; ++i) hmax = se[i] - sb[i] > hmax ? se[i] - sb[i] : hmax;
     const int nwin = (int)((hmax + LP_W - 1) / LP_W);
-    // this thread's path (8 threads a path) and its steps u = (tid & 7) + 8 k of every
-    // window: each load instruction reads 8 paths' runs of 8 consecutive steps
-    const int mp = tid >> 3, mu = tid & 7;
+    // this thread's path (LP_TPP threads a path) and its steps u = mu + LP_TPP k of every
+    // window: each load instruction reads runs of LP_TPP consecutive steps
+    constexpr int LP_TPP = LP_T / LP_PATHS;
+    const int mp = tid / LP_TPP, mu = tid % LP_TPP;
     // an empty path (or a lane past the last path) reads index 0: valid whenever a
     // window exists, and never used (the chains and the drain skip its steps)
     const int64_t pb = se[mp] > sb[mp] ? sb[mp] : 0, pe = se[mp] > sb[mp] ? se[mp] : 1;
@@ -592,7 +595,7 @@ __global__ void __launch_bounds__(LP_T) k_gae_lp(const double* __restrict__ rew,
         // loads from clamped indices, unconditional (no exec-masked loads in the stream)
 #pragma unroll
         for (int k = 0; k < LP_PER; ++k) {
-            const int u = mu + 8 * k;
+            const int u = mu + LP_TPP * k;
             int64_t tb = pe - (int64_t)(j + 1) * LP_W + u, tf = pb + (int64_t)j * LP_W + u;
             tb = tb < pb ? pb : tb;
             tf = tf < pe ? tf : pe - 1;
@@ -606,7 +609,7 @@ __global__ void __launch_bounds__(LP_T) k_gae_lp(const double* __restrict__ rew,
     auto put = [&](int j) {
 #pragma unroll
         for (int k = 0; k < LP_PER; ++k) {
-            const int u = mu + 8 * k;
+            const int u = mu + LP_TPP * k;
             const int64_t tb = pe - (int64_t)(j + 1) * LP_W + u;
             const double bn = tb + 1 < pe ? xn[k] : pbl;   // b1[t + 1] (process_samples.py:24-27)
             RB[mp * LP_LD + u] = xr[k];
@@ -619,7 +622,7 @@ __global__ void __launch_bounds__(LP_T) k_gae_lp(const double* __restrict__ rew,
     auto drain = [&](int j) {   // window j's outputs (in RB / TD) to HBM
 #pragma unroll
         for (int k = 0; k < LP_PER; ++k) {
-            const int u = mu + 8 * k;
+            const int u = mu + LP_TPP * k;
             const int64_t tb = de - (int64_t)(j + 1) * LP_W + u;
             if (tb >= db) {
                 const double rr = RB[mp * LP_LD + u];

@@ -435,9 +435,13 @@ __global__ void __launch_bounds__(CGM_T) k_cgm_p(mjrl_shape s, const float* __re
 
 // cg_solve.py:4-7 over many workgroups: x = 0, r = p = b (and packed p), rdotr
 // = b.b folded in fixed order by the last workgroup.
-__global__ void __launch_bounds__(CGM_T) k_cgm_init(mjrl_shape s, const float* __restrict__ b, float* __restrict__ x,
+// b: the right-hand side, or (gsum != null) b = float(double(gsum) * scale) formed
+// here and written to b (the VPG's mean from its sums, k_scale_vec's arithmetic:
+// one launch fewer per update)
+__global__ void __launch_bounds__(CGM_T) k_cgm_init(mjrl_shape s, float* __restrict__ b, float* __restrict__ x,
                                                     float* __restrict__ r, float* __restrict__ p,
-                                                    float* __restrict__ packed_p, float* cg, int32_t* __restrict__ done) {
+                                                    float* __restrict__ packed_p, float* cg, int32_t* __restrict__ done,
+                                                    const float* __restrict__ gsum, double scale) {
     __shared__ double red[CGM_T / 64];
     const PackMap pm(s);
     double acc = 0.0;
@@ -445,7 +449,13 @@ __global__ void __launch_bounds__(CGM_T) k_cgm_init(mjrl_shape s, const float* _
     for (int u = 0; u < CGM_U; ++u) {
         const int f = blockIdx.x * CGM_WG + u * CGM_T + threadIdx.x;
         if (f >= s.d) continue;
-        const float v = b[f];
+        float v;
+        if (gsum) {
+            v = (float)((double)gsum[f] * scale);
+            b[f] = v;
+        } else {
+            v = b[f];
+        }
         x[f] = 0.f;
         r[f] = v;
         p[f] = v;
@@ -625,13 +635,28 @@ int mjrl_cg_init(const mjrl_shape* s, const float* b, float* x, float* r, float*
     if (!s || !b || !x || !r || !p || !packed_p || !cg || !done) return MJRL_EINVAL;
     const int nwg = (s->d + CGM_WG - 1) / CGM_WG;
     if (nwg <= CGM_MAXWG && nwg > 0) {
-        hipLaunchKernelGGL(k_cgm_init, dim3(nwg), dim3(CGM_T), 0, (hipStream_t)stream, *s, b, x, r, p, packed_p, cg,
-                           done);
+        hipLaunchKernelGGL(k_cgm_init, dim3(nwg), dim3(CGM_T), 0, (hipStream_t)stream, *s, const_cast<float*>(b), x, r,
+                           p, packed_p, cg, done, (const float*)nullptr, 0.0);
         return err(hipGetLastError());
     }
     hipLaunchKernelGGL(k_cg_init, dim3(1), dim3(CG_THREADS), 0, (hipStream_t)stream, *s, b, x, r, p, packed_p, cg,
                        done);
     return err(hipGetLastError());
+}
+
+int mjrl_cg_init_scaled(const mjrl_shape* s, const float* gsum, double scale, float* g, float* x, float* r, float* p,
+                        float* packed_p, float* cg, int32_t* done, void* stream) {
+    if (!s || !gsum || !g || !x || !r || !p || !packed_p || !cg || !done) return MJRL_EINVAL;
+    const int nwg = (s->d + CGM_WG - 1) / CGM_WG;
+    if (nwg <= CGM_MAXWG && nwg > 0) {
+        hipLaunchKernelGGL(k_cgm_init, dim3(nwg), dim3(CGM_T), 0, (hipStream_t)stream, *s, g, x, r, p, packed_p, cg,
+                           done, gsum, scale);
+        return err(hipGetLastError());
+    }
+    // beyond the multi-workgroup partials: the two launches
+    const int rc = mjrl_scale_vec(gsum, s->d, scale, g, stream);
+    if (rc != MJRL_OK) return rc;
+    return mjrl_cg_init(s, g, x, r, p, packed_p, cg, done, stream);
 }
 
 int mjrl_cg_step_xr_p(const mjrl_shape* s, float* x, const float* r, float* r_out, float* p, const float* z,

@@ -697,6 +697,7 @@ class UpdateEngine:
         self.mom_part = torch.zeros(4 * 256 + 16, dtype=torch.float64, device=dev)
         self.mom2_part = torch.zeros(_lib.MOM_SCRATCH, dtype=torch.float64, device=dev)   # one-launch moments
         self.transforms = (None, None, None, None)
+        self._act_rows = None   # set per update: the batch's f32 actions when the row passes read them in place
         # sharded schedule (one rank of several, or a one-rank communicator forced
         # onto it): moments through one all-gather + mjrl_moments_combine, an
         # all-reduce between every FVP's gather and its CG step
@@ -834,6 +835,8 @@ class UpdateEngine:
         for k, key in (("act", "act32"), ("adv", "adv32"), ("a0", "a0"), ("a1", "a1"),
                        ("mu0", "mu0"), ("ll0", "ll0"), ("gu0", "gu0"), ("gu1", "gu1"), ("gp", "gp")):
             setattr(r, k, w[key].data_ptr())
+        if self._act_rows is not None:   # the batch's own f32 actions (no copy into act32)
+            r.act = self._act_rows.data_ptr()
         if self.split:
             r.xs, r.xu, r.xc = w["xs"].data_ptr(), w["xu"].data_ptr(), w["xc"].data_ptr()
         else:
@@ -1058,9 +1061,16 @@ class UpdateEngine:
             # into the forward pass below when it can be (_fused_pack): then only the
             # column scales and the f32 actions here
             fused = self._fused_pack(batch, T_all, T_all if (algo == "dapg" and demo_coef is not None) else T)
+            self._act_rows = None
             if fused:
                 self._colscale(batch.obs, T_all, st, batch.obs_range)
-                w["act32"][:T_all].copy_(batch.act[:T_all])
+                if batch.act.dtype == torch.float32 and batch.act.is_contiguous() and tuple(batch.act.shape) == (
+                        T_all, s.m):
+                    # f32 staging: the row passes read the staged actions where they are
+                    # (a [T][m] copy into act32 cost ~30 us per 1M-row update)
+                    self._act_rows = batch.act
+                else:
+                    w["act32"][:T_all].copy_(batch.act[:T_all])
             else:
                 self._pack(batch.obs, batch.act, T_all, st, batch.obs_range)
             main.wait_stream(side)
@@ -1117,7 +1127,9 @@ class UpdateEngine:
                 _lib.check(L.mjrl_policy_vpg(sp, C.byref(rows), _lib.ptr(self.packed_theta), _lib.ptr(osh),
                                              _lib.ptr(osc), C.byref(sc), _lib.ptr(v["gsum"]), st), "mjrl_policy_vpg")
             self.comm.allreduce_sum(v["gsum"])
-            _lib.check(L.mjrl_scale_vec(_lib.ptr(v["gsum"]), s.d, inv_T, _lib.ptr(v["g"]), st), "mjrl_scale_vec")
+            if algo == "vpg":
+                _lib.check(L.mjrl_scale_vec(_lib.ptr(v["gsum"]), s.d, inv_T, _lib.ptr(v["g"]), st), "mjrl_scale_vec")
+            # (otherwise g = gsum / T is formed by the CG initialisation below, in the same launch)
             timing[1].record()
 
             # a12-a13: conjugate gradient with the device FVP
@@ -1127,9 +1139,9 @@ class UpdateEngine:
                 x = v["g"]
                 cg_iters_run = 0
             else:
-                _lib.check(L.mjrl_cg_init(sp, _lib.ptr(v["g"]), _lib.ptr(v["x"]), _lib.ptr(v["r"]), _lib.ptr(v["p"]),
-                                          _lib.ptr(self.packed_p), _lib.ptr(self.cg), _lib.ptr(self.done), st),
-                           "mjrl_cg_init")
+                _lib.check(L.mjrl_cg_init_scaled(sp, _lib.ptr(v["gsum"]), inv_T, _lib.ptr(v["g"]), _lib.ptr(v["x"]),
+                                                 _lib.ptr(v["r"]), _lib.ptr(v["p"]), _lib.ptr(self.packed_p),
+                                                 _lib.ptr(self.cg), _lib.ptr(self.done), st), "mjrl_cg_init_scaled")
                 prof = self.kernel_timing
                 inv_T_fvp = inv_T if sub is None else 1.0 / max(sub["Ts"], 1)
                 # gather + CG z fused when no all-reduce sits between them and the CG
@@ -1556,6 +1568,7 @@ class UpdateEngine:
         batch_reinforce.py:38 does) as the current rows."""
         T = int(obs.shape[0])
         self._ensure(T, 1)
+        self._act_rows = None   # the rows' actions are act32's from here on
         self.st = st = _lib.stream_ptr()
         dev = self.device
         o = torch.from_numpy(np.ascontiguousarray(obs, dtype=np.float64)).to(dev)

@@ -444,8 +444,9 @@ def e2e_stream(paths_range, eng, th0, base, upd, device, cfg, nslots=64):
                 ts = [t] * len(grp)
                 sink.rows(slots, np.stack([paths[ep]["observations"][t] for ep in grp]), ts)
                 sink.actions(slots, np.stack([paths[ep]["actions"][t] for ep in grp]), ts)
+                sink.rewards(slots, [paths[ep]["rewards"][t] for ep in grp], ts)
             for j in slots:
-                sink.finish(j, H)
+                sink.finish(j, H, False)
             tf += time.perf_counter() - f0
         t0 = time.perf_counter()
         b = sink.batch(paths)
@@ -462,7 +463,8 @@ def e2e_stream(paths_range, eng, th0, base, upd, device, cfg, nslots=64):
                 note="StreamSink fed per lock step as the vectorised sampler feeds it (observation rows through "
                      "mjrl_host_stage_rows_f64x into pinned per-slot slabs, each trajectory copied to HBM when it "
                      "ends); post_sampling_ms = from the last trajectory's hand-over to the update's readback "
-                     "(gather of the padded slabs, 1-D slots, update); feed_ms = the sampler-side cost of the "
+                     "(the padded slabs are the batch when every path runs the full horizon, else one device "
+                     "gather; offsets / flags; update); feed_ms = the sampler-side cost of the "
                      "hand-overs (spread over sampling, timed without environments); median of 2")
 
 

@@ -900,20 +900,14 @@ __global__ void __launch_bounds__(MOM_THREADS) k_moments2(const double* __restri
     }
 }
 
-// whitening (k_whiten) and, in the same launch, the moments of the f32 output
-// (the surr_before numerator, npg_cg.py:113 with LR == 1)
-__global__ void __launch_bounds__(MOM_THREADS) k_whiten_mom(const double* __restrict__ adv, int64_t T,
-                                                            const double* __restrict__ m1,
-                                                            const double* __restrict__ m2, double eps,
-                                                            float* __restrict__ adv32, double* __restrict__ w64,
-                                                            double* part, double* __restrict__ out) {
-    __shared__ double red[MOM_THREADS / 64];
-    const double mean = m1[0] / m1[2];
-    const double sd = sqrt(m2[1] / m1[2]);
-    const double den = sd + eps;
+// whitening of block blk of nblk (k_whiten's arithmetic) and the block partial of
+// the f32 output's moments
+__device__ __forceinline__ void whiten_block(const double* __restrict__ adv, int64_t T, double mean, double den,
+                                             int blk, int nblk, float* __restrict__ adv32, double* __restrict__ w64,
+                                             double* red, double (&o)[4]) {
     double s1 = 0.0, s2 = 0.0, mn = __builtin_inf(), mx = -__builtin_inf();
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < T; i += stride) {
+    const int64_t stride = (int64_t)nblk * blockDim.x;
+    for (int64_t i = (int64_t)blk * blockDim.x + threadIdx.x; i < T; i += stride) {
         const double w = (adv[i] - mean) / den;
         const float wf = (float)w;
         adv32[i] = wf;
@@ -924,7 +918,6 @@ __global__ void __launch_bounds__(MOM_THREADS) k_whiten_mom(const double* __rest
         mn = fmin(mn, v);
         mx = fmax(mx, v);
     }
-    double o[4];
     o[0] = block_sum<MOM_THREADS>(s1, red);
     o[1] = block_sum<MOM_THREADS>(s2, red);
 #pragma unroll
@@ -946,10 +939,64 @@ __global__ void __launch_bounds__(MOM_THREADS) k_whiten_mom(const double* __rest
     }
     o[2] = mn;
     o[3] = mx;
+}
+
+// whitening (k_whiten) and, in the same launch, the moments of the f32 output
+// (the surr_before numerator, npg_cg.py:113 with LR == 1)
+__global__ void __launch_bounds__(MOM_THREADS) k_whiten_mom(const double* __restrict__ adv, int64_t T,
+                                                            const double* __restrict__ m1,
+                                                            const double* __restrict__ m2, double eps,
+                                                            float* __restrict__ adv32, double* __restrict__ w64,
+                                                            double* part, double* __restrict__ out) {
+    __shared__ double red[MOM_THREADS / 64];
+    const double mean = m1[0] / m1[2];
+    const double sd = sqrt(m2[1] / m1[2]);
+    const double den = sd + eps;
+    double o[4];
+    whiten_block(adv, T, mean, den, blockIdx.x, gridDim.x, adv32, w64, red, o);
     if (mom_publish(part, o, gridDim.x)) {
         mom_fold(part, 0, gridDim.x, T, out);
         if (threadIdx.x == 0) *reinterpret_cast<unsigned*>(part + MOM2_TICKET) = 0u;
     }
+}
+
+// Small batches: the two moment passes (advantages and path returns) and the
+// whitening with its output moments in ONE workgroup and one launch (three before:
+// k_moments2 twice, k_whiten_mom), bit-identical to them: the workgroup walks
+// their blocks one after another with the same per-block arithmetic (mom_block,
+// whiten_block) and folds the partials with the same mom_fold, in the same order.
+__global__ void __launch_bounds__(MOM_THREADS) k_mom_whiten_small(
+    const double* __restrict__ adv, int64_t T, const double* __restrict__ pr, int64_t P, double eps,
+    float* __restrict__ adv32, double* __restrict__ w64, int nb1, int nb2, double* part, double* m1, double* pm1,
+    double* m2, double* pm2, double* ms) {
+    __shared__ double red[MOM_THREADS / 64];
+    double o[4];
+    for (int pass = 0; pass < 2; ++pass) {
+        const double c1 = pass ? m1[0] / m1[2] : 0.0, c2 = pass ? pm1[0] / pm1[2] : 0.0;
+        for (int b = 0; b < nb1 + nb2; ++b) {
+            if (b < nb1)
+                mom_block(adv, T, c1, b, nb1, red, o);
+            else
+                mom_block(pr, P, c2, b - nb1, nb2, red, o);
+            if (threadIdx.x == 0)
+                for (int k = 0; k < 4; ++k) part[4 * b + k] = o[k];
+        }
+        __syncthreads();
+        if (threadIdx.x < 64) {
+            mom_fold(part, 0, nb1, T, pass ? m2 : m1);
+            mom_fold(part, nb1, nb1 + nb2, P, pass ? pm2 : pm1);
+        }
+        __syncthreads();
+    }
+    const double mean = m1[0] / m1[2];
+    const double den = sqrt(m2[1] / m1[2]) + eps;
+    for (int b = 0; b < nb1; ++b) {
+        whiten_block(adv, T, mean, den, b, nb1, adv32, w64, red, o);
+        if (threadIdx.x == 0)
+            for (int k = 0; k < 4; ++k) part[4 * b + k] = o[k];
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) mom_fold(part, 0, nb1, T, ms);
 }
 
 // adv32 = float((adv - mean) / (std + 1e-6)) (npg_cg.py:91; .float() at batch_reinforce.py:38)
@@ -1392,6 +1439,19 @@ int mjrl_whiten_moments(const double* adv, int64_t T, const double* m1, const do
     const int nb = grid_for(T, MOM_THREADS * 4, mom2_grid(T));
     hipLaunchKernelGGL(k_whiten_mom, dim3(nb), dim3(MOM_THREADS), 0, (hipStream_t)stream, adv, T, m1, m2, eps, adv32,
                        w64, rpart, out);
+    return err(hipGetLastError());
+}
+
+int mjrl_moments_whiten_small(const double* adv, int64_t T, const double* path_ret, int64_t P, double eps,
+                              float* adv32, double* w64, double* rpart, double* m1, double* pm1, double* m2,
+                              double* pm2, double* ms, void* stream) {
+    if (T < 0 || P < 0 || !adv || !path_ret || !adv32 || !rpart || !m1 || !pm1 || !m2 || !pm2 || !ms)
+        return MJRL_EINVAL;
+    const int nb1 = grid_for(T, MOM_THREADS * 4, mom2_grid(T));
+    const int nb2 = grid_for(P, MOM_THREADS * 4, mom2_grid(P));
+    if (nb1 + nb2 > MOM2_MAXB) return MJRL_EINVAL;
+    hipLaunchKernelGGL(k_mom_whiten_small, dim3(1), dim3(MOM_THREADS), 0, (hipStream_t)stream, adv, T, path_ret, P,
+                       eps, adv32, w64, nb1, nb2, rpart, m1, pm1, m2, pm2, ms);
     return err(hipGetLastError());
 }
 

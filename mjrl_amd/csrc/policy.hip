@@ -1278,10 +1278,17 @@ bool ks_supported(const mjrl_shape* s) {
     return kg == 2 || kg == 4 || kg == 6 || kg == 8 || kg == 12;
 }
 
+// persistent grid of the 32-row-tile kernels: at most FGRID_CAP workgroups, as few
+// as give every workgroup the same (largest) tile count: the critical path is
+// ceil(tiles / FGRID_CAP) tiles either way, and each workgroup fewer is one weight-
+// gradient slab fewer for the gather (125k rows: 3907 tiles on 245 workgroups,
+// not 256)
 inline int ks_grid(int64_t T) {
     int64_t nt = (T + 31) / 32;
     if (nt < 1) nt = 1;
-    return (int)(nt < FGRID_CAP ? nt : FGRID_CAP);
+    if (nt <= FGRID_CAP) return (int)nt;
+    const int64_t per = (nt + FGRID_CAP - 1) / FGRID_CAP;
+    return (int)((nt + per - 1) / per);
 }
 
 // which accumulate kernel runs for (shape, T): 2 = K-split, 1 = fused, 0 = rows + wgrad

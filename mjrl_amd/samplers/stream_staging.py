@@ -18,9 +18,11 @@ sampling loop of samplers/vector_sampler.py:
   - when a trajectory ends, its rows are copied to HBM on the staging copy
     stream at the trajectory's fixed position ep * H of a padded device slab,
     while the other environments keep stepping;
+  - rewards and the predictions travel the same way (8 bytes a row each);
   - after sampling, batch() compacts the padded slabs into the contiguous
-    layout with one device gather (mjrl_gather_rows) and stages the 1-D slots
-    (rewards, offsets, flags, predictions: 24 bytes a row).
+    layout with one device gather per slot (mjrl_gather_rows; none when every
+    trajectory ran the full horizon: the padded slabs are then the batch) and
+    stages the path offsets and flags.
 
 The DeviceBatch it returns is bit-identical to DeviceBatch.from_paths on the
 same paths (the same f32 rounding, the same per-row prediction arithmetic,
@@ -66,11 +68,13 @@ class StreamSink:
         ent = _SLABS.get(key)
         if ent is None:
             _SLABS.clear()   # one shape at a time
-            ent = _SLABS[key] = dict(obs=torch.empty((S, B, H, self.n), dtype=torch.float32, pin_memory=True),
-                                     act=torch.empty((S, B, H, self.m), dtype=torch.float32, pin_memory=True),
-                                     pred=np.zeros((S, B, H), np.float64), ev=[[None] * B for _ in range(S)])
-        self._obs, self._act, self.pred_h, self._ev = ent["obs"], ent["act"], ent["pred"], ent["ev"]
-        self.obs_h, self.act_h = self._obs.numpy(), self._act.numpy()
+            pin = lambda *shape, dt=torch.float32: torch.empty(shape, dtype=dt, pin_memory=True)   # noqa: E731
+            ent = _SLABS[key] = dict(obs=pin(S, B, H, self.n), act=pin(S, B, H, self.m),
+                                     rew=pin(S, B, H, dt=torch.float64), pred=pin(S, B, H, dt=torch.float64),
+                                     ev=[[None] * B for _ in range(S)])
+        self._obs, self._act, self._rew, self._pred, self._ev = (ent[k] for k in ("obs", "act", "rew", "pred", "ev"))
+        self.obs_h, self.act_h, self.rew_h, self.pred_h = (t.numpy() for t in (self._obs, self._act, self._rew,
+                                                                               self._pred))
         self._row_ptr0 = self.obs_h.ctypes.data
         self.buf = np.zeros(S, np.int64)
         self.ep = np.full(S, -1, np.int64)
@@ -78,12 +82,13 @@ class StreamSink:
         self.hi = np.full(self.n, -np.inf, np.float32)
         self.flag = np.zeros(1, np.int32)
         self.lengths = np.zeros(self.N, np.int64)
-        self.pred = [None] * self.N
+        self.term = np.zeros(self.N, np.uint8)
         with torch.cuda.device(self.device):
-            self.obs_pad = _STAGING.device_slot("stream_obs", self.N * H * self.n, np.float32, self.device) \
-                .view(self.N * H, self.n)
-            self.act_pad = _STAGING.device_slot("stream_act", self.N * H * self.m, np.float32, self.device) \
-                .view(self.N * H, self.m)
+            slot = lambda name, k, dt: _STAGING.device_slot(name, self.N * H * k, dt, self.device)   # noqa: E731
+            self.obs_pad = slot("stream_obs", self.n, np.float32).view(self.N * H, self.n)
+            self.act_pad = slot("stream_act", self.m, np.float32).view(self.N * H, self.m)
+            self.rew_pad = slot("stream_rew", 1, np.float64)
+            self.pred_pad = slot("stream_pred", 1, np.float64) if self.coeffs is not None else None
             self.cs = _STAGING._copy_stream(self.device)
             # the padded slabs may still be read by work queued on the current stream
             self.cs.wait_stream(torch.cuda.current_stream(self.device))
@@ -126,16 +131,30 @@ class StreamSink:
         slots = np.asarray(slots, np.int64)
         self.act_h[slots, self.buf[slots], np.asarray(t, np.int64)] = np.asarray(act, dtype=np.float64)
 
-    def finish(self, slot, length):
-        """Slot `slot`'s trajectory ended after `length` rows: its rows leave for
-        HBM now, on the copy stream, while sampling continues."""
+    def rewards(self, slots, rew, t):
+        """Rewards rew [E] (f64) of environments `slots` at path indices t."""
+        slots = np.asarray(slots, np.int64)
+        self.rew_h[slots, self.buf[slots], np.asarray(t, np.int64)] = np.asarray(rew, dtype=np.float64)
+
+    def reward(self, slot, t, r):
+        """One environment's reward at path index t (the sampler's per-step call)."""
+        self.rew_h[slot, self.buf[slot], t] = r
+
+    def finish(self, slot, length, terminated=False):
+        """Slot `slot`'s trajectory ended after `length` rows: its rows (observations,
+        actions, rewards, baseline predictions) leave for HBM now, on the copy
+        stream, while sampling continues."""
         ep, b, Lr = int(self.ep[slot]), int(self.buf[slot]), int(length)
         self.lengths[ep] = Lr
-        self.pred[ep] = self.pred_h[slot, b, :Lr].copy() if self.coeffs is not None else None
+        self.term[ep] = bool(terminated)
         if Lr:
+            H = self.H
             with torch.cuda.stream(self.cs):
-                self.obs_pad[ep * self.H: ep * self.H + Lr].copy_(self._obs[slot, b, :Lr], non_blocking=True)
-                self.act_pad[ep * self.H: ep * self.H + Lr].copy_(self._act[slot, b, :Lr], non_blocking=True)
+                self.obs_pad[ep * H: ep * H + Lr].copy_(self._obs[slot, b, :Lr], non_blocking=True)
+                self.act_pad[ep * H: ep * H + Lr].copy_(self._act[slot, b, :Lr], non_blocking=True)
+                self.rew_pad[ep * H: ep * H + Lr].copy_(self._rew[slot, b, :Lr], non_blocking=True)
+                if self.pred_pad is not None:
+                    self.pred_pad[ep * H: ep * H + Lr].copy_(self._pred[slot, b, :Lr], non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(self.cs)
             self._ev[slot][b] = ev
@@ -156,31 +175,40 @@ class StreamSink:
         T = int(lengths.sum())
         cur = torch.cuda.current_stream(dev)
         cur.wait_stream(self.cs)   # every trajectory's copy
-        idx = np.concatenate([ep * H + np.arange(L, dtype=np.int64) for ep, L in enumerate(lengths)]) \
-            if T else np.zeros(0, np.int64)
-        idx_d = torch.from_numpy(idx).to(dev, non_blocking=False)
-        obs = _STAGING.device_slot("obs", T * self.n, np.float32, dev).view(T, self.n) if reuse else \
-            torch.empty((T, self.n), dtype=torch.float32, device=dev)
-        act = _STAGING.device_slot("act", T * self.m, np.float32, dev).view(T, self.m) if reuse else \
-            torch.empty((T, self.m), dtype=torch.float32, device=dev)
-        L = _lib.lib()
-        st = _lib.stream_ptr()
-        if T:
-            _lib.check(L.mjrl_gather_rows(_lib.ptr(self.obs_pad), 4 * self.n, _lib.ptr(idx_d), T, _lib.ptr(obs), st),
-                       "mjrl_gather_rows")
-            _lib.check(L.mjrl_gather_rows(_lib.ptr(self.act_pad), 4 * self.m, _lib.ptr(idx_d), T, _lib.ptr(act), st),
-                       "mjrl_gather_rows")
 
         def stage(slot, arrs, ncols, dtype=np.float64):
             return _STAGING.stage(slot, arrs, ncols, dtype, dev, reuse)
 
+        offs = np.concatenate([[0], np.cumsum(lengths)]).astype(np.int64)
+        off = stage("off", [offs], 0, np.int64)
+        term = stage("term", [self.term], 0, np.uint8)
         orange = stage("orange", [np.stack([self.lo, self.hi])], self.n, np.float32)
-        rew = stage("rew", [p["rewards"] for p in paths], 0)
-        off = stage("off", [np.concatenate([[0], np.cumsum(lengths)]).astype(np.int64)], 0, np.int64)
-        term = stage("term", [np.array([bool(p.get("terminated", False)) for p in paths], dtype=np.uint8)], 0,
-                     np.uint8)
-        if self.coeffs is not None:
-            base = stage("base", self.pred, 0)
+        pads = [("obs", self.obs_pad, self.n, np.float32), ("act", self.act_pad, self.m, np.float32),
+                ("rew", self.rew_pad, 1, np.float64)] + \
+            ([("base", self.pred_pad, 1, np.float64)] if self.pred_pad is not None else [])
+        out = {}
+        if T == N * H:
+            # every trajectory ran the full horizon: the padded slabs are the batch
+            for name, pad, k, _ in pads:
+                out[name] = pad[:T] if k == 1 else pad.view(-1)[:T * k].view(T, k)
+        else:
+            # compact: row i of the batch is row ep H + (i - off[ep]) of the slabs, one
+            # device gather per slot
+            start = torch.from_numpy(np.arange(N, dtype=np.int64) * H - offs[:-1]).to(dev)
+            idx = torch.arange(T, dtype=torch.int64, device=dev) + torch.repeat_interleave(
+                start, torch.from_numpy(lengths).to(dev), output_size=T)
+            L = _lib.lib()
+            st = _lib.stream_ptr()
+            for name, pad, k, dt in pads:
+                dst = _STAGING.device_slot(name, T * k, dt, dev) if reuse else \
+                    torch.empty(T * k, dtype=torch.float32 if dt == np.float32 else torch.float64, device=dev)
+                if T:
+                    _lib.check(L.mjrl_gather_rows(_lib.ptr(pad), k * np.dtype(dt).itemsize, _lib.ptr(idx), T,
+                                                  _lib.ptr(dst), st), "mjrl_gather_rows")
+                out[name] = dst.view(T, k) if k > 1 else dst
+        obs, act, rew = out["obs"], out["act"], out["rew"]
+        if self.pred_pad is not None:
+            base = out["base"]
         elif not self.linear and self.baseline is not None:
             # another baseline: its own predict per path, as DeviceBatch.from_paths
             # (process_samples.py:23)

@@ -151,7 +151,7 @@ def sample_paths_vectorized(N, policy, T=1e6, env=None, env_name=None, pegasus_s
 
     def finish(s, done):
         if sink is not None:
-            sink.finish(s.idx, s.t)
+            sink.finish(s.idx, s.t, bool(done))
         paths[s.ep] = dict(observations=np.array(s.obs), actions=np.array(s.act), rewards=np.array(s.rew),
                            agent_infos=_stack(s.ainfo), env_infos=_stack(s.einfo), terminated=done)
         if s.ep == N - 1:
@@ -175,6 +175,8 @@ def sample_paths_vectorized(N, policy, T=1e6, env=None, env_name=None, pegasus_s
             sink.actions(idx, np.stack(acts), ts)
         for s, mean, a in zip(live, means, acts):
             next_o, r, done, info = s.env.step(a)
+            if sink is not None:
+                sink.reward(s.idx, s.t, r)
             s.obs.append(s.o)
             s.act.append(a)
             s.rew.append(r)

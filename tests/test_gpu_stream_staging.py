@@ -20,8 +20,8 @@ def _same_batch(a, b):
     assert a.obs_inexact == b.obs_inexact and np.array_equal(a.lengths, b.lengths)
 
 
-@pytest.mark.parametrize("fitted", [False, True])
-def test_stream_batch_equals_from_paths(fitted):
+@pytest.mark.parametrize("fitted,ragged", [(False, True), (True, True), (True, False)])
+def test_stream_batch_equals_from_paths(fitted, ragged):
     from mjrl_amd.baselines.linear_baseline import LinearBaseline
     from mjrl_amd.engine import DeviceBatch
     from mjrl_amd.policies.gaussian_mlp import MLP
@@ -40,13 +40,16 @@ def test_stream_batch_equals_from_paths(fitted):
     def make(N, H, S):
         sinks.append(StreamSink(6, 2, H, N, dev, baseline=base, nslots=S))
         return sinks[-1]
-    plain = sample_paths_vectorized(37, policy, 1e6, env=StubEnv, pegasus_seed=7, num_envs=8)
-    paths = sample_paths_vectorized(37, policy, 1e6, env=StubEnv, pegasus_seed=7, num_envs=8, sink=make)
+    # ragged: terminations (the sink's device gather); else every path runs the
+    # horizon (the padded slabs are the batch)
+    env = StubEnv if ragged else (lambda: StubEnv(radius=1e9))
+    plain = sample_paths_vectorized(37, policy, 1e6, env=env, pegasus_seed=7, num_envs=8)
+    paths = sample_paths_vectorized(37, policy, 1e6, env=env, pegasus_seed=7, num_envs=8, sink=make)
     for p, q in zip(paths, plain):
         assert np.array_equal(p["observations"], q["observations"]) and np.array_equal(p["actions"], q["actions"])
         assert p["terminated"] == q["terminated"]
     lengths = [len(p["rewards"]) for p in paths]
-    assert len(set(lengths)) > 1   # ragged: terminations moved the offsets
+    assert (len(set(lengths)) > 1) == ragged
     ref = DeviceBatch.from_paths(paths, dev, baseline=base, reuse=False)
     got = sinks[0].batch(paths, reuse=False)
     torch.cuda.synchronize()

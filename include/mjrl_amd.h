@@ -299,6 +299,11 @@ int mjrl_policy_eval(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_eval,
                      const float* packed_theta_new, const float* packed_theta_old,
                      const float* out_shift, const float* out_scale,
                      const mjrl_scratch* sc, double* sums, void* stream);
+/* The same, skipped whole (nothing written) while *skip != 0: the speculative
+ * evaluations of the device TRPO line search (mjrl_trpo_trial). */
+int mjrl_policy_eval_if(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_eval, const float* packed_theta_new,
+                        const float* packed_theta_old, const float* out_shift, const float* out_scale,
+                        const mjrl_scratch* sc, double* sums, const int32_t* skip, void* stream);
 
 /* The two steps behind the composites above, for callers that time or overlap
  * them separately.  *_accumulate writes per-slice partial sums of every weight /
@@ -415,6 +420,23 @@ int mjrl_npg_step(const mjrl_shape* s, const float* g, const float* x, const flo
                   int32_t mode, float delta, float alpha_in, int32_t const_lr,
                   float min_log_std, float* theta_new, float* packed_new, float* out,
                   void* stream);
+
+/* ---- TRPO line search on the device (trpo.py:105-118) ----
+ * Trial k >= 1: logs trial k - 1's evaluation (sums = [surr sum, kl sum] of
+ * mjrl_policy_eval; kl = float(sums[1] * inv_T)), and if kl >= kl_dist steps to
+ * alpha_k = float32(0.9) * alpha_{k-1} (f32), writing theta + alpha_k x (log-std
+ * clamp, packed copy) for the next mjrl_policy_eval_if; an accepted trial sets *skip,
+ * after which the remaining trials and evaluations of the sequence do nothing
+ * (out[0] = the accepted alpha, as a host step leaves it).
+ * apply = 0: log and test only.  alpha_0 is out[0] of the mode-0 mjrl_npg_step.
+ * ls: MJRL_LS_STATE floats, [1] accepted, [2] trials logged, [MJRL_LS_LOG + 3 t ..]
+ * trial t's (alpha, kl, surr); one readback after the sequence replaces a host round
+ * trip per trial (the host continues past the sequence's last trial as before). */
+#define MJRL_LS_LOG 32
+#define MJRL_LS_STATE 128
+int mjrl_trpo_trial(const mjrl_shape* s, const float* x, const float* theta, float min_log_std, float* theta_new,
+                    float* packed_new, float* out, const double* sums, double inv_T, double kl_dist, int32_t k,
+                    int32_t apply, float* ls, int32_t* skip, void* stream);
 
 /* ---- batched policy forward for vectorised sampling ----
  * Replaces the per-observation MuNet forward inside policy.get_action

@@ -22,6 +22,7 @@ MJRL_ESHAPE = -2
 CG_STATE = 4096   # MJRL_CG_STATE: floats of the device CG state
 CG_PZ_PARTS = 1024   # float offset of the fused gather's p.z partials (csrc/common.h)
 STEP_OUT = 1024   # MJRL_STEP_OUT: floats of mjrl_npg_step's out buffer
+LS_LOG, LS_STATE = 32, 128   # MJRL_LS_LOG / MJRL_LS_STATE (device TRPO line search state)
 MOM_SCRATCH = 2056   # MJRL_MOM_SCRATCH: doubles of the one-launch moments scratch
 
 
@@ -75,6 +76,7 @@ SIGNATURES = {
     "mjrl_policy_vpg": [SP, C.POINTER(Rows), P, P, P, C.POINTER(Scratch), P, P],
     "mjrl_policy_fvp": [SP, C.POINTER(Rows), I64, P, P, P, C.POINTER(Scratch), P, P, P],
     "mjrl_policy_eval": [SP, C.POINTER(Rows), I64, P, P, P, P, C.POINTER(Scratch), P, P],
+    "mjrl_policy_eval_if": [SP, C.POINTER(Rows), I64, P, P, P, P, C.POINTER(Scratch), P, P, P],
     "mjrl_vpg_accumulate": [SP, C.POINTER(Rows), P, P, P, C.POINTER(Scratch), P],
     "mjrl_vpg_accumulate_pack": [SP, C.POINTER(Rows), P, P, P, P, C.POINTER(Scratch), P],
     "mjrl_policy_vpg_pack": [SP, C.POINTER(Rows), P, P, P, P, C.POINTER(Scratch), P, P],
@@ -100,6 +102,7 @@ SIGNATURES = {
     "mjrl_linear_baseline_gram_f32x2": [P, P, P, I64, I32, P, I64, P, P, P],
     "mjrl_linear_baseline_residual_f32x2": [P, P, P, I64, I32, P, I64, P, P, P, P],
     "mjrl_npg_step": [SP, P, P, P, I32, F32, F32, I32, F32, P, P, P, P],
+    "mjrl_trpo_trial": [SP, P, P, F32, P, P, P, P, F64, F64, I32, I32, P, P, P],
     "mjrl_policy_mean": [SP, P, I64, P, P, P, P, P, P, P],
     "mjrl_build_flags": [],
     "mjrl_host_stage_f64": [P, I64, I32, P, P, P],

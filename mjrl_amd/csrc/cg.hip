@@ -506,12 +506,12 @@ __global__ void __launch_bounds__(CGM_T) k_npgm_dot(int d, const float* __restri
     }
 }
 
-__global__ void __launch_bounds__(CGM_T) k_npgm_apply(mjrl_shape s, const float* __restrict__ x,
-                                                      const float* __restrict__ theta, float min_ls,
-                                                      float* __restrict__ theta_new, float* __restrict__ packed_new,
-                                                      const float* __restrict__ out) {
+// theta_new = theta + alpha x over this workgroup's elements, the log-std clamp of
+// set_param_values, the packed copy
+__device__ __forceinline__ void apply_step(const mjrl_shape& s, const float* __restrict__ x,
+                                           const float* __restrict__ theta, float min_ls, float alpha,
+                                           float* __restrict__ theta_new, float* __restrict__ packed_new) {
     const PackMap pm(s);
-    const float alpha = out[0];
 #pragma unroll
     for (int u = 0; u < CGM_U; ++u) {
         const int f = blockIdx.x * CGM_WG + u * CGM_T + threadIdx.x;
@@ -523,6 +523,50 @@ __global__ void __launch_bounds__(CGM_T) k_npgm_apply(mjrl_shape s, const float*
         packed_new[p1] = v;
         if (p2 >= 0) packed_new[p2] = v;
     }
+}
+
+__global__ void __launch_bounds__(CGM_T) k_npgm_apply(mjrl_shape s, const float* __restrict__ x,
+                                                      const float* __restrict__ theta, float min_ls,
+                                                      float* __restrict__ theta_new, float* __restrict__ packed_new,
+                                                      const float* __restrict__ out) {
+    apply_step(s, x, theta, min_ls, out[0], theta_new, packed_new);
+}
+
+// TRPO's backtracking (trpo.py:105-118) on the device, trial k >= 1 of a line search:
+// trial k - 1's evaluation (its sums) is logged and tested (kl < kl_dist, kl =
+// float(sums[1] / T) as the host forms it); a rejected trial sets alpha_k =
+// float32(0.9) * alpha_{k-1} in f32 (numpy 2: `0.9 * np.float32`) and writes theta +
+// alpha_k x for the next evaluation, an accepted one raises *skip, so the remaining
+// speculative trials and evaluations of the launch sequence return at once, and
+// out[0] = the accepted alpha.
+// apply = 0: log and test only (the sequence's last launch).  State ls (floats):
+// [1] accepted, [2] trials logged, [8 + t] alpha_t (t >= 1; alpha_0 is out[0] of the
+// mode-0 step), [MJRL_LS_LOG + 3 t ..] trial t's (alpha, kl, surr).
+__global__ void __launch_bounds__(CGM_T) k_trpo_trial(mjrl_shape s, const float* __restrict__ x,
+                                                      const float* __restrict__ theta, float min_ls,
+                                                      float* __restrict__ theta_new, float* __restrict__ packed_new,
+                                                      float* out, const double* __restrict__ sums,
+                                                      double inv_T, double kl_dist, int k, int apply, float* ls,
+                                                      int32_t* skip) {
+    if (k > 1 && *skip) return;   // trial 1 starts the search: the flag is its to set
+    const float a_prev = k == 1 ? out[0] : ls[8 + (k - 1)];
+    const float kl = (float)(sums[1] * inv_T), surr = (float)(sums[0] * inv_T);
+    const bool acc = (double)kl < kl_dist;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        float* lg = ls + MJRL_LS_LOG + 3 * (k - 1);
+        lg[0] = a_prev;
+        lg[1] = kl;
+        lg[2] = surr;
+        ls[1] = acc ? 1.f : 0.f;
+        ls[2] = (float)k;
+        *skip = acc ? 1 : 0;
+        // the accepted alpha is the step's result (out[0], as a host step leaves it);
+        // trial 1 writes the value its other workgroups read, unchanged
+        if (acc) out[0] = a_prev;
+        if (!acc && apply) ls[8 + k] = __fmul_rn(0.9f, a_prev);
+    }
+    if (acc || !apply) return;
+    apply_step(s, x, theta, min_ls, __fmul_rn(0.9f, a_prev), theta_new, packed_new);
 }
 
 // Step size and parameter update (npg_cg.py:128-141), one workgroup (d beyond the
@@ -725,6 +769,18 @@ int mjrl_cg_update(int32_t d, const float* z, float* x, float* r, float* p, floa
     if (d < 0 || !z || !x || !r || !p || !cg || !done) return MJRL_EINVAL;
     hipLaunchKernelGGL(k_cg_update, dim3(1), dim3(CG_THREADS), 0, (hipStream_t)stream, d, z, x, r, p, cg, done,
                        residual_tol);
+    return err(hipGetLastError());
+}
+
+int mjrl_trpo_trial(const mjrl_shape* s, const float* x, const float* theta, float min_log_std, float* theta_new,
+                    float* packed_new, float* out, const double* sums, double inv_T, double kl_dist, int32_t k,
+                    int32_t apply, float* ls, int32_t* skip, void* stream) {
+    if (!s || !x || !theta || !theta_new || !packed_new || !out || !sums || !ls || !skip || k < 1 ||
+        k + 8 >= MJRL_LS_LOG || MJRL_LS_LOG + 3 * k > MJRL_LS_STATE)
+        return MJRL_EINVAL;
+    const int nwg = (s->d + CGM_WG - 1) / CGM_WG;
+    hipLaunchKernelGGL(k_trpo_trial, dim3(nwg > 0 ? nwg : 1), dim3(CGM_T), 0, (hipStream_t)stream, *s, x, theta,
+                       min_log_std, theta_new, packed_new, out, sums, inv_T, kl_dist, (int)k, (int)apply, ls, skip);
     return err(hipGetLastError());
 }
 

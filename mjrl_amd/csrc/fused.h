@@ -292,7 +292,9 @@ __device__ __forceinline__ void fused_body(const RowArgs& a, const FOut& o) {
     }
     // a converged CG loop (cg_solve.py:19-20): checked once the preamble's loads have
     // been consumed, so the flag's load overlaps them
-    if (MODE == FVP && a.done && *a.done) return;
+    // FVP: a converged CG loop (cg_solve.py:19-20); EVAL: a TRPO trial the device line
+    // search no longer needs (mjrl_policy_eval_if)
+    if ((MODE == FVP || MODE == EVAL) && a.done && *a.done) return;
 
     KX_STAMP(15);
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {

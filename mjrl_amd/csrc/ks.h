@@ -123,7 +123,9 @@ __global__ void __launch_bounds__(KT, 1) k_ks(RowArgs a, FOut o) {
     float* sW2 = smem + L::oW2;
     float* sdW2 = smem + L::odW2;
 
-    if (MODE == FVP && a.done && *a.done) return;
+    // FVP: a converged CG loop (cg_solve.py:19-20); EVAL: a TRPO trial the device line
+    // search no longer needs (mjrl_policy_eval_if)
+    if ((MODE == FVP || MODE == EVAL) && a.done && *a.done) return;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int r16 = lane & 15, q = lane >> 4;
     const int cb = w & 3, kh = w >> 2;

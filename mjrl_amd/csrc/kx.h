@@ -438,7 +438,9 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
     }
     // a converged CG loop (cg_solve.py:19-20): checked once the preamble's loads have
     // been consumed (image stores, W0 slice split), so the flag's load overlaps them
-    if (MODE == FVP && a.done && *a.done) return;
+    // FVP: a converged CG loop (cg_solve.py:19-20); EVAL: a TRPO trial the device line
+    // search no longer needs (mjrl_policy_eval_if)
+    if ((MODE == FVP || MODE == EVAL) && a.done && *a.done) return;
 
     floatx4 g0[KG];
 #pragma unroll

@@ -291,7 +291,9 @@ __global__ void __launch_bounds__((Layout<H0, H1, MP>::NT), (Layout<H0, H1, MP>:
     float* GPs = smem + L::oGP;
     float* XS = smem + L::oXS;
 
-    if (MODE == FVP && a.done && *a.done) return;
+    // FVP: a converged CG loop (cg_solve.py:19-20); EVAL: a TRPO trial the device line
+    // search no longer needs (mjrl_policy_eval_if)
+    if ((MODE == FVP || MODE == EVAL) && a.done && *a.done) return;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int r16 = lane & 15, q = lane >> 4;
     const int np = a.np, m = a.m;
@@ -1137,7 +1139,9 @@ __global__ void __launch_bounds__(64 * GATHER_WAVES) k_gather_flat(const float* 
     }
 }
 
-__global__ void __launch_bounds__(64) k_eval_final(const double* __restrict__ rpart, int G, double* __restrict__ sums) {
+__global__ void __launch_bounds__(64) k_eval_final(const double* __restrict__ rpart, int G, double* __restrict__ sums,
+                                                   const int32_t* __restrict__ skip) {
+    if (skip && *skip) return;
     // one wave: lane l folds partials l, l+64, ... in order, then a fixed shuffle tree
     double s = 0.0, k = 0.0;
     for (int b = threadIdx.x; b < G; b += 64) {
@@ -1645,7 +1649,11 @@ int mjrl_scratch_size(const mjrl_shape* s, int64_t T, int64_t* wpart_floats, int
     // k_wgrad_all's slice count is not monotonic in T (equal tile counts per slice):
     // size for its cap, so a scratch sized for T holds every pass over T' <= T rows
     if (T > 0 && wall_supported(s) && wall_cap(s) > S) S = wall_cap(s);
-    if (ks_grid(T) > S) S = ks_grid(T);
+    // ks_grid balances tiles per workgroup and is not monotonic in T (8192 tiles:
+    // 256 workgroups, 8224: 129): size for its cap, min(tiles, FGRID_CAP)
+    const int64_t nt = (T + 31) / 32;
+    const int kcap = (int)(nt < 1 ? 1 : (nt < FGRID_CAP ? nt : FGRID_CAP));
+    if (kcap > S) S = kcap;
     *slices = S;
     *wpart_floats = slab_floats(s, S);
     const int64_t rp = (int64_t)ROW_GRID_CAP * (s->mp > 2 ? s->mp : 2);
@@ -1767,9 +1775,28 @@ int mjrl_fused_path(const mjrl_shape* s) { return s ? acc_path(s, 1) : 0; }
 
 int mjrl_split_supported(const mjrl_shape* s) { return s && ksx_supported(s) ? 1 : 0; }
 
+static int policy_eval(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_eval, const float* packed_theta_new,
+                       const float* packed_theta_old, const float* out_shift, const float* out_scale,
+                       const mjrl_scratch* sc, double* sums, const int32_t* skip, void* stream);
+
 int mjrl_policy_eval(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_eval, const float* packed_theta_new,
                      const float* packed_theta_old, const float* out_shift, const float* out_scale,
                      const mjrl_scratch* sc, double* sums, void* stream) {
+    return policy_eval(s, rows, T_eval, packed_theta_new, packed_theta_old, out_shift, out_scale, sc, sums, nullptr,
+                       stream);
+}
+
+int mjrl_policy_eval_if(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_eval, const float* packed_theta_new,
+                        const float* packed_theta_old, const float* out_shift, const float* out_scale,
+                        const mjrl_scratch* sc, double* sums, const int32_t* skip, void* stream) {
+    if (!skip) return MJRL_EINVAL;
+    return policy_eval(s, rows, T_eval, packed_theta_new, packed_theta_old, out_shift, out_scale, sc, sums, skip,
+                       stream);
+}
+
+static int policy_eval(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_eval, const float* packed_theta_new,
+                       const float* packed_theta_old, const float* out_shift, const float* out_scale,
+                       const mjrl_scratch* sc, double* sums, const int32_t* skip, void* stream) {
     if (!rows_ok(s, rows) || !packed_theta_new || !packed_theta_old || !sc || !sums || T_eval < 0 ||
         T_eval > rows->T || !rows->adv || !rows->mu0 || !rows->ll0)
         return MJRL_EINVAL;
@@ -1781,6 +1808,7 @@ int mjrl_policy_eval(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_eval,
     ra.out_shift = out_shift;
     ra.out_scale = out_scale;
     ra.rpart = sc->rpart;
+    ra.done = skip;   // EVAL: the whole pass is skipped while *skip != 0
     // forward-only: the K-split kernel in EVAL mode where it applies, else the row kernel
     const bool ks = ks_supported(s);
     const int G = ks ? ks_grid(T_eval) : row_grid(s, T_eval);
@@ -1790,7 +1818,7 @@ int mjrl_policy_eval(const mjrl_shape* s, const mjrl_rows* rows, int64_t T_eval,
     } else {
         hipMemsetAsync(sc->rpart, 0, sizeof(double) * 2 * G, st);
     }
-    hipLaunchKernelGGL(k_eval_final, dim3(1), dim3(64), 0, st, sc->rpart, G, sums);
+    hipLaunchKernelGGL(k_eval_final, dim3(1), dim3(64), 0, st, sc->rpart, G, sums, skip);
     return (int)hipGetLastError();
 }
 

@@ -612,6 +612,7 @@ class DeviceBatch:
 # the forward pass assembles the split rows itself where it can (UpdateEngine._fused_pack)
 FUSED_PACK = os.environ.get("MJRL_AMD_FUSED_PACK", "1") != "0"
 SMALL_MOMENTS_ROWS = 65_536   # one-workgroup moments + whitening (mjrl_moments_whiten_small) up to this many rows
+TRPO_DEVICE_TRIALS = int(os.environ.get("MJRL_AMD_TRPO_DEVICE_TRIALS", "4"))   # see UpdateEngine.trpo_device_trials
 GRAPH_AUTO_ROWS = 300_000   # UpdateEngine.graphs == "auto": replay graphs up to this many rows (125k-row shard: 2.03 -> 1.97 ms; 1M rows: eager 4 % faster)
 HIDDEN_WIDTHS = (32, 64, 128, 256)   # hidden widths the row kernels are built for
 
@@ -699,6 +700,11 @@ class UpdateEngine:
         self.mom2_part = torch.zeros(_lib.MOM_SCRATCH, dtype=torch.float64, device=dev)   # one-launch moments
         self.transforms = (None, None, None, None)
         self._act_rows = None   # set per update: the batch's f32 actions when the row passes read them in place
+        # the device TRPO line search: trials per launch sequence (0: the host loop only),
+        # its state (MJRL_LS_STATE floats) and skip flag
+        self.trpo_device_trials = TRPO_DEVICE_TRIALS
+        self.ls_state = torch.zeros(_lib.LS_STATE, **f32)
+        self.ls_skip = torch.zeros(1, dtype=torch.int32, device=dev)
         # sharded schedule (one rank of several, or a one-rank communicator forced
         # onto it): moments through one all-gather + mjrl_moments_combine, an
         # all-reduce between every FVP's gather and its CG step
@@ -1233,6 +1239,22 @@ class UpdateEngine:
                 delta = 2.0 * kl_dist
                 self._step(plan, 0, delta, 0.0, 0)
             self._evaluate(plan)
+            if algo == "trpo" and self.trpo_device_trials > 0 and not self.sharded:
+                # the first backtracking trials on the device (mjrl_trpo_trial): each
+                # tests the last evaluation and, rejected, steps to 0.9 alpha for the
+                # next; once one is accepted the rest return at once.  No host round
+                # trip per trial, and the whole sequence is part of the captured graph;
+                # the host continues past it only when all are rejected (_trpo_search)
+                K = int(self.trpo_device_trials)
+                for k in range(1, K + 2):
+                    _lib.check(L.mjrl_trpo_trial(sp, _lib.ptr(x), _lib.ptr(theta), self.min_log_std,
+                                                 _lib.ptr(v["theta_new"]), _lib.ptr(self.packed_new),
+                                                 _lib.ptr(self.out), C.c_void_p(self.stats[S_EVAL:].data_ptr()),
+                                                 inv_T, float(kl_dist), k, int(k <= K), _lib.ptr(self.ls_state),
+                                                 _lib.ptr(self.ls_skip), st), "mjrl_trpo_trial")
+                    if k <= K:
+                        self._evaluate(plan, skip=self.ls_skip)
+                plan["dev_trials"] = K
             if algo != "trpo":
                 timing[3].record()
             return plan, delta, timing
@@ -1256,11 +1278,19 @@ class UpdateEngine:
                                    self.min_log_std, _lib.ptr(self.pvec["theta_new"]), _lib.ptr(self.packed_new),
                                    _lib.ptr(self.out), _lib.stream_ptr()), "mjrl_npg_step")
 
-    def _evaluate(self, plan):
+    def _evaluate(self, plan, skip=None):
         """Surrogate and KL at theta_new (npg_cg.py:142-143): one EVAL pass, then
         (sharded) the all-reduce of its sums; the first one carries surr_before's
-        moments too."""
+        moments too.  skip: a device flag that turns the pass into a no-op (the
+        device line search's speculative evaluations; one process only)."""
         L = self.lib
+        if skip is not None:
+            _lib.check(L.mjrl_policy_eval_if(C.byref(self.shape), C.byref(plan["rows"]), plan["T"],
+                                             _lib.ptr(self.packed_new), _lib.ptr(self.packed_theta),
+                                             _lib.ptr(plan["osh"]), _lib.ptr(plan["osc"]), C.byref(plan["sc"]),
+                                             C.c_void_p(self.stats[S_EVAL:].data_ptr()), _lib.ptr(skip),
+                                             _lib.stream_ptr()), "mjrl_policy_eval_if")
+            return
         _lib.check(L.mjrl_policy_eval(C.byref(self.shape), C.byref(plan["rows"]), plan["T"],
                                       _lib.ptr(self.packed_new), _lib.ptr(self.packed_theta), _lib.ptr(plan["osh"]),
                                       _lib.ptr(plan["osc"]), C.byref(plan["sc"]),
@@ -1273,25 +1303,50 @@ class UpdateEngine:
             self._reduce_stats(S_EVAL, S_EVAL + 2)
 
     def _trpo_search(self, plan, delta, kl_dist, verbose, timing):
-        """TRPO's KL backtracking on the host (trpo.py:98-124) after the first
-        evaluation: alpha *= 0.9 while KL >= kl_dist (at most 100 trials), then the
-        final re-evaluation at the accepted alpha.  The step and the evaluation
-        launch on the current stream (eager, or after a graph replay of everything
-        before)."""
+        """TRPO's KL backtracking (trpo.py:98-124) after the first evaluation: alpha
+        *= 0.9 while KL >= kl_dist (at most 100 trials), then the final
+        re-evaluation at the accepted alpha.  The first trpo_device_trials trials
+        ran on the device inside the update's launch sequence (mjrl_trpo_trial): one
+        readback of their log here; the host loop takes over only past them (the
+        step and the evaluation launch on the current stream, eager, or after a graph
+        replay of everything before)."""
         trials = []
         inv_T = plan["inv_T"]
-        res = self.stats[S_EVAL:S_EVAL + 2].cpu().numpy()
-        alpha = np.float32(self.out[0].item())
         surr_before = float(self.stats[S_MS].item() / self.stats[S_MS + 2].item())
-        for k in range(100):
+
+        def backtrack_msg(kl, surr):
+            if verbose:
+                print("Step size too high. Backtracking. | kl = %f | surr diff = %f" % (kl, surr - surr_before))
+
+        K = plan.get("dev_trials", 0)
+        k0 = 0
+        if K:
+            ls = self.ls_state.cpu().numpy()
+            n, accepted = int(ls[2]), bool(ls[1])
+            for t in range(n):
+                a, kl, surr = (np.float32(v) for v in ls[_lib.LS_LOG + 3 * t: _lib.LS_LOG + 3 * t + 3])
+                trials.append((float(a), float(kl), float(surr)))
+                if not (accepted and t == n - 1):
+                    backtrack_msg(kl, surr)
+            if accepted:
+                timing[3].record()
+                return trials
+            # every device trial rejected: the host steps on from the last one
+            alpha = np.float32(0.9 * np.float32(trials[-1][0]))   # trpo.py:114 (python float * np.float32)
+            self._step(plan, 1, delta, alpha, 0)
+            self._evaluate(plan)
+            k0 = n
+        else:
+            alpha = np.float32(self.out[0].item())
+        res = self.stats[S_EVAL:S_EVAL + 2].cpu().numpy()
+        for k in range(k0, 100):
             kl = np.float32(res[1] * inv_T)
             surr = np.float32(res[0] * inv_T)
             trials.append((float(alpha), float(kl), float(surr)))
             if kl < kl_dist:
                 break
             alpha = np.float32(0.9 * alpha)   # trpo.py:114 (python float * np.float32)
-            if verbose:
-                print("Step size too high. Backtracking. | kl = %f | surr diff = %f" % (kl, surr - surr_before))
+            backtrack_msg(kl, surr)
             if k == 99:
                 alpha = np.float32(0.0)
                 break

@@ -535,36 +535,39 @@ __global__ void __launch_bounds__(64 * GAE_WAVES) k_gae(const double* __restrict
 }
 
 // Lanes = paths (round 6): the serial recurrences of LP_PATHS paths run side by side
-// in ONE instruction stream each, one wave per chain — wave 0 the returns
-// (discount_sum(rewards, gamma)), wave 1 the advantages (discount_sum(td, gamma
-// lambda), or nothing without GAE), wave 2 the path-return sum (front to back) —
-// each lane one path; wave 3 only loads and stores.  A dependent fp64 multiply -> add costs ~10 cycles of issue
-// per step for the whole wave (tools/gae_latency.hip), so LP_PATHS paths advance for the
-// price k_gae paid for one.  The paths' steps come through LDS in windows of LP_W
-// steps per path (backward windows aligned at each path's end, forward windows at
-// its start): all four waves load window j + 1 into registers (each instruction 8
-// paths' runs of 8 consecutive steps) while the chains consume window j, then store it (td formed on
-// the way) after a barrier; the chains write their outputs in place, and the
-// window leaves for HBM with coalesced writes.  Bit-identical to k_gae: the same
-// __dmul_rn / __dadd_rn / __dsub_rn per step in the same order.
+// in ONE instruction stream each, one wave per chain, each lane one path — wave 0
+// the returns (discount_sum(rewards, gamma)), wave 1 the advantages (discount_sum(td,
+// gamma lambda), idle without GAE), wave 2 the path-return sum (front to back).  A
+// dependent fp64 multiply -> add costs ~10 cycles of issue per step for the whole
+// wave, however many lanes are on (profiles/r06b/gae_latency.txt), so LP_PATHS paths
+// advance for the price one did.  The chain waves touch LDS only: the steps come
+// through two LDS buffers in windows of LP_W steps per path (backward windows
+// aligned at each path's end, forward windows at its start), and four mover waves
+// (3..6) do all the global traffic — while the chains consume window j from one
+// buffer, the movers drain window j - 1's outputs from the other (coalesced
+// stores), put window j + 1 there (td formed on the way) and issue window j + 2's
+// loads.  One barrier per window; a chain wave never waits on HBM.  Bit-identical
+// to k_gae: the same __dmul_rn / __dadd_rn / __dsub_rn per step in the same order.
 constexpr int LP_PATHS = 8;               // paths per workgroup (lanes 0..7 of each chain wave)
-constexpr int LP_W = 512;                 // steps per window: a window's chain (~2.5 us) covers the
-                                          // HBM latency of the next window's loads (128-step windows of
-                                          // 32 paths waited ~5 us a window on them, r06b/gae_probe.txt)
+constexpr int LP_W = 256;                 // steps per window (a window's chain ~2-3 us covers the next loads)
 constexpr int LP_LD = LP_W + 1;           // LDS row stride (doubles): chain lanes conflict-free
 constexpr int LP_GB = 16;                 // chain steps per register batch
-constexpr int LP_T = 256;                 // 4 waves: three chain waves, all four load / store
-constexpr int LP_PER = LP_PATHS * LP_W / LP_T;   // window elements per thread per array
-static_assert(LP_PATHS * LP_W % LP_T == 0 && LP_W % 64 == 0, "window split");
+constexpr int LP_CH = 3;                  // chain waves 0..2
+constexpr int LP_MV = 256;                // mover threads (waves 3..6)
+constexpr int LP_T = 64 * LP_CH + LP_MV;
+constexpr int LP_TPP = LP_MV / LP_PATHS;  // mover threads a path: runs of LP_TPP consecutive steps a load
+constexpr int LP_PER = LP_W / LP_TPP;     // window elements per mover thread per array
+constexpr int LP_BUF = LP_PATHS * LP_LD;  // one array of one buffer (doubles)
+static_assert(LP_W % LP_TPP == 0 && LP_W % LP_GB == 0, "window split");
 
 __global__ void __launch_bounds__(LP_T) k_gae_lp(const double* __restrict__ rew, const double* __restrict__ base,
                                                  const int64_t* __restrict__ off, const uint8_t* __restrict__ term,
                                                  int64_t P, double gamma, double gl, int use_gae,
                                                  double* __restrict__ ret, double* __restrict__ adv,
                                                  double* __restrict__ path_ret) {
-    __shared__ double RB[LP_PATHS * LP_LD];   // backward rewards -> returns (in place)
-    __shared__ double TD[LP_PATHS * LP_LD];   // td -> advantages (in place); no GAE: the baseline
-    __shared__ double RF[LP_PATHS * LP_LD];   // forward rewards
+    // buffer q of array A at A + q * LP_BUF: RB backward rewards -> returns (in place),
+    // TD td -> advantages (in place; no GAE: the baseline), RF forward rewards
+    __shared__ double RB[2 * LP_BUF], TD[2 * LP_BUF], RF[2 * LP_BUF];
     __shared__ int64_t sb[LP_PATHS], se[LP_PATHS];
     __shared__ double sbl[LP_PATHS];          // b1's last entry: 0 if terminated else b[-1]
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -581,14 +584,74 @@ __global__ void __launch_bounds__(LP_T) k_gae_lp(const double* __restrict__ rew,
     int64_t hmax = 0;
     for (int i = 0; i < np; ++i) hmax = se[i] - sb[i] > hmax ? se[i] - sb[i] : hmax;
     const int nwin = (int)((hmax + LP_W - 1) / LP_W);
-    // this thread's path (LP_TPP threads a path) and its steps u = mu + LP_TPP k of every
-    // window: each load instruction reads runs of LP_TPP consecutive steps
-    constexpr int LP_TPP = LP_T / LP_PATHS;
-    const int mp = tid / LP_TPP, mu = tid % LP_TPP;
-    // an empty path (or a lane past the last path) reads index 0: valid whenever a
+    if (w < LP_CH) {
+        // ---- a chain wave: LDS only ----
+        const bool chain = lane < np && (w != 1 || use_gae);
+        const double c = w == 0 ? gamma : gl;
+        double* const cw = (w == 0 ? RB : (w == 1 ? TD : RF)) + lane * LP_LD;
+        double acc = 0.0;
+        __syncthreads();   // window 0 put
+        for (int j = 0; j < nwin; ++j) {
+            if (chain) {
+                // the steps come into registers in batches of LP_GB (the next batch's
+                // LDS reads issued before this batch's serial steps), so only the
+                // dependent multiply -> add is on the critical path
+                double* const row = cw + (j & 1) * LP_BUF;
+                double x[LP_GB], xn2[LP_GB];
+                if (w == 2) {
+                    // front to back: Python's sum(p["rewards"]) (npg_cg.py:97); x + 1.0 * acc
+                    // is x + acc exactly (k_gae's form); steps past the path's end hold 0.0
+#pragma unroll
+                    for (int g = 0; g < LP_GB; ++g) x[g] = row[g];
+#pragma unroll
+                    for (int u0 = 0; u0 < LP_W; u0 += LP_GB) {
+                        if (u0 + LP_GB < LP_W) {
+#pragma unroll
+                            for (int g = 0; g < LP_GB; ++g) xn2[g] = row[u0 + LP_GB + g];
+                        }
+#pragma unroll
+                        for (int g = 0; g < LP_GB; ++g) acc = __dadd_rn(x[g], acc);
+#pragma unroll
+                        for (int g = 0; g < LP_GB; ++g) x[g] = xn2[g];
+                    }
+                } else {
+                    // backward over the whole window with no step mask: a partial window
+                    // (the path's first steps) holds its valid steps at u >= W - left,
+                    // which the chain meets first; what it computes below them is never
+                    // drained, and the path's chain ends there
+#pragma unroll
+                    for (int g = 0; g < LP_GB; ++g) x[g] = row[LP_W - LP_GB + g];
+#pragma unroll
+                    for (int u0 = LP_W - LP_GB; u0 >= 0; u0 -= LP_GB) {
+                        if (u0 >= LP_GB) {
+#pragma unroll
+                            for (int g = 0; g < LP_GB; ++g) xn2[g] = row[u0 - LP_GB + g];
+                        }
+#pragma unroll
+                        for (int g = LP_GB - 1; g >= 0; --g) {
+                            acc = __dadd_rn(x[g], __dmul_rn(c, acc));
+                            x[g] = acc;
+                        }
+#pragma unroll
+                        for (int g = 0; g < LP_GB; ++g) row[u0 + g] = x[g];
+#pragma unroll
+                        for (int g = 0; g < LP_GB; ++g) x[g] = xn2[g];
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        if (w == 2 && lane < np) path_ret[p0 + lane] = acc;
+        return;
+    }
+    // ---- a mover: all global loads and stores ----
+    const int m = tid - 64 * LP_CH;
+    const int mp = m / LP_TPP, mu = m % LP_TPP;
+    // an empty path (or a thread past the last path) reads index 0: valid whenever a
     // window exists, and never used (the chains and the drain skip its steps)
     const int64_t pb = se[mp] > sb[mp] ? sb[mp] : 0, pe = se[mp] > sb[mp] ? se[mp] : 1;
     const double pbl = sbl[mp];
+    const int64_t db = sb[mp], de = se[mp], plen = de - db;
     double xr[LP_PER], xb[LP_PER], xn[LP_PER], xf[LP_PER];
     auto load = [&](int j) {
         // backward window: step t = e - (j + 1) W + u; forward window: t = b + j W + u;
@@ -607,33 +670,153 @@ __global__ void __launch_bounds__(LP_T) k_gae_lp(const double* __restrict__ rew,
         }
     };
     auto put = [&](int j) {
+        const int q = (j & 1) * LP_BUF + mp * LP_LD;
 #pragma unroll
         for (int k = 0; k < LP_PER; ++k) {
             const int u = mu + LP_TPP * k;
             const int64_t tb = pe - (int64_t)(j + 1) * LP_W + u;
             const double bn = tb + 1 < pe ? xn[k] : pbl;   // b1[t + 1] (process_samples.py:24-27)
-            RB[mp * LP_LD + u] = xr[k];
+            RB[q + u] = xr[k];
             // GAE td = r + gamma * b1[t+1] - b1[t] (process_samples.py:28); plain: b
-            TD[mp * LP_LD + u] = use_gae ? __dsub_rn(__dadd_rn(xr[k], __dmul_rn(gamma, bn)), xb[k]) : xb[k];
-            RF[mp * LP_LD + u] = xf[k];
+            TD[q + u] = use_gae ? __dsub_rn(__dadd_rn(xr[k], __dmul_rn(gamma, bn)), xb[k]) : xb[k];
+            // past the path's end: 0.0, which the forward sum adds exactly (acc is never -0.0)
+            RF[q + u] = (int64_t)j * LP_W + u < plen ? xf[k] : 0.0;
         }
     };
-    const int64_t db = sb[mp], de = se[mp];
-    auto drain = [&](int j) {   // window j's outputs (in RB / TD) to HBM
+    auto drain = [&](int j) {   // window j's outputs (in RB / TD of its buffer) to HBM
+        const int q = (j & 1) * LP_BUF + mp * LP_LD;
 #pragma unroll
         for (int k = 0; k < LP_PER; ++k) {
             const int u = mu + LP_TPP * k;
             const int64_t tb = de - (int64_t)(j + 1) * LP_W + u;
             if (tb >= db) {
-                const double rr = RB[mp * LP_LD + u];
+                const double rr = RB[q + u];
                 ret[tb] = rr;
-                adv[tb] = use_gae ? TD[mp * LP_LD + u] : __dsub_rn(rr, TD[mp * LP_LD + u]);   // plain: ret - b
+                adv[tb] = use_gae ? TD[q + u] : __dsub_rn(rr, TD[q + u]);   // plain: ret - b
+            }
+        }
+    };
+    if (nwin > 0) {
+        load(0);
+        put(0);
+    }
+    if (nwin > 1) load(1);
+    __syncthreads();   // window 0 put
+    for (int j = 0; j < nwin; ++j) {
+        // the chains run window j (buffer j & 1); the other buffer holds window j - 1
+        if (j >= 1) drain(j - 1);
+        if (j + 1 < nwin) put(j + 1);
+        if (j + 2 < nwin) load(j + 2);
+        __syncthreads();
+    }
+    if (nwin > 0) drain(nwin - 1);
+}
+
+#ifdef MJRL_GAE_LP4
+// Variant build only (-DMJRL_GAE_LP4, tools/gae_probe.py A/B): the first lanes-=-paths
+// kernel of round 6, in which all four waves load and store.
+// Lanes = paths (round 6): the serial recurrences of L4_PATHS paths run side by side
+// in ONE instruction stream each, one wave per chain — wave 0 the returns
+// (discount_sum(rewards, gamma)), wave 1 the advantages (discount_sum(td, gamma
+// lambda), or nothing without GAE), wave 2 the path-return sum (front to back) —
+// each lane one path; wave 3 only loads and stores.  A dependent fp64 multiply -> add costs ~10 cycles of issue
+// per step for the whole wave (tools/gae_latency.hip), so L4_PATHS paths advance for the
+// price k_gae paid for one.  The paths' steps come through LDS in windows of L4_W
+// steps per path (backward windows aligned at each path's end, forward windows at
+// its start): all four waves load window j + 1 into registers (each instruction 8
+// paths' runs of 8 consecutive steps) while the chains consume window j, then store it (td formed on
+// the way) after a barrier; the chains write their outputs in place, and the
+// window leaves for HBM with coalesced writes.  Bit-identical to k_gae: the same
+// __dmul_rn / __dadd_rn / __dsub_rn per step in the same order.
+constexpr int L4_PATHS = 8;               // paths per workgroup (lanes 0..7 of each chain wave)
+constexpr int L4_W = 256;                 // steps per window: a window's chain covers the HBM latency
+                                          // of the next window's loads; 512-step windows held 64 loads a
+                                          // thread, more than the registers beside the chain (the chain
+                                          // then waited on half of them, r06c/gae_probe.txt)
+constexpr int L4_LD = L4_W + 1;           // LDS row stride (doubles): chain lanes conflict-free
+constexpr int L4_GB = 16;                 // chain steps per register batch
+constexpr int L4_T = 256;                 // 4 waves: three chain waves, all four load / store
+constexpr int L4_PER = L4_PATHS * L4_W / L4_T;   // window elements per thread per array
+static_assert(L4_PATHS * L4_W % L4_T == 0 && L4_W % 64 == 0, "window split");
+
+__global__ void __launch_bounds__(L4_T) k_gae_lp4(const double* __restrict__ rew, const double* __restrict__ base,
+                                                 const int64_t* __restrict__ off, const uint8_t* __restrict__ term,
+                                                 int64_t P, double gamma, double gl, int use_gae,
+                                                 double* __restrict__ ret, double* __restrict__ adv,
+                                                 double* __restrict__ path_ret) {
+    __shared__ double RB[L4_PATHS * L4_LD];   // backward rewards -> returns (in place)
+    __shared__ double TD[L4_PATHS * L4_LD];   // td -> advantages (in place); no GAE: the baseline
+    __shared__ double RF[L4_PATHS * L4_LD];   // forward rewards
+    __shared__ int64_t sb[L4_PATHS], se[L4_PATHS];
+    __shared__ double sbl[L4_PATHS];          // b1's last entry: 0 if terminated else b[-1]
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int64_t p0 = (int64_t)blockIdx.x * L4_PATHS;
+    const int np = (int)(P - p0 < L4_PATHS ? P - p0 : L4_PATHS);
+    if (tid < L4_PATHS) {
+        const bool ok = tid < np;
+        const int64_t b = ok ? off[p0 + tid] : 0, e = ok ? off[p0 + tid + 1] : 0;
+        sb[tid] = b;
+        se[tid] = e;
+        sbl[tid] = e > b ? (term[p0 + tid] ? 0.0 : base[e - 1]) : 0.0;
+    }
+    __syncthreads();
+    int64_t hmax = 0;
+    for (int i = 0; i < np; ++i) hmax = se[i] - sb[i] > hmax ? se[i] - sb[i] : hmax;
+    const int nwin = (int)((hmax + L4_W - 1) / L4_W);
+    // this thread's path (L4_TPP threads a path) and its steps u = mu + L4_TPP k of every
+    // window: each load instruction reads runs of L4_TPP consecutive steps
+    constexpr int L4_TPP = L4_T / L4_PATHS;
+    const int mp = tid / L4_TPP, mu = tid % L4_TPP;
+    // an empty path (or a lane past the last path) reads index 0: valid whenever a
+    // window exists, and never used (the chains and the drain skip its steps)
+    const int64_t pb = se[mp] > sb[mp] ? sb[mp] : 0, pe = se[mp] > sb[mp] ? se[mp] : 1;
+    const double pbl = sbl[mp];
+    const int64_t plen = se[mp] - sb[mp];
+    double xr[L4_PER], xb[L4_PER], xn[L4_PER], xf[L4_PER];
+    auto load = [&](int j) {
+        // backward window: step t = e - (j + 1) W + u; forward window: t = b + j W + u;
+        // loads from clamped indices, unconditional (no exec-masked loads in the stream)
+#pragma unroll
+        for (int k = 0; k < L4_PER; ++k) {
+            const int u = mu + L4_TPP * k;
+            int64_t tb = pe - (int64_t)(j + 1) * L4_W + u, tf = pb + (int64_t)j * L4_W + u;
+            tb = tb < pb ? pb : tb;
+            tf = tf < pe ? tf : pe - 1;
+            const int64_t tn = tb + 1 < pe ? tb + 1 : pe - 1;
+            xr[k] = rew[tb];
+            xb[k] = base[tb];
+            xn[k] = base[tn];
+            xf[k] = rew[tf];
+        }
+    };
+    auto put = [&](int j) {
+#pragma unroll
+        for (int k = 0; k < L4_PER; ++k) {
+            const int u = mu + L4_TPP * k;
+            const int64_t tb = pe - (int64_t)(j + 1) * L4_W + u;
+            const double bn = tb + 1 < pe ? xn[k] : pbl;   // b1[t + 1] (process_samples.py:24-27)
+            RB[mp * L4_LD + u] = xr[k];
+            // GAE td = r + gamma * b1[t+1] - b1[t] (process_samples.py:28); plain: b
+            TD[mp * L4_LD + u] = use_gae ? __dsub_rn(__dadd_rn(xr[k], __dmul_rn(gamma, bn)), xb[k]) : xb[k];
+            // past the path's end: 0.0, which the forward sum adds exactly (acc is never -0.0)
+            RF[mp * L4_LD + u] = (int64_t)j * L4_W + u < plen ? xf[k] : 0.0;
+        }
+    };
+    const int64_t db = sb[mp], de = se[mp];
+    auto drain = [&](int j) {   // window j's outputs (in RB / TD) to HBM
+#pragma unroll
+        for (int k = 0; k < L4_PER; ++k) {
+            const int u = mu + L4_TPP * k;
+            const int64_t tb = de - (int64_t)(j + 1) * L4_W + u;
+            if (tb >= db) {
+                const double rr = RB[mp * L4_LD + u];
+                ret[tb] = rr;
+                adv[tb] = use_gae ? TD[mp * L4_LD + u] : __dsub_rn(rr, TD[mp * L4_LD + u]);   // plain: ret - b
             }
         }
     };
     // the chains: wave 0 returns, wave 1 advantages, wave 2 the path-return sum
     const bool chain = w < 3 && lane < np && (w != 1 || use_gae);
-    const int64_t H = lane < LP_PATHS ? se[lane < np ? lane : 0] - sb[lane < np ? lane : 0] : 0;
     const double c = w == 0 ? gamma : gl;
     double* cw = w == 0 ? RB : (w == 1 ? TD : RF);
     double acc = 0.0;
@@ -645,59 +828,50 @@ __global__ void __launch_bounds__(LP_T) k_gae_lp(const double* __restrict__ rew,
     for (int j = 0; j < nwin; ++j) {
         if (j + 1 < nwin) load(j + 1);   // in flight under the chains
         if (chain) {
-            // the window's steps come into registers in batches of LP_GB (the next
+            // the window's steps come into registers in batches of L4_GB (the next
             // batch's LDS reads issued before this batch's serial steps), so only the
             // dependent fp64 multiply -> add is on the critical path
-            double* row = cw + lane * LP_LD;
-            const int64_t s0 = (int64_t)j * LP_W;
-            const int64_t left = H - s0;   // this path's steps from this window on
-            if (w == 2 && left >= LP_W) {
+            double* row = cw + lane * L4_LD;
+            if (w == 2) {
                 // front to back: Python's sum(p["rewards"]) (npg_cg.py:97); x + 1.0 * acc is
-                // x + acc exactly (k_gae's form)
-                double x[LP_GB], xn2[LP_GB];
+                // x + acc exactly (k_gae's form); the steps past the path's end hold 0.0
+                double x[L4_GB], xn2[L4_GB];
 #pragma unroll
-                for (int g = 0; g < LP_GB; ++g) x[g] = row[g];
+                for (int g = 0; g < L4_GB; ++g) x[g] = row[g];
 #pragma unroll
-                for (int u0 = 0; u0 < LP_W; u0 += LP_GB) {
-                    if (u0 + LP_GB < LP_W) {
+                for (int u0 = 0; u0 < L4_W; u0 += L4_GB) {
+                    if (u0 + L4_GB < L4_W) {
 #pragma unroll
-                        for (int g = 0; g < LP_GB; ++g) xn2[g] = row[u0 + LP_GB + g];
+                        for (int g = 0; g < L4_GB; ++g) xn2[g] = row[u0 + L4_GB + g];
                     }
 #pragma unroll
-                    for (int g = 0; g < LP_GB; ++g) acc = __dadd_rn(x[g], acc);
+                    for (int g = 0; g < L4_GB; ++g) acc = __dadd_rn(x[g], acc);
 #pragma unroll
-                    for (int g = 0; g < LP_GB; ++g) x[g] = xn2[g];
+                    for (int g = 0; g < L4_GB; ++g) x[g] = xn2[g];
                 }
-            } else if (w == 2) {
-                for (int u = 0; u < (int)(left > 0 ? left : 0); ++u) acc = __dadd_rn(row[u], acc);
-            } else if (left >= LP_W) {
-                // a whole window of this path: the backward recurrence with no step mask,
-                // outputs written back in place a batch at a time
-                double x[LP_GB], xn2[LP_GB];
+            } else {
+                // the backward recurrence over the whole window with no step mask: a
+                // partial window (the path's first steps) holds its valid steps at
+                // u >= W - left, which the chain meets first; what it computes below
+                // them is never drained, and the path's chain ends there
+                double x[L4_GB], xn2[L4_GB];
 #pragma unroll
-                for (int g = 0; g < LP_GB; ++g) x[g] = row[LP_W - LP_GB + g];
+                for (int g = 0; g < L4_GB; ++g) x[g] = row[L4_W - L4_GB + g];
 #pragma unroll
-                for (int u0 = LP_W - LP_GB; u0 >= 0; u0 -= LP_GB) {
-                    if (u0 >= LP_GB) {
+                for (int u0 = L4_W - L4_GB; u0 >= 0; u0 -= L4_GB) {
+                    if (u0 >= L4_GB) {
 #pragma unroll
-                        for (int g = 0; g < LP_GB; ++g) xn2[g] = row[u0 - LP_GB + g];
+                        for (int g = 0; g < L4_GB; ++g) xn2[g] = row[u0 - L4_GB + g];
                     }
 #pragma unroll
-                    for (int g = LP_GB - 1; g >= 0; --g) {
+                    for (int g = L4_GB - 1; g >= 0; --g) {
                         acc = __dadd_rn(x[g], __dmul_rn(c, acc));
                         x[g] = acc;
                     }
 #pragma unroll
-                    for (int g = 0; g < LP_GB; ++g) row[u0 + g] = x[g];
+                    for (int g = 0; g < L4_GB; ++g) row[u0 + g] = x[g];
 #pragma unroll
-                    for (int g = 0; g < LP_GB; ++g) x[g] = xn2[g];
-                }
-            } else if (left > 0) {
-                // the path's first steps (a partial window): element u holds step
-                // t = e - (j + 1) W + u, valid for u >= W - left
-                for (int u = LP_W - 1; u >= LP_W - (int)left; --u) {
-                    acc = __dadd_rn(row[u], __dmul_rn(c, acc));
-                    row[u] = acc;
+                    for (int g = 0; g < L4_GB; ++g) x[g] = xn2[g];
                 }
             }
         }
@@ -708,6 +882,8 @@ __global__ void __launch_bounds__(LP_T) k_gae_lp(const double* __restrict__ rew,
     }
     if (w == 2 && lane < np) path_ret[p0 + lane] = acc;
 }
+
+#endif
 
 // Moments pass 1: per-block partials of sum(x-c), sum((x-c)^2), min, max.
 template <typename T>
@@ -1389,9 +1565,15 @@ int mjrl_gae(const double* rew, const double* base, const int64_t* path_off, con
         return MJRL_EINVAL;
     if (P == 0) return MJRL_OK;
     const double gl = gamma * gae_lambda;   // python: gamma*gae_lambda (process_samples.py:29)
+#ifdef MJRL_GAE_LP4
+    const int64_t g = (P + L4_PATHS - 1) / L4_PATHS;
+    hipLaunchKernelGGL(k_gae_lp4, dim3((unsigned)g), dim3(L4_T), 0, (hipStream_t)stream, rew, base, path_off,
+                       terminated, P, gamma, gl, use_gae, ret, adv, path_ret);
+#else
     const int64_t g = (P + LP_PATHS - 1) / LP_PATHS;
     hipLaunchKernelGGL(k_gae_lp, dim3((unsigned)g), dim3(LP_T), 0, (hipStream_t)stream, rew, base, path_off,
                        terminated, P, gamma, gl, use_gae, ret, adv, path_ret);
+#endif
     return err(hipGetLastError());
 }
 

@@ -306,15 +306,15 @@ def test_linear_baseline_predict_on_device():
 @pytest.mark.parametrize("use_gae", [1, 0])
 @pytest.mark.parametrize("fn", ["mjrl_gae", "mjrl_gae_wave"])
 def test_gae_kernel_ragged_many_paths(use_gae, fn):
-    """Both GAE kernels (lanes = paths, 32 paths per workgroup and 128-step
-    windows: mjrl_gae; one wave per path: mjrl_gae_wave) on 83 ragged paths
+    """Both GAE kernels (lanes = paths, 8 paths per workgroup and 256-step
+    windows: mjrl_gae; one wave per path: mjrl_gae_wave) on 86 ragged paths
     (empty, 1, window +-1, several windows, terminated or not; P not a multiple
-    of 32): bit-identical to the oracle's discount_sum chains."""
+    of 8): bit-identical to the oracle's discount_sum chains."""
     from mjrl_amd import _lib
     from oracle import npg_cpu as O
     L = _lib.lib()
     rs = np.random.RandomState(23)
-    lengths = np.concatenate([[0, 1, 2, 127, 128, 129, 255, 256, 257, 1000, 0, 3001, 640],
+    lengths = np.concatenate([[0, 1, 2, 127, 128, 129, 255, 256, 257, 1000, 0, 3001, 640, 511, 512, 513],
                               rs.randint(1, 700, size=70)])
     T = int(lengths.sum())
     rew = rs.randn(T) * 3.0
@@ -345,7 +345,7 @@ def test_gae_kernel_ragged_many_paths(use_gae, fn):
 @pytest.mark.parametrize("use_gae", [1, 0])
 def test_gae_kernel_multiwindow_bitexact(use_gae):
     """mjrl_gae through the C-ABI on paths shorter than, equal to and longer
-    than the kernel's 1024-step LDS window (and an empty path): returns,
+    than the 1024-step LDS window of rounds 1-5 (and an empty path): returns,
     advantages and per-path reward sums bit-identical to the oracle
     (process_samples.py:3-44, npg_cg.py:97)."""
     import ctypes as C

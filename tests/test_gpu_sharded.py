@@ -266,13 +266,14 @@ def test_trpo_device_line_search_equals_host(name, graph):
     """The device line search (mjrl_trpo_trial + mjrl_policy_eval_if: the first
     trials tested and stepped on the device, no host round trip per trial) against
     the host loop (trpo_device_trials = 0): the same trials (alpha, kl, surr), the
-    same parameters and statistics, bit for bit; 2 device trials so the
-    backtracking case also exercises the host continuation past them."""
+    same parameters and statistics, bit for bit. The full step is evaluated in
+    the launch and K device trials follow it, so with K = 1 the backtracking case
+    (3 trials) also exercises the host continuation past them."""
     from mjrl_amd.comm import LocalComm
     c = _case(name)
     th0 = _t(c["theta0"].astype(np.float32))
     out = {}
-    for K in (0, 2, 4):
+    for K in (0, 1, 2, 4):
         eng = _engine(c, LocalComm())
         eng.trpo_device_trials = K
         eng.graphs = graph
@@ -281,10 +282,10 @@ def test_trpo_device_line_search_equals_host(name, graph):
             r = eng.update(b, th0, **_args(c))
         out[K] = (r, eng.vec["theta_new"].cpu().numpy())
     r0, th_0 = out[0]
-    for K in (2, 4):
+    for K in (1, 2, 4):
         r, th = out[K]
         assert r["trials"] == r0["trials"], (K, r["trials"], r0["trials"])
         assert np.array_equal(th, th_0)
         assert r["alpha"] == r0["alpha"] and r["kl_dist"] == r0["kl_dist"] and r["surr_after"] == r0["surr_after"]
     if name == "c3_trpo_backtrack":
-        assert len(r0["trials"]) > 3   # past the 2-trial device sequence
+        assert len(r0["trials"]) > 2   # past the K = 1 device sequence

@@ -560,6 +560,69 @@ constexpr int LP_PER = LP_W / LP_TPP;     // window elements per mover thread pe
 constexpr int LP_BUF = LP_PATHS * LP_LD;  // one array of one buffer (doubles)
 static_assert(LP_W % LP_TPP == 0 && LP_W % LP_GB == 0, "window split");
 
+// One chain wave's pass over one LDS window row (its lane's path).
+template <bool FWD>
+__device__ __forceinline__ double lp_chain(double* __restrict__ row, double acc, double c);
+
+// Forward (the path-return sum, one add a step: slack beside the backward waves):
+// front to back, Python's sum(p["rewards"]) (npg_cg.py:97); x + 1.0 * acc is x + acc
+// exactly (k_gae's form); steps past the path's end hold 0.0.  The next batch's
+// reads are issued before this batch's adds.
+template <>
+__device__ __forceinline__ double lp_chain<true>(double* __restrict__ row, double acc, double) {
+    double x[LP_GB], xn[LP_GB];
+#pragma unroll
+    for (int g = 0; g < LP_GB; ++g) x[g] = row[g];
+#pragma unroll
+    for (int u0 = 0; u0 < LP_W; u0 += LP_GB) {
+        if (u0 + LP_GB < LP_W) {
+#pragma unroll
+            for (int g = 0; g < LP_GB; ++g) xn[g] = row[u0 + LP_GB + g];
+        }
+#pragma unroll
+        for (int g = 0; g < LP_GB; ++g) acc = __dadd_rn(x[g], acc);
+#pragma unroll
+        for (int g = 0; g < LP_GB; ++g) x[g] = xn[g];
+    }
+    return acc;
+}
+
+// Backward (returns / advantages, acc = x + c * acc, outputs written back in place)
+// over the whole window with no step mask: a partial window (the path's first steps)
+// holds its valid steps at u >= W - left, which the chain meets first; what it
+// computes below them is never drained, and the path's chain ends there.  The LDS
+// reads of batch k + 2 are issued before batch k's serial steps (two batches of LDS
+// latency covered; sched_barrier keeps the compiler from sinking them to their use),
+// so only the dependent multiply -> add is on the critical path.  Batch k: u in
+// [W - (k + 1) GB, W - k GB).
+template <>
+__device__ __forceinline__ double lp_chain<false>(double* __restrict__ row, double acc, double c) {
+    constexpr int NB = LP_W / LP_GB;
+    double X[3][LP_GB];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+#pragma unroll
+        for (int g = 0; g < LP_GB; ++g) X[k][g] = row[LP_W - (k + 1) * LP_GB + g];
+    }
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+        if (k + 2 < NB) {
+#pragma unroll
+            for (int g = 0; g < LP_GB; ++g) X[(k + 2) % 3][g] = row[LP_W - (k + 3) * LP_GB + g];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int g = LP_GB - 1; g >= 0; --g) {
+            acc = __dadd_rn(X[k % 3][g], __dmul_rn(c, acc));
+            X[k % 3][g] = acc;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int g = 0; g < LP_GB; ++g) row[LP_W - (k + 1) * LP_GB + g] = X[k % 3][g];
+    }
+    return acc;
+}
+
 __global__ void __launch_bounds__(LP_T) k_gae_lp(const double* __restrict__ rew, const double* __restrict__ base,
                                                  const int64_t* __restrict__ off, const uint8_t* __restrict__ term,
                                                  int64_t P, double gamma, double gl, int use_gae,
@@ -570,7 +633,8 @@ __global__ void __launch_bounds__(LP_T) k_gae_lp(const double* __restrict__ rew,
     __shared__ double RB[2 * LP_BUF], TD[2 * LP_BUF], RF[2 * LP_BUF];
     __shared__ int64_t sb[LP_PATHS], se[LP_PATHS];
     __shared__ double sbl[LP_PATHS];          // b1's last entry: 0 if terminated else b[-1]
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar branches
     const int64_t p0 = (int64_t)blockIdx.x * LP_PATHS;
     const int np = (int)(P - p0 < LP_PATHS ? P - p0 : LP_PATHS);
     if (tid < LP_PATHS) {
@@ -593,51 +657,11 @@ __global__ void __launch_bounds__(LP_T) k_gae_lp(const double* __restrict__ rew,
         __syncthreads();   // window 0 put
         for (int j = 0; j < nwin; ++j) {
             if (chain) {
-                // the steps come into registers in batches of LP_GB (the next batch's
-                // LDS reads issued before this batch's serial steps), so only the
-                // dependent multiply -> add is on the critical path
                 double* const row = cw + (j & 1) * LP_BUF;
-                double x[LP_GB], xn2[LP_GB];
-                if (w == 2) {
-                    // front to back: Python's sum(p["rewards"]) (npg_cg.py:97); x + 1.0 * acc
-                    // is x + acc exactly (k_gae's form); steps past the path's end hold 0.0
-#pragma unroll
-                    for (int g = 0; g < LP_GB; ++g) x[g] = row[g];
-#pragma unroll
-                    for (int u0 = 0; u0 < LP_W; u0 += LP_GB) {
-                        if (u0 + LP_GB < LP_W) {
-#pragma unroll
-                            for (int g = 0; g < LP_GB; ++g) xn2[g] = row[u0 + LP_GB + g];
-                        }
-#pragma unroll
-                        for (int g = 0; g < LP_GB; ++g) acc = __dadd_rn(x[g], acc);
-#pragma unroll
-                        for (int g = 0; g < LP_GB; ++g) x[g] = xn2[g];
-                    }
-                } else {
-                    // backward over the whole window with no step mask: a partial window
-                    // (the path's first steps) holds its valid steps at u >= W - left,
-                    // which the chain meets first; what it computes below them is never
-                    // drained, and the path's chain ends there
-#pragma unroll
-                    for (int g = 0; g < LP_GB; ++g) x[g] = row[LP_W - LP_GB + g];
-#pragma unroll
-                    for (int u0 = LP_W - LP_GB; u0 >= 0; u0 -= LP_GB) {
-                        if (u0 >= LP_GB) {
-#pragma unroll
-                            for (int g = 0; g < LP_GB; ++g) xn2[g] = row[u0 - LP_GB + g];
-                        }
-#pragma unroll
-                        for (int g = LP_GB - 1; g >= 0; --g) {
-                            acc = __dadd_rn(x[g], __dmul_rn(c, acc));
-                            x[g] = acc;
-                        }
-#pragma unroll
-                        for (int g = 0; g < LP_GB; ++g) row[u0 + g] = x[g];
-#pragma unroll
-                        for (int g = 0; g < LP_GB; ++g) x[g] = xn2[g];
-                    }
-                }
+                if (w == 2)
+                    acc = lp_chain<true>(row, acc, c);
+                else
+                    acc = lp_chain<false>(row, acc, c);
             }
             __syncthreads();
         }

@@ -540,14 +540,15 @@ __global__ void __launch_bounds__(64 * GAE_WAVES) k_gae(const double* __restrict
 // gamma lambda), idle without GAE), wave 2 the path-return sum (front to back).  A
 // dependent fp64 multiply -> add costs ~10 cycles of issue per step for the whole
 // wave, however many lanes are on (profiles/r06b/gae_latency.txt), so LP_PATHS paths
-// advance for the price one did.  The chain waves touch LDS only: the steps come
-// through two LDS buffers in windows of LP_W steps per path (backward windows
-// aligned at each path's end, forward windows at its start), and four mover waves
-// (3..6) do all the global traffic — while the chains consume window j from one
-// buffer, the movers drain window j - 1's outputs from the other (coalesced
-// stores), put window j + 1 there (td formed on the way) and issue window j + 2's
-// loads.  One barrier per window; a chain wave never waits on HBM.  Bit-identical
-// to k_gae: the same __dmul_rn / __dadd_rn / __dsub_rn per step in the same order.
+// advance for the price one did.  The steps come through two LDS buffers in windows
+// of LP_W steps per path (backward windows aligned at each path's end, forward
+// windows at its start): four mover waves (3..6) do every global load — while the
+// chains consume window j from one buffer, the movers put window j + 1 into the
+// other (td formed on the way) and issue window j + 2's loads — and the chain waves
+// store their own outputs to HBM in 16-byte stores (cheaper for the chain than
+// writing them back to LDS for the movers, lp_chain_bwd).  One barrier per window; a
+// chain wave never waits on HBM.  Bit-identical to k_gae: the same __dmul_rn /
+// __dadd_rn / __dsub_rn per step in the same order.
 constexpr int LP_PATHS = 8;               // paths per workgroup (lanes 0..7 of each chain wave)
 constexpr int LP_W = 256;                 // steps per window (a window's chain ~2-3 us covers the next loads)
 constexpr int LP_LD = LP_W + 1;           // LDS row stride (doubles): chain lanes conflict-free
@@ -587,28 +588,40 @@ __device__ __forceinline__ double lp_chain<true>(double* __restrict__ row, doubl
     return acc;
 }
 
-// Backward (returns / advantages, acc = x + c * acc, outputs written back in place)
-// over the whole window with no step mask: a partial window (the path's first steps)
-// holds its valid steps at u >= W - left, which the chain meets first; what it
-// computes below them is never drained, and the path's chain ends there.  The LDS
-// reads of batch k + 2 are issued before batch k's serial steps (two batches of LDS
-// latency covered; sched_barrier keeps the compiler from sinking them to their use),
-// so only the dependent multiply -> add is on the critical path.  Batch k: u in
+// Backward (returns / advantages, acc = x + c * acc) over the whole window with no
+// step mask: a partial window (the path's first steps) holds its valid steps at
+// u >= vmin = W - left, which the chain meets first; what it computes below them is
+// never stored, and the path's chain ends there.  The LDS reads of batch k + 2 are
+// issued before batch k's serial steps (sched_barrier keeps the compiler from sinking
+// them to their use).  The outputs leave for HBM from the chain wave itself, a batch
+// at a time in 16-byte stores: an LDS write costs the wave ~13 cycles a step against
+// ~2 for the reads and ~5 for the global stores (profiles/r06c/gae_latency.txt, the
+// lanes rows).  out points at the window's step u = 0 (t = e - (j + 1) W).  PLAIN
+// (no GAE): wave 0 also stores adv = ret - b, b from the TD row.  Batch k: u in
 // [W - (k + 1) GB, W - k GB).
-template <>
-__device__ __forceinline__ double lp_chain<false>(double* __restrict__ row, double acc, double c) {
+typedef double lp_d2 __attribute__((ext_vector_type(2), aligned(8)));
+template <bool PLAIN>
+__device__ __forceinline__ double lp_chain_bwd(const double* __restrict__ row, const double* __restrict__ brow,
+                                               double acc, double c, double* out, double* out2, int vmin) {
     constexpr int NB = LP_W / LP_GB;
-    double X[3][LP_GB];
+    constexpr int NQ = PLAIN ? 3 : 1;
+    double X[3][LP_GB], B[NQ][LP_GB];
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
 #pragma unroll
-        for (int g = 0; g < LP_GB; ++g) X[k][g] = row[LP_W - (k + 1) * LP_GB + g];
+        for (int g = 0; g < LP_GB; ++g) {
+            X[k][g] = row[LP_W - (k + 1) * LP_GB + g];
+            if (PLAIN) B[k % NQ][g] = brow[LP_W - (k + 1) * LP_GB + g];
+        }
     }
 #pragma unroll
     for (int k = 0; k < NB; ++k) {
         if (k + 2 < NB) {
 #pragma unroll
-            for (int g = 0; g < LP_GB; ++g) X[(k + 2) % 3][g] = row[LP_W - (k + 3) * LP_GB + g];
+            for (int g = 0; g < LP_GB; ++g) {
+                X[(k + 2) % 3][g] = row[LP_W - (k + 3) * LP_GB + g];
+                if (PLAIN) B[(k + 2) % NQ][g] = brow[LP_W - (k + 3) * LP_GB + g];
+            }
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -617,8 +630,24 @@ __device__ __forceinline__ double lp_chain<false>(double* __restrict__ row, doub
             X[k % 3][g] = acc;
         }
         __builtin_amdgcn_sched_barrier(0);
+        const int lo = LP_W - (k + 1) * LP_GB;
+        if (lo >= vmin) {
 #pragma unroll
-        for (int g = 0; g < LP_GB; ++g) row[LP_W - (k + 1) * LP_GB + g] = X[k % 3][g];
+            for (int g = 0; g < LP_GB; g += 2) {
+                *(lp_d2*)(out + lo + g) = lp_d2{X[k % 3][g], X[k % 3][g + 1]};
+                if (PLAIN)   // plain advantages: ret - b (process_samples.py:31-32)
+                    *(lp_d2*)(out2 + lo + g) = lp_d2{__dsub_rn(X[k % 3][g], B[k % NQ][g]),
+                                                     __dsub_rn(X[k % 3][g + 1], B[k % NQ][g + 1])};
+            }
+        } else if (lo + LP_GB > vmin) {   // the batch holding the path's first step
+#pragma unroll
+            for (int g = 0; g < LP_GB; ++g) {
+                if (lo + g >= vmin) {
+                    out[lo + g] = X[k % 3][g];
+                    if (PLAIN) out2[lo + g] = __dsub_rn(X[k % 3][g], B[k % NQ][g]);
+                }
+            }
+        }
     }
     return acc;
 }
@@ -649,30 +678,38 @@ __global__ void __launch_bounds__(LP_T) k_gae_lp(const double* __restrict__ rew,
     for (int i = 0; i < np; ++i) hmax = se[i] - sb[i] > hmax ? se[i] - sb[i] : hmax;
     const int nwin = (int)((hmax + LP_W - 1) / LP_W);
     if (w < LP_CH) {
-        // ---- a chain wave: LDS only ----
+        // ---- a chain wave: LDS reads, its own outputs' stores ----
         const bool chain = lane < np && (w != 1 || use_gae);
         const double c = w == 0 ? gamma : gl;
         double* const cw = (w == 0 ? RB : (w == 1 ? TD : RF)) + lane * LP_LD;
+        const int64_t lb = lane < np ? sb[lane] : 0, le = lane < np ? se[lane] : 0;
+        double* const o1 = w == 0 ? ret : adv;
         double acc = 0.0;
         __syncthreads();   // window 0 put
         for (int j = 0; j < nwin; ++j) {
             if (chain) {
                 double* const row = cw + (j & 1) * LP_BUF;
+                const int64_t t0 = le - (int64_t)(j + 1) * LP_W;   // the window's u = 0
+                const int64_t vm = lb - t0;                         // first valid u
+                const int vmin = (int)(vm < 0 ? 0 : (vm > LP_W ? LP_W : vm));
                 if (w == 2)
                     acc = lp_chain<true>(row, acc, c);
+                else if (w == 1 || use_gae)
+                    acc = lp_chain_bwd<false>(row, nullptr, acc, c, o1 + t0, nullptr, vmin);
                 else
-                    acc = lp_chain<false>(row, acc, c);
+                    acc = lp_chain_bwd<true>(row, TD + (j & 1) * LP_BUF + lane * LP_LD, acc, c, ret + t0,
+                                             adv + t0, vmin);
             }
             __syncthreads();
         }
         if (w == 2 && lane < np) path_ret[p0 + lane] = acc;
         return;
     }
-    // ---- a mover: all global loads and stores ----
+    // ---- a mover: every global load ----
     const int m = tid - 64 * LP_CH;
     const int mp = m / LP_TPP, mu = m % LP_TPP;
     // an empty path (or a thread past the last path) reads index 0: valid whenever a
-    // window exists, and never used (the chains and the drain skip its steps)
+    // window exists, and never used (the chains skip its steps)
     const int64_t pb = se[mp] > sb[mp] ? sb[mp] : 0, pe = se[mp] > sb[mp] ? se[mp] : 1;
     const double pbl = sbl[mp];
     const int64_t db = sb[mp], de = se[mp], plen = de - db;
@@ -707,19 +744,6 @@ __global__ void __launch_bounds__(LP_T) k_gae_lp(const double* __restrict__ rew,
             RF[q + u] = (int64_t)j * LP_W + u < plen ? xf[k] : 0.0;
         }
     };
-    auto drain = [&](int j) {   // window j's outputs (in RB / TD of its buffer) to HBM
-        const int q = (j & 1) * LP_BUF + mp * LP_LD;
-#pragma unroll
-        for (int k = 0; k < LP_PER; ++k) {
-            const int u = mu + LP_TPP * k;
-            const int64_t tb = de - (int64_t)(j + 1) * LP_W + u;
-            if (tb >= db) {
-                const double rr = RB[q + u];
-                ret[tb] = rr;
-                adv[tb] = use_gae ? TD[q + u] : __dsub_rn(rr, TD[q + u]);   // plain: ret - b
-            }
-        }
-    };
     if (nwin > 0) {
         load(0);
         put(0);
@@ -727,13 +751,11 @@ __global__ void __launch_bounds__(LP_T) k_gae_lp(const double* __restrict__ rew,
     if (nwin > 1) load(1);
     __syncthreads();   // window 0 put
     for (int j = 0; j < nwin; ++j) {
-        // the chains run window j (buffer j & 1); the other buffer holds window j - 1
-        if (j >= 1) drain(j - 1);
+        // the chains run window j (buffer j & 1); the other buffer held window j - 1
         if (j + 1 < nwin) put(j + 1);
         if (j + 2 < nwin) load(j + 2);
         __syncthreads();
     }
-    if (nwin > 0) drain(nwin - 1);
 }
 
 #ifdef MJRL_GAE_LP4

@@ -108,6 +108,74 @@ float run(const double* in, double* out, int nb, int reps) {
     return ms / reps;
 }
 
+
+// k_gae_lp's chain-wave pattern (round 6): lanes = paths, each lane its own LDS row
+// (stride 257 doubles: conflict-free), 16-step batches, the reads of batch k + 2
+// issued before batch k's steps.  NL lanes active; MODE 0 reads + writes back (the
+// kernel's pattern), 1 reads only, 2 writes only, 3 reads + outputs to global
+// (dwordx2 per step, lane rows in HBM), 4 registers only.
+constexpr int RW = 256, RLD = 257, RB = 16;
+template <int MODE, int NL>
+__global__ void __launch_bounds__(64) k_lane(double* __restrict__ out, int nw, double c) {
+    __shared__ double row_s[NL * RLD];
+    const int lane = threadIdx.x;
+    for (int i = lane; i < NL * RLD; i += 64) row_s[i] = 0.001 * (i % 97) - 0.03;
+    __syncthreads();
+    if (lane >= NL) return;
+    double* row = row_s + lane * RLD;
+    double acc = 0.0;
+    double* o = out + 64 + (size_t)lane * RW;
+    for (int j = 0; j < nw; ++j) {
+        constexpr int NB = RW / RB;
+        double X[3][RB];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+#pragma unroll
+            for (int g = 0; g < RB; ++g) X[k][g] = (MODE == 2 || MODE == 4) ? 0.5 * g : row[RW - (k + 1) * RB + g];
+        }
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+            if (k + 2 < NB && MODE != 2 && MODE != 4) {
+#pragma unroll
+                for (int g = 0; g < RB; ++g) X[(k + 2) % 3][g] = row[RW - (k + 3) * RB + g];
+            } else if (k + 2 < NB) {
+#pragma unroll
+                for (int g = 0; g < RB; ++g) X[(k + 2) % 3][g] = 0.25 * g + k;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int g = RB - 1; g >= 0; --g) {
+                acc = __dadd_rn(X[k % 3][g], __dmul_rn(c, acc));
+                X[k % 3][g] = acc;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if (MODE == 0 || MODE == 2) {
+#pragma unroll
+                for (int g = 0; g < RB; ++g) row[RW - (k + 1) * RB + g] = X[k % 3][g];
+            } else if (MODE == 3) {
+#pragma unroll
+                for (int g = 0; g < RB; ++g) o[RW - (k + 1) * RB + g] = X[k % 3][g];
+            }
+        }
+    }
+    out[lane] = acc + row[lane & 7];
+}
+
+template <int MODE, int NL>
+float run_lane(double* out, int nw, int reps) {
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    hipLaunchKernelGGL((k_lane<MODE, NL>), dim3(1), dim3(64), 0, 0, out, nw, 0.995);
+    hipEventRecord(a, 0);
+    for (int r = 0; r < reps; ++r) hipLaunchKernelGGL((k_lane<MODE, NL>), dim3(1), dim3(64), 0, 0, out, nw, 0.995);
+    hipEventRecord(b, 0);
+    hipEventSynchronize(b);
+    float ms = 0;
+    hipEventElapsedTime(&ms, a, b);
+    return ms / reps;
+}
+
 int main() {
     double *in, *out;
     hipMalloc(&in, 2048 * sizeof(double));
@@ -140,6 +208,27 @@ int main() {
         const double ns = t[i] * 1e6 / (nb * GU);
         printf("%-42s %7.3f ns/step  %6.1f cycles/step\n", names[i], ns, ns * clk / 1e6);
     }
+    // the lanes = paths chain of k_gae_lp (one wave, nw windows of 256 steps)
+    double* out2;
+    hipMalloc(&out2, (64 + 64 * RW) * sizeof(double));
+    const int nw = 512;
+    const char* lnames[] = {"lanes: 8 paths, LDS reads + writes (k_gae_lp)", "lanes: 8 paths, LDS reads only",
+                            "lanes: 8 paths, LDS writes only", "lanes: 8 paths, LDS reads, outputs to global",
+                            "lanes: 64 paths, LDS reads + writes", "lanes: 8 paths, registers only"};
+    float lt[6];
+    for (int pass = 0; pass < 2; ++pass) {
+        lt[0] = run_lane<0, 8>(out2, nw, 5);
+        lt[1] = run_lane<1, 8>(out2, nw, 5);
+        lt[2] = run_lane<2, 8>(out2, nw, 5);
+        lt[3] = run_lane<3, 8>(out2, nw, 5);
+        lt[4] = run_lane<0, 64>(out2, nw, 5);
+        lt[5] = run_lane<4, 8>(out2, nw, 5);
+    }
+    for (int i = 0; i < 6; ++i) {
+        const double ns = lt[i] * 1e6 / (nw * RW);
+        printf("%-46s %7.3f ns/step  %6.1f cycles/step\n", lnames[i], ns, ns * clk / 1e6);
+    }
+    hipFree(out2);
     hipFree(in);
     hipFree(out);
     return 0;

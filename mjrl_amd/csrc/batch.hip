@@ -554,8 +554,14 @@ constexpr int LP_W = 256;                 // steps per window (a window's chain 
 constexpr int LP_LD = LP_W + 1;           // LDS row stride (doubles): chain lanes conflict-free
 constexpr int LP_GB = 16;                 // chain steps per register batch
 constexpr int LP_CH = 3;                  // chain waves 0..2
-constexpr int LP_MV = 256;                // mover threads (waves 3..6)
-constexpr int LP_T = 64 * LP_CH + LP_MV;
+#ifdef MJRL_GAE_MV4
+constexpr int LP_MVW = 4;                 // variant (A/B): mover waves 3..6, two of them beside chain waves
+constexpr int LP_T = 64 * (LP_CH + LP_MVW);
+#else
+constexpr int LP_MVW = 2;                 // mover waves 3 and 7: the fourth SIMD to themselves (waves are
+constexpr int LP_T = 512;                 // dealt to SIMDs w % 4), so no chain wave shares its issue port;
+#endif                                    // waves 4..6 end at once
+constexpr int LP_MV = 64 * LP_MVW;
 constexpr int LP_TPP = LP_MV / LP_PATHS;  // mover threads a path: runs of LP_TPP consecutive steps a load
 constexpr int LP_PER = LP_W / LP_TPP;     // window elements per mover thread per array
 constexpr int LP_BUF = LP_PATHS * LP_LD;  // one array of one buffer (doubles)
@@ -657,32 +663,32 @@ __global__ void __launch_bounds__(LP_T) k_gae_lp(const double* __restrict__ rew,
                                                  int64_t P, double gamma, double gl, int use_gae,
                                                  double* __restrict__ ret, double* __restrict__ adv,
                                                  double* __restrict__ path_ret) {
-    // buffer q of array A at A + q * LP_BUF: RB backward rewards -> returns (in place),
-    // TD td -> advantages (in place; no GAE: the baseline), RF forward rewards
+    // buffer q of array A at A + q * LP_BUF: RB backward rewards, TD td (no GAE: the
+    // baseline), RF forward rewards
     __shared__ double RB[2 * LP_BUF], TD[2 * LP_BUF], RF[2 * LP_BUF];
-    __shared__ int64_t sb[LP_PATHS], se[LP_PATHS];
-    __shared__ double sbl[LP_PATHS];          // b1's last entry: 0 if terminated else b[-1]
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar branches
+    if (LP_MVW == 2 && w > 3 && w < 7) return;
     const int64_t p0 = (int64_t)blockIdx.x * LP_PATHS;
     const int np = (int)(P - p0 < LP_PATHS ? P - p0 : LP_PATHS);
-    if (tid < LP_PATHS) {
-        const bool ok = tid < np;
-        const int64_t b = ok ? off[p0 + tid] : 0, e = ok ? off[p0 + tid + 1] : 0;
-        sb[tid] = b;
-        se[tid] = e;
-        sbl[tid] = e > b ? (term[p0 + tid] ? 0.0 : base[e - 1]) : 0.0;
-    }
-    __syncthreads();
+    // the window count from the workgroup's path bounds (uniform addresses: scalar
+    // loads); each chain lane and mover reads its own path's bounds with a vector load,
+    // so the first window's loads wait on one HBM round trip and no barrier
     int64_t hmax = 0;
-    for (int i = 0; i < np; ++i) hmax = se[i] - sb[i] > hmax ? se[i] - sb[i] : hmax;
+#pragma unroll
+    for (int i = 0; i < LP_PATHS; ++i) {
+        if (i < np) {
+            const int64_t l = off[p0 + i + 1] - off[p0 + i];
+            hmax = l > hmax ? l : hmax;
+        }
+    }
     const int nwin = (int)((hmax + LP_W - 1) / LP_W);
     if (w < LP_CH) {
         // ---- a chain wave: LDS reads, its own outputs' stores ----
         const bool chain = lane < np && (w != 1 || use_gae);
         const double c = w == 0 ? gamma : gl;
         double* const cw = (w == 0 ? RB : (w == 1 ? TD : RF)) + lane * LP_LD;
-        const int64_t lb = lane < np ? sb[lane] : 0, le = lane < np ? se[lane] : 0;
+        const int64_t lb = lane < np ? off[p0 + lane] : 0, le = lane < np ? off[p0 + lane + 1] : 0;
         double* const o1 = w == 0 ? ret : adv;
         double acc = 0.0;
         __syncthreads();   // window 0 put
@@ -706,13 +712,15 @@ __global__ void __launch_bounds__(LP_T) k_gae_lp(const double* __restrict__ rew,
         return;
     }
     // ---- a mover: every global load ----
-    const int m = tid - 64 * LP_CH;
+    const int m = (LP_MVW == 2 ? (w == 3 ? 0 : 1) : w - LP_CH) * 64 + lane;
     const int mp = m / LP_TPP, mu = m % LP_TPP;
+    const bool okp = mp < np;
+    const int64_t db = okp ? off[p0 + mp] : 0, de = okp ? off[p0 + mp + 1] : 0, plen = de - db;
+    // b1's last entry: 0 if terminated else b[-1] (process_samples.py:24-27)
+    const double pbl = de > db ? (term[p0 + mp] ? 0.0 : base[de - 1]) : 0.0;
     // an empty path (or a thread past the last path) reads index 0: valid whenever a
     // window exists, and never used (the chains skip its steps)
-    const int64_t pb = se[mp] > sb[mp] ? sb[mp] : 0, pe = se[mp] > sb[mp] ? se[mp] : 1;
-    const double pbl = sbl[mp];
-    const int64_t db = sb[mp], de = se[mp], plen = de - db;
+    const int64_t pb = de > db ? db : 0, pe = de > db ? de : 1;
     double xr[LP_PER], xb[LP_PER], xn[LP_PER], xf[LP_PER];
     auto load = [&](int j) {
         // backward window: step t = e - (j + 1) W + u; forward window: t = b + j W + u;

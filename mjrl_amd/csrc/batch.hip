@@ -554,13 +554,15 @@ constexpr int LP_W = 256;                 // steps per window (a window's chain 
 constexpr int LP_LD = LP_W + 1;           // LDS row stride (doubles): chain lanes conflict-free
 constexpr int LP_GB = 16;                 // chain steps per register batch
 constexpr int LP_CH = 3;                  // chain waves 0..2
-#ifdef MJRL_GAE_MV4
-constexpr int LP_MVW = 4;                 // variant (A/B): mover waves 3..6, two of them beside chain waves
+#ifndef MJRL_GAE_MVW
+#define MJRL_GAE_MVW 4
+#endif
+// mover waves 3 .. 3 + LP_MVW - 1.  Two movers on the fourth SIMD alone (waves 3 and
+// 7, no chain wave sharing their SIMD) measured slower than four (22.9 vs 21.3 us
+// at 125 x 1000, profiles/r06c/gae5): the movers' window, not the chains' issue, is
+// what the chains wait for
+constexpr int LP_MVW = MJRL_GAE_MVW;
 constexpr int LP_T = 64 * (LP_CH + LP_MVW);
-#else
-constexpr int LP_MVW = 2;                 // mover waves 3 and 7: the fourth SIMD to themselves (waves are
-constexpr int LP_T = 512;                 // dealt to SIMDs w % 4), so no chain wave shares its issue port;
-#endif                                    // waves 4..6 end at once
 constexpr int LP_MV = 64 * LP_MVW;
 constexpr int LP_TPP = LP_MV / LP_PATHS;  // mover threads a path: runs of LP_TPP consecutive steps a load
 constexpr int LP_PER = LP_W / LP_TPP;     // window elements per mover thread per array
@@ -668,7 +670,6 @@ __global__ void __launch_bounds__(LP_T) k_gae_lp(const double* __restrict__ rew,
     __shared__ double RB[2 * LP_BUF], TD[2 * LP_BUF], RF[2 * LP_BUF];
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar branches
-    if (LP_MVW == 2 && w > 3 && w < 7) return;
     const int64_t p0 = (int64_t)blockIdx.x * LP_PATHS;
     const int np = (int)(P - p0 < LP_PATHS ? P - p0 : LP_PATHS);
     // the window count from the workgroup's path bounds (uniform addresses: scalar
@@ -712,7 +713,7 @@ __global__ void __launch_bounds__(LP_T) k_gae_lp(const double* __restrict__ rew,
         return;
     }
     // ---- a mover: every global load ----
-    const int m = (LP_MVW == 2 ? (w == 3 ? 0 : 1) : w - LP_CH) * 64 + lane;
+    const int m = (w - LP_CH) * 64 + lane;
     const int mp = m / LP_TPP, mu = m % LP_TPP;
     const bool okp = mp < np;
     const int64_t db = okp ? off[p0 + mp] : 0, de = okp ? off[p0 + mp + 1] : 0, plen = de - db;

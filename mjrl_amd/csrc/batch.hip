@@ -550,7 +550,10 @@ __global__ void __launch_bounds__(64 * GAE_WAVES) k_gae(const double* __restrict
 // chain wave never waits on HBM.  Bit-identical to k_gae: the same __dmul_rn /
 // __dadd_rn / __dsub_rn per step in the same order.
 constexpr int LP_PATHS = 8;               // paths per workgroup (lanes 0..7 of each chain wave)
-constexpr int LP_W = 256;                 // steps per window (a window's chain ~2-3 us covers the next loads)
+#ifndef MJRL_GAE_W
+#define MJRL_GAE_W 256
+#endif
+constexpr int LP_W = MJRL_GAE_W;          // steps per window (a window's chain ~2-3 us covers the next loads)
 constexpr int LP_LD = LP_W + 1;           // LDS row stride (doubles): chain lanes conflict-free
 constexpr int LP_GB = 16;                 // chain steps per register batch
 constexpr int LP_CH = 3;                  // chain waves 0..2
@@ -699,6 +702,9 @@ __global__ void __launch_bounds__(LP_T) k_gae_lp(const double* __restrict__ rew,
                 const int64_t t0 = le - (int64_t)(j + 1) * LP_W;   // the window's u = 0
                 const int64_t vm = lb - t0;                         // first valid u
                 const int vmin = (int)(vm < 0 ? 0 : (vm > LP_W ? LP_W : vm));
+#ifdef MJRL_GAE_ABL_NOCHAIN
+                if (j >= 0) continue;   // timing ablation: the chains skipped, barriers kept
+#endif
                 if (w == 2)
                     acc = lp_chain<true>(row, acc, c);
                 else if (w == 1 || use_gae)
@@ -761,8 +767,14 @@ __global__ void __launch_bounds__(LP_T) k_gae_lp(const double* __restrict__ rew,
     __syncthreads();   // window 0 put
     for (int j = 0; j < nwin; ++j) {
         // the chains run window j (buffer j & 1); the other buffer held window j - 1
+#if defined(MJRL_GAE_ABL_NOPUT) || defined(MJRL_GAE_ABL_NOLOAD)
+        // timing ablations: the movers' puts (NOPUT) or puts and loads (NOLOAD) skipped
+#else
         if (j + 1 < nwin) put(j + 1);
+#endif
+#ifndef MJRL_GAE_ABL_NOLOAD
         if (j + 2 < nwin) load(j + 2);
+#endif
         __syncthreads();
     }
 }

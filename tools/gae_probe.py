@@ -1,7 +1,9 @@
 """Times mjrl_gae (exact serial chains) and mjrl_gae_scan on the bench's path
 shapes with HIP events, and checks the exact kernel against the oracle's
 discount_sum chains bit for bit on the first paths.  GPU box:
-    python tools/gae_probe.py"""
+    python tools/gae_probe.py
+GAE_PROBE_ONLY=1: mjrl_gae alone; GAE_PROBE_NOCHECK=1 (with MJRL_AMD_ALLOW_ABLATION=1):
+time a timing-ablation build of the kernel (-DMJRL_GAE_ABL_*), results unchecked."""
 import os
 import sys
 
@@ -25,7 +27,9 @@ def run(P, H, reps=20):
     pr = torch.empty(P, dtype=torch.float64, device=dev)
     st = _lib.stream_ptr()
     out = {}
-    for name in ("mjrl_gae", "mjrl_gae_wave", "mjrl_gae_scan"):
+    only = os.environ.get("GAE_PROBE_ONLY") == "1"
+    nocheck = os.environ.get("GAE_PROBE_NOCHECK") == "1"
+    for name in ("mjrl_gae",) if only else ("mjrl_gae", "mjrl_gae_wave", "mjrl_gae_scan"):
         fn = getattr(L, name)
         args = (_lib.ptr(rew), _lib.ptr(base), _lib.ptr(off), _lib.ptr(term), P, 0.995, 0.97, 1, _lib.ptr(ret),
                 _lib.ptr(adv), _lib.ptr(pr), st)
@@ -38,7 +42,7 @@ def run(P, H, reps=20):
         e1.record()
         torch.cuda.synchronize()
         out[name] = e0.elapsed_time(e1) / reps * 1e3
-        if name in ("mjrl_gae", "mjrl_gae_wave"):
+        if name in ("mjrl_gae", "mjrl_gae_wave") and not nocheck:
             from oracle import npg_cpu as O
             r, b = rew.cpu().numpy(), base.cpu().numpy()
             lengths = np.full(P, H)
@@ -52,4 +56,5 @@ if __name__ == "__main__":
                  (125, 1024), (125, 2000), (125, 4000), (1, 4000)):
         o = run(P, H)
         print("P %5d H %5d  gae (lanes = paths) %7.2f us  gae_wave (round 5) %7.2f us  gae_scan %7.2f us"
-              % (P, H, o["mjrl_gae"], o["mjrl_gae_wave"], o["mjrl_gae_scan"]), flush=True)
+              % (P, H, o["mjrl_gae"], o.get("mjrl_gae_wave", float("nan")), o.get("mjrl_gae_scan", float("nan"))),
+              flush=True)

@@ -576,25 +576,32 @@ static_assert(LP_W % LP_TPP == 0 && LP_W % LP_GB == 0, "window split");
 template <bool FWD>
 __device__ __forceinline__ double lp_chain(double* __restrict__ row, double acc, double c);
 
-// Forward (the path-return sum, one add a step: slack beside the backward waves):
-// front to back, Python's sum(p["rewards"]) (npg_cg.py:97); x + 1.0 * acc is x + acc
-// exactly (k_gae's form); steps past the path's end hold 0.0.  The next batch's
-// reads are issued before this batch's adds.
+// Forward (the path-return sum, one add a step): front to back, Python's
+// sum(p["rewards"]) (npg_cg.py:97); x + 1.0 * acc is x + acc exactly (k_gae's form);
+// steps past the path's end hold 0.0.  Batch k + 2's reads are issued before batch
+// k's adds, as in the backward chains.
 template <>
 __device__ __forceinline__ double lp_chain<true>(double* __restrict__ row, double acc, double) {
-    double x[LP_GB], xn[LP_GB];
+    constexpr int NB = LP_W / LP_GB;
+    double X[3][LP_GB];
 #pragma unroll
-    for (int g = 0; g < LP_GB; ++g) x[g] = row[g];
+    for (int k = 0; k < 2; ++k) {
 #pragma unroll
-    for (int u0 = 0; u0 < LP_W; u0 += LP_GB) {
-        if (u0 + LP_GB < LP_W) {
+        for (int g = 0; g < LP_GB; ++g) X[k][g] = row[k * LP_GB + g];
+    }
 #pragma unroll
-            for (int g = 0; g < LP_GB; ++g) xn[g] = row[u0 + LP_GB + g];
+    for (int k = 0; k < NB; ++k) {
+        if (k + 2 < NB) {
+#pragma unroll
+            for (int g = 0; g < LP_GB; ++g) X[(k + 2) % 3][g] = row[(k + 2) * LP_GB + g];
         }
+        // no store follows to order them, so without a compiler barrier the reads of
+        // every batch are hoisted to the top (and spilled)
+        asm volatile("" ::: "memory");
+#ifndef MJRL_GAE_ABL_NOFWD
 #pragma unroll
-        for (int g = 0; g < LP_GB; ++g) acc = __dadd_rn(x[g], acc);
-#pragma unroll
-        for (int g = 0; g < LP_GB; ++g) x[g] = xn[g];
+        for (int g = 0; g < LP_GB; ++g) acc = __dadd_rn(X[k % 3][g], acc);
+#endif
     }
     return acc;
 }
@@ -642,7 +649,11 @@ __device__ __forceinline__ double lp_chain_bwd(const double* __restrict__ row, c
         }
         __builtin_amdgcn_sched_barrier(0);
         const int lo = LP_W - (k + 1) * LP_GB;
+#ifdef MJRL_GAE_ABL_NOSTORE
+        if (lo < -1) {   // timing ablation: the outputs' stores skipped
+#else
         if (lo >= vmin) {
+#endif
 #pragma unroll
             for (int g = 0; g < LP_GB; g += 2) {
                 *(lp_d2*)(out + lo + g) = lp_d2{X[k % 3][g], X[k % 3][g + 1]};

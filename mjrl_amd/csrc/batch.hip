@@ -538,137 +538,76 @@ __global__ void __launch_bounds__(64 * GAE_WAVES) k_gae(const double* __restrict
 // in ONE instruction stream each, one wave per chain, each lane one path — wave 0
 // the returns (discount_sum(rewards, gamma)), wave 1 the advantages (discount_sum(td,
 // gamma lambda), idle without GAE), wave 2 the path-return sum (front to back).  A
-// dependent fp64 multiply -> add costs ~10 cycles of issue per step for the whole
+// dependent fp64 multiply -> add costs ~11 cycles of issue per step for the whole
 // wave, however many lanes are on (profiles/r06b/gae_latency.txt), so LP_PATHS paths
-// advance for the price one did.  The steps come through two LDS buffers in windows
-// of LP_W steps per path (backward windows aligned at each path's end, forward
-// windows at its start): four mover waves (3..6) do every global load — while the
-// chains consume window j from one buffer, the movers put window j + 1 into the
-// other (td formed on the way) and issue window j + 2's loads — and the chain waves
-// store their own outputs to HBM in 16-byte stores (cheaper for the chain than
-// writing them back to LDS for the movers, lp_chain_bwd).  One barrier per window; a
-// chain wave never waits on HBM.  Bit-identical to k_gae: the same __dmul_rn /
-// __dadd_rn / __dsub_rn per step in the same order.
+// advance for the price one did — as long as the chain wave does little else: a
+// store of its outputs costs it ~10 cycles a step to HBM and ~13 to LDS, an LDS read
+// ~2 (profiles/r06c/gae_latency.txt, the "lanes" rows).  So the chain waves only read
+// and keep one checkpoint per LP_GB-step segment (the accumulator entering it, one
+// LDS write per segment), and the four mover waves (3..6) recompute every segment
+// from its checkpoint — the same __dmul_rn / __dadd_rn in the same order, so the
+// same values bit for bit — one segment per lane, 256 segments side by side, and
+// store them (each lane a 128-byte run).  The steps come through three LDS buffers in
+// windows of LP_W steps per path (backward windows aligned at each path's end,
+// forward windows at its start): while the chains consume window i, the movers
+// recompute and store window i - 1, put window i + 1 (td formed on the way) and issue
+// window i + 2's loads.  One barrier per window.  Bit-identical to k_gae.
+typedef double lp_d2 __attribute__((ext_vector_type(2), aligned(8)));   // 16-byte store, 8-byte aligned
 constexpr int LP_PATHS = 8;               // paths per workgroup (lanes 0..7 of each chain wave)
 #ifndef MJRL_GAE_W
 #define MJRL_GAE_W 256
 #endif
-constexpr int LP_W = MJRL_GAE_W;          // steps per window (a window's chain ~2-3 us covers the next loads)
+constexpr int LP_W = MJRL_GAE_W;          // steps per window
 constexpr int LP_LD = LP_W + 1;           // LDS row stride (doubles): chain lanes conflict-free
-constexpr int LP_GB = 16;                 // chain steps per register batch
+constexpr int LP_GB = 16;                 // steps per segment (chain register batch, recompute task)
+constexpr int LP_NS = LP_W / LP_GB;       // segments per window row
 constexpr int LP_CH = 3;                  // chain waves 0..2
-#ifndef MJRL_GAE_MVW
-#define MJRL_GAE_MVW 4
-#endif
-// mover waves 3 .. 3 + LP_MVW - 1.  Two movers on the fourth SIMD alone (waves 3 and
-// 7, no chain wave sharing their SIMD) measured slower than four (22.9 vs 21.3 us
-// at 125 x 1000, profiles/r06c/gae5): the movers' window, not the chains' issue, is
-// what the chains wait for
-constexpr int LP_MVW = MJRL_GAE_MVW;
+constexpr int LP_MVW = 4;                 // mover waves 3..6
 constexpr int LP_T = 64 * (LP_CH + LP_MVW);
 constexpr int LP_MV = 64 * LP_MVW;
 constexpr int LP_TPP = LP_MV / LP_PATHS;  // mover threads a path: runs of LP_TPP consecutive steps a load
 constexpr int LP_PER = LP_W / LP_TPP;     // window elements per mover thread per array
 constexpr int LP_BUF = LP_PATHS * LP_LD;  // one array of one buffer (doubles)
+constexpr int LP_NB = 3;                  // LDS buffers
 static_assert(LP_W % LP_TPP == 0 && LP_W % LP_GB == 0, "window split");
+static_assert(2 * LP_PATHS * LP_NS <= LP_MV, "one recompute segment per mover thread");
 
-// One chain wave's pass over one LDS window row (its lane's path).
+// A chain wave's pass over one window row (its lane's path), batch k + 2's LDS reads
+// issued before batch k's steps (the compiler barrier keeps them from all being
+// hoisted to the top).  Forward: the path-return sum front to back, Python's
+// sum(p["rewards"]) (npg_cg.py:97; x + 1.0 * acc is x + acc exactly, k_gae's form;
+// steps past the path's end hold 0.0).  Backward: acc = x + c * acc over the whole
+// window with no step mask (a partial window, the path's first steps, holds its valid
+// steps at the top, which the chain meets first; what it computes below them is never
+// stored and the path's chain ends there), writing the accumulator entering each
+// segment to ck[k * LP_PATHS] (segment k = batch k: u in [W - (k + 1) GB, W - k GB)).
 template <bool FWD>
-__device__ __forceinline__ double lp_chain(double* __restrict__ row, double acc, double c);
-
-// Forward (the path-return sum, one add a step): front to back, Python's
-// sum(p["rewards"]) (npg_cg.py:97); x + 1.0 * acc is x + acc exactly (k_gae's form);
-// steps past the path's end hold 0.0.  Batch k + 2's reads are issued before batch
-// k's adds, as in the backward chains.
-template <>
-__device__ __forceinline__ double lp_chain<true>(double* __restrict__ row, double acc, double) {
-    constexpr int NB = LP_W / LP_GB;
+__device__ __forceinline__ double lp_chain(const double* __restrict__ row, double acc, double c,
+                                           double* __restrict__ ck) {
     double X[3][LP_GB];
+    auto at = [](int k) { return FWD ? k * LP_GB : LP_W - (k + 1) * LP_GB; };
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
 #pragma unroll
-        for (int g = 0; g < LP_GB; ++g) X[k][g] = row[k * LP_GB + g];
+        for (int g = 0; g < LP_GB; ++g) X[k][g] = row[at(k) + g];
     }
 #pragma unroll
-    for (int k = 0; k < NB; ++k) {
-        if (k + 2 < NB) {
+    for (int k = 0; k < LP_NS; ++k) {
+        if (k + 2 < LP_NS) {
 #pragma unroll
-            for (int g = 0; g < LP_GB; ++g) X[(k + 2) % 3][g] = row[(k + 2) * LP_GB + g];
+            for (int g = 0; g < LP_GB; ++g) X[(k + 2) % 3][g] = row[at(k + 2) + g];
         }
-        // no store follows to order them, so without a compiler barrier the reads of
-        // every batch are hoisted to the top (and spilled)
         asm volatile("" ::: "memory");
 #ifndef MJRL_GAE_ABL_NOFWD
+        if (FWD) {
 #pragma unroll
-        for (int g = 0; g < LP_GB; ++g) acc = __dadd_rn(X[k % 3][g], acc);
+            for (int g = 0; g < LP_GB; ++g) acc = __dadd_rn(X[k % 3][g], acc);
+        }
 #endif
-    }
-    return acc;
-}
-
-// Backward (returns / advantages, acc = x + c * acc) over the whole window with no
-// step mask: a partial window (the path's first steps) holds its valid steps at
-// u >= vmin = W - left, which the chain meets first; what it computes below them is
-// never stored, and the path's chain ends there.  The LDS reads of batch k + 2 are
-// issued before batch k's serial steps (sched_barrier keeps the compiler from sinking
-// them to their use).  The outputs leave for HBM from the chain wave itself, a batch
-// at a time in 16-byte stores: an LDS write costs the wave ~13 cycles a step against
-// ~2 for the reads and ~5 for the global stores (profiles/r06c/gae_latency.txt, the
-// lanes rows).  out points at the window's step u = 0 (t = e - (j + 1) W).  PLAIN
-// (no GAE): wave 0 also stores adv = ret - b, b from the TD row.  Batch k: u in
-// [W - (k + 1) GB, W - k GB).
-typedef double lp_d2 __attribute__((ext_vector_type(2), aligned(8)));
-template <bool PLAIN>
-__device__ __forceinline__ double lp_chain_bwd(const double* __restrict__ row, const double* __restrict__ brow,
-                                               double acc, double c, double* out, double* out2, int vmin) {
-    constexpr int NB = LP_W / LP_GB;
-    constexpr int NQ = PLAIN ? 3 : 1;
-    double X[3][LP_GB], B[NQ][LP_GB];
+        if (!FWD) {
+            ck[k * LP_PATHS] = acc;
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-#pragma unroll
-        for (int g = 0; g < LP_GB; ++g) {
-            X[k][g] = row[LP_W - (k + 1) * LP_GB + g];
-            if (PLAIN) B[k % NQ][g] = brow[LP_W - (k + 1) * LP_GB + g];
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < NB; ++k) {
-        if (k + 2 < NB) {
-#pragma unroll
-            for (int g = 0; g < LP_GB; ++g) {
-                X[(k + 2) % 3][g] = row[LP_W - (k + 3) * LP_GB + g];
-                if (PLAIN) B[(k + 2) % NQ][g] = brow[LP_W - (k + 3) * LP_GB + g];
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int g = LP_GB - 1; g >= 0; --g) {
-            acc = __dadd_rn(X[k % 3][g], __dmul_rn(c, acc));
-            X[k % 3][g] = acc;
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        const int lo = LP_W - (k + 1) * LP_GB;
-#ifdef MJRL_GAE_ABL_NOSTORE
-        if (lo < -1) {   // timing ablation: the outputs' stores skipped
-#else
-        if (lo >= vmin) {
-#endif
-#pragma unroll
-            for (int g = 0; g < LP_GB; g += 2) {
-                *(lp_d2*)(out + lo + g) = lp_d2{X[k % 3][g], X[k % 3][g + 1]};
-                if (PLAIN)   // plain advantages: ret - b (process_samples.py:31-32)
-                    *(lp_d2*)(out2 + lo + g) = lp_d2{__dsub_rn(X[k % 3][g], B[k % NQ][g]),
-                                                     __dsub_rn(X[k % 3][g + 1], B[k % NQ][g + 1])};
-            }
-        } else if (lo + LP_GB > vmin) {   // the batch holding the path's first step
-#pragma unroll
-            for (int g = 0; g < LP_GB; ++g) {
-                if (lo + g >= vmin) {
-                    out[lo + g] = X[k % 3][g];
-                    if (PLAIN) out2[lo + g] = __dsub_rn(X[k % 3][g], B[k % NQ][g]);
-                }
-            }
+            for (int g = LP_GB - 1; g >= 0; --g) acc = __dadd_rn(X[k % 3][g], __dmul_rn(c, acc));
         }
     }
     return acc;
@@ -680,15 +619,15 @@ __global__ void __launch_bounds__(LP_T) k_gae_lp(const double* __restrict__ rew,
                                                  double* __restrict__ ret, double* __restrict__ adv,
                                                  double* __restrict__ path_ret) {
     // buffer q of array A at A + q * LP_BUF: RB backward rewards, TD td (no GAE: the
-    // baseline), RF forward rewards
-    __shared__ double RB[2 * LP_BUF], TD[2 * LP_BUF], RF[2 * LP_BUF];
+    // baseline), RF forward rewards; CK[chain][window parity][segment][path]
+    __shared__ double RB[LP_NB * LP_BUF], TD[LP_NB * LP_BUF], RF[LP_NB * LP_BUF];
+    __shared__ double CK[2][2][LP_NS][LP_PATHS];
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar branches
     const int64_t p0 = (int64_t)blockIdx.x * LP_PATHS;
     const int np = (int)(P - p0 < LP_PATHS ? P - p0 : LP_PATHS);
     // the window count from the workgroup's path bounds (uniform addresses: scalar
-    // loads); each chain lane and mover reads its own path's bounds with a vector load,
-    // so the first window's loads wait on one HBM round trip and no barrier
+    // loads); chain lanes and movers read their own path's bounds with vector loads
     int64_t hmax = 0;
 #pragma unroll
     for (int i = 0; i < LP_PATHS; ++i) {
@@ -699,37 +638,32 @@ __global__ void __launch_bounds__(LP_T) k_gae_lp(const double* __restrict__ rew,
     }
     const int nwin = (int)((hmax + LP_W - 1) / LP_W);
     if (w < LP_CH) {
-        // ---- a chain wave: LDS reads, its own outputs' stores ----
+        // ---- a chain wave: LDS reads, one checkpoint write a segment ----
         const bool chain = lane < np && (w != 1 || use_gae);
         const double c = w == 0 ? gamma : gl;
-        double* const cw = (w == 0 ? RB : (w == 1 ? TD : RF)) + lane * LP_LD;
-        const int64_t lb = lane < np ? off[p0 + lane] : 0, le = lane < np ? off[p0 + lane + 1] : 0;
-        double* const o1 = w == 0 ? ret : adv;
+        const double* const cw = (w == 0 ? RB : (w == 1 ? TD : RF)) + lane * LP_LD;
         double acc = 0.0;
         __syncthreads();   // window 0 put
-        for (int j = 0; j < nwin; ++j) {
-            if (chain) {
-                double* const row = cw + (j & 1) * LP_BUF;
-                const int64_t t0 = le - (int64_t)(j + 1) * LP_W;   // the window's u = 0
-                const int64_t vm = lb - t0;                         // first valid u
-                const int vmin = (int)(vm < 0 ? 0 : (vm > LP_W ? LP_W : vm));
+        for (int i = 0; i < nwin; ++i) {
 #ifdef MJRL_GAE_ABL_NOCHAIN
-                if (j >= 0) continue;   // timing ablation: the chains skipped, barriers kept
+            if (i >= 0) {   // timing ablation: the chains skipped, barriers kept
+                __syncthreads();
+                continue;
+            }
 #endif
+            if (chain) {
+                const double* const row = cw + (i % LP_NB) * LP_BUF;
                 if (w == 2)
-                    acc = lp_chain<true>(row, acc, c);
-                else if (w == 1 || use_gae)
-                    acc = lp_chain_bwd<false>(row, nullptr, acc, c, o1 + t0, nullptr, vmin);
+                    acc = lp_chain<true>(row, acc, c, nullptr);
                 else
-                    acc = lp_chain_bwd<true>(row, TD + (j & 1) * LP_BUF + lane * LP_LD, acc, c, ret + t0,
-                                             adv + t0, vmin);
+                    acc = lp_chain<false>(row, acc, c, &CK[w][i & 1][0][lane]);
             }
             __syncthreads();
         }
         if (w == 2 && lane < np) path_ret[p0 + lane] = acc;
         return;
     }
-    // ---- a mover: every global load ----
+    // ---- a mover: every global load, the recompute, every output store ----
     const int m = (w - LP_CH) * 64 + lane;
     const int mp = m / LP_TPP, mu = m % LP_TPP;
     const bool okp = mp < np;
@@ -737,7 +671,7 @@ __global__ void __launch_bounds__(LP_T) k_gae_lp(const double* __restrict__ rew,
     // b1's last entry: 0 if terminated else b[-1] (process_samples.py:24-27)
     const double pbl = de > db ? (term[p0 + mp] ? 0.0 : base[de - 1]) : 0.0;
     // an empty path (or a thread past the last path) reads index 0: valid whenever a
-    // window exists, and never used (the chains skip its steps)
+    // window exists, and never used (nothing is stored for its steps)
     const int64_t pb = de > db ? db : 0, pe = de > db ? de : 1;
     double xr[LP_PER], xb[LP_PER], xn[LP_PER], xf[LP_PER];
     auto load = [&](int j) {
@@ -757,7 +691,7 @@ __global__ void __launch_bounds__(LP_T) k_gae_lp(const double* __restrict__ rew,
         }
     };
     auto put = [&](int j) {
-        const int q = (j & 1) * LP_BUF + mp * LP_LD;
+        const int q = (j % LP_NB) * LP_BUF + mp * LP_LD;
 #pragma unroll
         for (int k = 0; k < LP_PER; ++k) {
             const int u = mu + LP_TPP * k;
@@ -770,198 +704,68 @@ __global__ void __launch_bounds__(LP_T) k_gae_lp(const double* __restrict__ rew,
             RF[q + u] = (int64_t)j * LP_W + u < plen ? xf[k] : 0.0;
         }
     };
+    // recompute task: chain rc (0 returns from RB, 1 advantages from TD), path rp,
+    // segment rs (u in [rs GB, (rs + 1) GB) = the chain's batch k = NS - 1 - rs)
+    const int rc = m / (LP_PATHS * LP_NS), rp = (m / LP_NS) % LP_PATHS, rs = m % LP_NS;
+    const bool rok = rp < np && (rc == 0 || use_gae) && rc < 2;
+    const int64_t rb = rok ? off[p0 + rp] : 0, re = rok ? off[p0 + rp + 1] : 0;
+    const double rcoef = rc == 0 ? gamma : gl;
+    double* const rout = rc == 0 ? ret : adv;
+    auto recompute = [&](int j) {
+        if (!rok) return;
+        const int q = (j % LP_NB) * LP_BUF + rp * LP_LD + rs * LP_GB;
+        const double* const row = (rc == 0 ? RB : TD) + q;
+        double x[LP_GB], bb[LP_GB];
+#pragma unroll
+        for (int g = 0; g < LP_GB; ++g) {
+            x[g] = row[g];
+            if (!use_gae) bb[g] = TD[q + g];   // plain: the baseline, for ret - b
+        }
+        double acc = CK[rc][j & 1][LP_NS - 1 - rs][rp];
+#pragma unroll
+        for (int g = LP_GB - 1; g >= 0; --g) {
+            acc = __dadd_rn(x[g], __dmul_rn(rcoef, acc));
+            x[g] = acc;
+        }
+        // step t = e - (j + 1) W + rs GB + g, stored when t >= b
+        const int64_t t0 = re - (int64_t)(j + 1) * LP_W + rs * LP_GB;
+        double* const o = rout + t0;
+        double* const o2 = adv + t0;
+        if (t0 >= rb) {
+#pragma unroll
+            for (int g = 0; g < LP_GB; g += 2) {
+                *(lp_d2*)(o + g) = lp_d2{x[g], x[g + 1]};
+                if (!use_gae)   // plain advantages: ret - b (process_samples.py:31-32)
+                    *(lp_d2*)(o2 + g) = lp_d2{__dsub_rn(x[g], bb[g]), __dsub_rn(x[g + 1], bb[g + 1])};
+            }
+        } else if (t0 + LP_GB > rb) {   // the segment holding the path's first step
+#pragma unroll
+            for (int g = 0; g < LP_GB; ++g) {
+                if (t0 + g >= rb) {
+                    o[g] = x[g];
+                    if (!use_gae) o2[g] = __dsub_rn(x[g], bb[g]);
+                }
+            }
+        }
+    };
     if (nwin > 0) {
         load(0);
         put(0);
     }
     if (nwin > 1) load(1);
     __syncthreads();   // window 0 put
-    for (int j = 0; j < nwin; ++j) {
-        // the chains run window j (buffer j & 1); the other buffer held window j - 1
-#if defined(MJRL_GAE_ABL_NOPUT) || defined(MJRL_GAE_ABL_NOLOAD)
-        // timing ablations: the movers' puts (NOPUT) or puts and loads (NOLOAD) skipped
-#else
-        if (j + 1 < nwin) put(j + 1);
-#endif
+    for (int i = 0; i < nwin; ++i) {
+        // the chains run window i (buffer i % 3); buffer (i - 1) % 3 holds window i - 1,
+        // whose checkpoints are CK[.][(i - 1) & 1]; put(i + 1) fills the third buffer
+        if (i >= 1) recompute(i - 1);
 #ifndef MJRL_GAE_ABL_NOLOAD
-        if (j + 2 < nwin) load(j + 2);
+        if (i + 1 < nwin) put(i + 1);
+        if (i + 2 < nwin) load(i + 2);
 #endif
         __syncthreads();
     }
+    if (nwin > 0) recompute(nwin - 1);
 }
-
-#ifdef MJRL_GAE_LP4
-// Variant build only (-DMJRL_GAE_LP4, tools/gae_probe.py A/B): the first lanes-=-paths
-// kernel of round 6, in which all four waves load and store.
-// Lanes = paths (round 6): the serial recurrences of L4_PATHS paths run side by side
-// in ONE instruction stream each, one wave per chain — wave 0 the returns
-// (discount_sum(rewards, gamma)), wave 1 the advantages (discount_sum(td, gamma
-// lambda), or nothing without GAE), wave 2 the path-return sum (front to back) —
-// each lane one path; wave 3 only loads and stores.  A dependent fp64 multiply -> add costs ~10 cycles of issue
-// per step for the whole wave (tools/gae_latency.hip), so L4_PATHS paths advance for the
-// price k_gae paid for one.  The paths' steps come through LDS in windows of L4_W
-// steps per path (backward windows aligned at each path's end, forward windows at
-// its start): all four waves load window j + 1 into registers (each instruction 8
-// paths' runs of 8 consecutive steps) while the chains consume window j, then store it (td formed on
-// the way) after a barrier; the chains write their outputs in place, and the
-// window leaves for HBM with coalesced writes.  Bit-identical to k_gae: the same
-// __dmul_rn / __dadd_rn / __dsub_rn per step in the same order.
-constexpr int L4_PATHS = 8;               // paths per workgroup (lanes 0..7 of each chain wave)
-constexpr int L4_W = 256;                 // steps per window: a window's chain covers the HBM latency
-                                          // of the next window's loads; 512-step windows held 64 loads a
-                                          // thread, more than the registers beside the chain (the chain
-                                          // then waited on half of them, r06c/gae_probe.txt)
-constexpr int L4_LD = L4_W + 1;           // LDS row stride (doubles): chain lanes conflict-free
-constexpr int L4_GB = 16;                 // chain steps per register batch
-constexpr int L4_T = 256;                 // 4 waves: three chain waves, all four load / store
-constexpr int L4_PER = L4_PATHS * L4_W / L4_T;   // window elements per thread per array
-static_assert(L4_PATHS * L4_W % L4_T == 0 && L4_W % 64 == 0, "window split");
-
-__global__ void __launch_bounds__(L4_T) k_gae_lp4(const double* __restrict__ rew, const double* __restrict__ base,
-                                                 const int64_t* __restrict__ off, const uint8_t* __restrict__ term,
-                                                 int64_t P, double gamma, double gl, int use_gae,
-                                                 double* __restrict__ ret, double* __restrict__ adv,
-                                                 double* __restrict__ path_ret) {
-    __shared__ double RB[L4_PATHS * L4_LD];   // backward rewards -> returns (in place)
-    __shared__ double TD[L4_PATHS * L4_LD];   // td -> advantages (in place); no GAE: the baseline
-    __shared__ double RF[L4_PATHS * L4_LD];   // forward rewards
-    __shared__ int64_t sb[L4_PATHS], se[L4_PATHS];
-    __shared__ double sbl[L4_PATHS];          // b1's last entry: 0 if terminated else b[-1]
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int64_t p0 = (int64_t)blockIdx.x * L4_PATHS;
-    const int np = (int)(P - p0 < L4_PATHS ? P - p0 : L4_PATHS);
-    if (tid < L4_PATHS) {
-        const bool ok = tid < np;
-        const int64_t b = ok ? off[p0 + tid] : 0, e = ok ? off[p0 + tid + 1] : 0;
-        sb[tid] = b;
-        se[tid] = e;
-        sbl[tid] = e > b ? (term[p0 + tid] ? 0.0 : base[e - 1]) : 0.0;
-    }
-    __syncthreads();
-    int64_t hmax = 0;
-    for (int i = 0; i < np; ++i) hmax = se[i] - sb[i] > hmax ? se[i] - sb[i] : hmax;
-    const int nwin = (int)((hmax + L4_W - 1) / L4_W);
-    // this thread's path (L4_TPP threads a path) and its steps u = mu + L4_TPP k of every
-    // window: each load instruction reads runs of L4_TPP consecutive steps
-    constexpr int L4_TPP = L4_T / L4_PATHS;
-    const int mp = tid / L4_TPP, mu = tid % L4_TPP;
-    // an empty path (or a lane past the last path) reads index 0: valid whenever a
-    // window exists, and never used (the chains and the drain skip its steps)
-    const int64_t pb = se[mp] > sb[mp] ? sb[mp] : 0, pe = se[mp] > sb[mp] ? se[mp] : 1;
-    const double pbl = sbl[mp];
-    const int64_t plen = se[mp] - sb[mp];
-    double xr[L4_PER], xb[L4_PER], xn[L4_PER], xf[L4_PER];
-    auto load = [&](int j) {
-        // backward window: step t = e - (j + 1) W + u; forward window: t = b + j W + u;
-        // loads from clamped indices, unconditional (no exec-masked loads in the stream)
-#pragma unroll
-        for (int k = 0; k < L4_PER; ++k) {
-            const int u = mu + L4_TPP * k;
-            int64_t tb = pe - (int64_t)(j + 1) * L4_W + u, tf = pb + (int64_t)j * L4_W + u;
-            tb = tb < pb ? pb : tb;
-            tf = tf < pe ? tf : pe - 1;
-            const int64_t tn = tb + 1 < pe ? tb + 1 : pe - 1;
-            xr[k] = rew[tb];
-            xb[k] = base[tb];
-            xn[k] = base[tn];
-            xf[k] = rew[tf];
-        }
-    };
-    auto put = [&](int j) {
-#pragma unroll
-        for (int k = 0; k < L4_PER; ++k) {
-            const int u = mu + L4_TPP * k;
-            const int64_t tb = pe - (int64_t)(j + 1) * L4_W + u;
-            const double bn = tb + 1 < pe ? xn[k] : pbl;   // b1[t + 1] (process_samples.py:24-27)
-            RB[mp * L4_LD + u] = xr[k];
-            // GAE td = r + gamma * b1[t+1] - b1[t] (process_samples.py:28); plain: b
-            TD[mp * L4_LD + u] = use_gae ? __dsub_rn(__dadd_rn(xr[k], __dmul_rn(gamma, bn)), xb[k]) : xb[k];
-            // past the path's end: 0.0, which the forward sum adds exactly (acc is never -0.0)
-            RF[mp * L4_LD + u] = (int64_t)j * L4_W + u < plen ? xf[k] : 0.0;
-        }
-    };
-    const int64_t db = sb[mp], de = se[mp];
-    auto drain = [&](int j) {   // window j's outputs (in RB / TD) to HBM
-#pragma unroll
-        for (int k = 0; k < L4_PER; ++k) {
-            const int u = mu + L4_TPP * k;
-            const int64_t tb = de - (int64_t)(j + 1) * L4_W + u;
-            if (tb >= db) {
-                const double rr = RB[mp * L4_LD + u];
-                ret[tb] = rr;
-                adv[tb] = use_gae ? TD[mp * L4_LD + u] : __dsub_rn(rr, TD[mp * L4_LD + u]);   // plain: ret - b
-            }
-        }
-    };
-    // the chains: wave 0 returns, wave 1 advantages, wave 2 the path-return sum
-    const bool chain = w < 3 && lane < np && (w != 1 || use_gae);
-    const double c = w == 0 ? gamma : gl;
-    double* cw = w == 0 ? RB : (w == 1 ? TD : RF);
-    double acc = 0.0;
-    if (nwin > 0) {
-        load(0);
-        put(0);
-    }
-    __syncthreads();
-    for (int j = 0; j < nwin; ++j) {
-        if (j + 1 < nwin) load(j + 1);   // in flight under the chains
-        if (chain) {
-            // the window's steps come into registers in batches of L4_GB (the next
-            // batch's LDS reads issued before this batch's serial steps), so only the
-            // dependent fp64 multiply -> add is on the critical path
-            double* row = cw + lane * L4_LD;
-            if (w == 2) {
-                // front to back: Python's sum(p["rewards"]) (npg_cg.py:97); x + 1.0 * acc is
-                // x + acc exactly (k_gae's form); the steps past the path's end hold 0.0
-                double x[L4_GB], xn2[L4_GB];
-#pragma unroll
-                for (int g = 0; g < L4_GB; ++g) x[g] = row[g];
-#pragma unroll
-                for (int u0 = 0; u0 < L4_W; u0 += L4_GB) {
-                    if (u0 + L4_GB < L4_W) {
-#pragma unroll
-                        for (int g = 0; g < L4_GB; ++g) xn2[g] = row[u0 + L4_GB + g];
-                    }
-#pragma unroll
-                    for (int g = 0; g < L4_GB; ++g) acc = __dadd_rn(x[g], acc);
-#pragma unroll
-                    for (int g = 0; g < L4_GB; ++g) x[g] = xn2[g];
-                }
-            } else {
-                // the backward recurrence over the whole window with no step mask: a
-                // partial window (the path's first steps) holds its valid steps at
-                // u >= W - left, which the chain meets first; what it computes below
-                // them is never drained, and the path's chain ends there
-                double x[L4_GB], xn2[L4_GB];
-#pragma unroll
-                for (int g = 0; g < L4_GB; ++g) x[g] = row[L4_W - L4_GB + g];
-#pragma unroll
-                for (int u0 = L4_W - L4_GB; u0 >= 0; u0 -= L4_GB) {
-                    if (u0 >= L4_GB) {
-#pragma unroll
-                        for (int g = 0; g < L4_GB; ++g) xn2[g] = row[u0 - L4_GB + g];
-                    }
-#pragma unroll
-                    for (int g = L4_GB - 1; g >= 0; --g) {
-                        acc = __dadd_rn(x[g], __dmul_rn(c, acc));
-                        x[g] = acc;
-                    }
-#pragma unroll
-                    for (int g = 0; g < L4_GB; ++g) row[u0 + g] = x[g];
-#pragma unroll
-                    for (int g = 0; g < L4_GB; ++g) x[g] = xn2[g];
-                }
-            }
-        }
-        __syncthreads();
-        drain(j);
-        if (j + 1 < nwin) put(j + 1);
-        __syncthreads();
-    }
-    if (w == 2 && lane < np) path_ret[p0 + lane] = acc;
-}
-
-#endif
 
 // Moments pass 1: per-block partials of sum(x-c), sum((x-c)^2), min, max.
 template <typename T>
@@ -1643,15 +1447,9 @@ int mjrl_gae(const double* rew, const double* base, const int64_t* path_off, con
         return MJRL_EINVAL;
     if (P == 0) return MJRL_OK;
     const double gl = gamma * gae_lambda;   // python: gamma*gae_lambda (process_samples.py:29)
-#ifdef MJRL_GAE_LP4
-    const int64_t g = (P + L4_PATHS - 1) / L4_PATHS;
-    hipLaunchKernelGGL(k_gae_lp4, dim3((unsigned)g), dim3(L4_T), 0, (hipStream_t)stream, rew, base, path_off,
-                       terminated, P, gamma, gl, use_gae, ret, adv, path_ret);
-#else
     const int64_t g = (P + LP_PATHS - 1) / LP_PATHS;
     hipLaunchKernelGGL(k_gae_lp, dim3((unsigned)g), dim3(LP_T), 0, (hipStream_t)stream, rew, base, path_off,
                        terminated, P, gamma, gl, use_gae, ret, adv, path_ret);
-#endif
     return err(hipGetLastError());
 }
 

@@ -1614,8 +1614,8 @@ int mjrl_debug_kx_prof(unsigned long long* out) {
 int mjrl_build_flags(void) {
     int f = 0;
 #if defined(MJRL_KX_ABL_NOP1) || defined(MJRL_KX_ABL_NOP6) || defined(MJRL_KX_ABL_NOCHAIN) || \
-    defined(MJRL_KX_ABL_NOCOLS) || defined(MJRL_GAE_ABL_NOPUT) || defined(MJRL_GAE_ABL_NOLOAD) ||  \
-    defined(MJRL_GAE_ABL_NOCHAIN) || defined(MJRL_GAE_ABL_NOFWD) || defined(MJRL_GAE_ABL_NOSTORE)
+    defined(MJRL_KX_ABL_NOCOLS) || defined(MJRL_GAE_ABL_NOLOAD) || defined(MJRL_GAE_ABL_NOCHAIN) ||   \
+    defined(MJRL_GAE_ABL_NOFWD)
     f |= MJRL_BUILD_ABLATION;
 #endif
 #ifdef MJRL_KX_PROF

@@ -5,7 +5,7 @@
 OUT=gpurun_out/${1:-gae_abl}
 mkdir -p $OUT
 export GAE_PROBE_ONLY=1
-for v in "" _nofwd _nostore _nochain; do
+for v in "" _nofwd _nochain; do
   if [ -z "$v" ]; then LIBV=mjrl_amd/lib/libmjrl_amd.so; NC=0; else LIBV=mjrl_amd/lib/libmjrl_amd$v.so; NC=1; fi
   [ "$v" = _w384 ] && NC=0
   echo "build: ${v:-default}"

@@ -1020,26 +1020,101 @@ __global__ void __launch_bounds__(MOM_THREADS) k_whiten_mom(const double* __rest
 
 // Small batches: the two moment passes (advantages and path returns) and the
 // whitening with its output moments in ONE workgroup and one launch (three before:
-// k_moments2 twice, k_whiten_mom), bit-identical to them: the workgroup walks
-// their blocks one after another with the same per-block arithmetic (mom_block,
-// whiten_block) and folds the partials with the same mom_fold, in the same order.
+// k_moments2 twice, k_whiten_mom), bit-identical to them.  The workgroup's thread t
+// plays thread t of every block of those launches AT ONCE (SM_NB <= 16 blocks when
+// T <= 65,536: mom2_grid), each block's per-thread sum in its own order (mom_block,
+// whiten_block), then every block's block_sum / min / max from one LDS exchange, in
+// block_sum's order; the partials fold with the same mom_fold.  (Walking the blocks
+// one after another paid a load latency and four barriers per block: 81 us for the
+// 12.5k-row Swimmer batch against 21 us for the three launches, profiles/r06d.)
+constexpr int SM_NB = 16;
+static_assert(MOM_THREADS == 256, "the LDS exchange below assumes four waves");
+
+template <bool WHITEN>
+__device__ __forceinline__ void mom_blocks_all(const double* __restrict__ x, int64_t N, double c, double den,
+                                               int nb, float* __restrict__ adv32, double* __restrict__ w64,
+                                               double* part, double (*xr)[4][4]) {
+    double s1[SM_NB], s2[SM_NB], mn[SM_NB], mx[SM_NB];
+#pragma unroll
+    for (int b = 0; b < SM_NB; ++b) {
+        s1[b] = 0.0;
+        s2[b] = 0.0;
+        mn[b] = __builtin_inf();
+        mx[b] = -__builtin_inf();
+    }
+    const int64_t stride = (int64_t)nb * MOM_THREADS;
+    for (int64_t i0 = threadIdx.x; i0 < N; i0 += stride) {   // element k of every block's sequence
+#pragma unroll
+        for (int b = 0; b < SM_NB; ++b) {
+            const int64_t i = i0 + (int64_t)b * MOM_THREADS;
+            if (b < nb && i < N) {
+                double v;
+                if (WHITEN) {   // whiten_block's arithmetic
+                    const double wv = (x[i] - c) / den;
+                    const float wf = (float)wv;
+                    adv32[i] = wf;
+                    if (w64) w64[i] = wv;
+                    v = (double)wf;
+                    s1[b] += v;
+                    s2[b] += v * v;
+                } else {        // mom_block's
+                    v = x[i];
+                    const double dv = v - c;
+                    s1[b] += dv;
+                    s2[b] += dv * dv;
+                }
+                mn[b] = fmin(mn[b], v);
+                mx[b] = fmax(mx[b], v);
+            }
+        }
+    }
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+#pragma unroll
+    for (int b = 0; b < SM_NB; ++b) {
+        if (b < nb) {
+            const double a = wave_sum(s1[b]), q = wave_sum(s2[b]);
+            double lo = mn[b], hi = mx[b];
+#pragma unroll
+            for (int k = 32; k > 0; k >>= 1) {
+                lo = fmin(lo, __shfl_xor(lo, k, 64));
+                hi = fmax(hi, __shfl_xor(hi, k, 64));
+            }
+            if (l == 0) {
+                xr[b][w][0] = a;
+                xr[b][w][1] = q;
+                xr[b][w][2] = lo;
+                xr[b][w][3] = hi;
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < nb) {   // block b's partial as its thread 0 formed it
+        const int b = threadIdx.x;
+        double a = 0.0, q = 0.0, lo = xr[b][0][2], hi = xr[b][0][3];
+#pragma unroll
+        for (int i = 0; i < MOM_THREADS / 64; ++i) {
+            a += xr[b][i][0];
+            q += xr[b][i][1];
+            lo = fmin(lo, xr[b][i][2]);
+            hi = fmax(hi, xr[b][i][3]);
+        }
+        part[4 * b + 0] = a;
+        part[4 * b + 1] = q;
+        part[4 * b + 2] = lo;
+        part[4 * b + 3] = hi;
+    }
+    __syncthreads();
+}
+
 __global__ void __launch_bounds__(MOM_THREADS) k_mom_whiten_small(
     const double* __restrict__ adv, int64_t T, const double* __restrict__ pr, int64_t P, double eps,
     float* __restrict__ adv32, double* __restrict__ w64, int nb1, int nb2, double* part, double* m1, double* pm1,
     double* m2, double* pm2, double* ms) {
-    __shared__ double red[MOM_THREADS / 64];
-    double o[4];
+    __shared__ double xr[SM_NB][4][4];
     for (int pass = 0; pass < 2; ++pass) {
         const double c1 = pass ? m1[0] / m1[2] : 0.0, c2 = pass ? pm1[0] / pm1[2] : 0.0;
-        for (int b = 0; b < nb1 + nb2; ++b) {
-            if (b < nb1)
-                mom_block(adv, T, c1, b, nb1, red, o);
-            else
-                mom_block(pr, P, c2, b - nb1, nb2, red, o);
-            if (threadIdx.x == 0)
-                for (int k = 0; k < 4; ++k) part[4 * b + k] = o[k];
-        }
-        __syncthreads();
+        mom_blocks_all<false>(adv, T, c1, 0.0, nb1, nullptr, nullptr, part, xr);
+        mom_blocks_all<false>(pr, P, c2, 0.0, nb2, nullptr, nullptr, part + 4 * nb1, xr);
         if (threadIdx.x < 64) {
             mom_fold(part, 0, nb1, T, pass ? m2 : m1);
             mom_fold(part, nb1, nb1 + nb2, P, pass ? pm2 : pm1);
@@ -1048,12 +1123,7 @@ __global__ void __launch_bounds__(MOM_THREADS) k_mom_whiten_small(
     }
     const double mean = m1[0] / m1[2];
     const double den = sqrt(m2[1] / m1[2]) + eps;
-    for (int b = 0; b < nb1; ++b) {
-        whiten_block(adv, T, mean, den, b, nb1, adv32, w64, red, o);
-        if (threadIdx.x == 0)
-            for (int k = 0; k < 4; ++k) part[4 * b + k] = o[k];
-    }
-    __syncthreads();
+    mom_blocks_all<true>(adv, T, mean, den, nb1, adv32, w64, part, xr);
     if (threadIdx.x < 64) mom_fold(part, 0, nb1, T, ms);
 }
 
@@ -1507,7 +1577,7 @@ int mjrl_moments_whiten_small(const double* adv, int64_t T, const double* path_r
         return MJRL_EINVAL;
     const int nb1 = grid_for(T, MOM_THREADS * 4, mom2_grid(T));
     const int nb2 = grid_for(P, MOM_THREADS * 4, mom2_grid(P));
-    if (nb1 + nb2 > MOM2_MAXB) return MJRL_EINVAL;
+    if (nb1 > SM_NB || nb2 > SM_NB) return MJRL_EINVAL;   // T, P <= 65,536
     hipLaunchKernelGGL(k_mom_whiten_small, dim3(1), dim3(MOM_THREADS), 0, (hipStream_t)stream, adv, T, path_ret, P,
                        eps, adv32, w64, nb1, nb2, rpart, m1, pm1, m2, pm2, ms);
     return err(hipGetLastError());

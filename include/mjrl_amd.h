@@ -240,8 +240,9 @@ int mjrl_whiten_moments(const double* adv, int64_t T, const double* m1, const do
 /* For small batches (UpdateEngine: T <= 65536): mjrl_moments2 twice (path returns
  * beside the advantages, centred at the first pass's means) and
  * mjrl_whiten_moments in ONE single-workgroup launch, bit-identical to the three
- * (the same blocks, walked in turn, and the same folds): m1 / pm1 / m2 / pm2 / ms
- * are their out1 / out2 / out arguments. */
+ * (the same blocks' sums and the same folds, formed inside the workgroup): m1 / pm1
+ * / m2 / pm2 / ms are their out1 / out2 / out arguments.  T, P <= 65536; rpart is
+ * not used (kept for the signature). */
 int mjrl_moments_whiten_small(const double* adv, int64_t T, const double* path_ret, int64_t P, double eps,
                               float* adv32, double* w64, double* rpart, double* m1, double* pm1, double* m2,
                               double* pm2, double* ms, void* stream);

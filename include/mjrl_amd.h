@@ -237,15 +237,6 @@ int mjrl_moments2(const double* x1, int64_t N1, const double* c1, const double* 
                   const double* c2, double* rpart, double* out1, double* out2, void* stream);
 int mjrl_whiten_moments(const double* adv, int64_t T, const double* m1, const double* m2, double eps,
                         float* adv32, double* w64, double* rpart, double* out, void* stream);
-/* For small batches (UpdateEngine: T <= 65536): mjrl_moments2 twice (path returns
- * beside the advantages, centred at the first pass's means) and
- * mjrl_whiten_moments in ONE single-workgroup launch, bit-identical to the three
- * (the same blocks' sums and the same folds, formed inside the workgroup): m1 / pm1
- * / m2 / pm2 / ms are their out1 / out2 / out arguments.  T, P <= 65536; rpart is
- * not used (kept for the signature). */
-int mjrl_moments_whiten_small(const double* adv, int64_t T, const double* path_ret, int64_t P, double eps,
-                              float* adv32, double* w64, double* rpart, double* m1, double* pm1, double* m2,
-                              double* pm2, double* ms, void* stream);
 
 /* Sharded moments in ONE collective (npg_cg.py:91, 97-102 over the union of the
  * shards): each rank runs pass 1 (center null) and pass 2 centred on its OWN mean

@@ -68,7 +68,6 @@ SIGNATURES = {
     "mjrl_moments_f32": [P, I64, P, P, P, P],
     "mjrl_moments2": [P, I64, P, P, I64, P, P, P, P, P],
     "mjrl_whiten_moments": [P, I64, P, P, F64, P, P, P, P, P],
-    "mjrl_moments_whiten_small": [P, I64, P, I64, F64, P, P, P, P, P, P, P, P, P],
     "mjrl_moments_combine": [P, I32, I32, I32, P, P],
     "mjrl_whiten": [P, I64, P, P, F64, P, P, P],
     "mjrl_dapg_adv": [P, I64, P, P, I64, F64, P, P],

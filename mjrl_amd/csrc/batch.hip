@@ -1018,144 +1018,6 @@ __global__ void __launch_bounds__(MOM_THREADS) k_whiten_mom(const double* __rest
     }
 }
 
-// Small batches: the two moment passes (advantages and path returns) and the
-// whitening with its output moments in ONE workgroup and one launch (three before:
-// k_moments2 twice, k_whiten_mom), bit-identical to them.  The workgroup's thread t
-// plays thread t of every block of those launches at once (nb <= SM_NB = 16 blocks
-// when T <= 65,536: mom2_grid): each block's per-thread sum in its own order
-// (mom_block, whiten_block), its loads issued SM_KC elements of every block at a
-// time; then every block's block_sum / min / max from one LDS exchange in
-// block_sum's order, and mom_fold's fold of the partials by wave 0 from registers
-// (the partials never leave the CU).  Walking the blocks one after another paid a
-// load latency and four barriers per block: 81 us at the 12.5k-row Swimmer batch
-// against 21 us for the three launches (profiles/r06d/cfg).
-constexpr int SM_NB = 16;
-constexpr int SM_KC = 2;
-static_assert(MOM_THREADS == 256, "the LDS exchange below assumes four waves");
-
-template <bool WHITEN>
-__device__ __forceinline__ void mom_all(const double* __restrict__ x, int64_t N, double c, double den, int nb,
-                                        float* __restrict__ adv32, double* __restrict__ w64, double (*xr)[4][4],
-                                        double* __restrict__ out, double* bc) {
-    double s1[SM_NB], s2[SM_NB], mn[SM_NB], mx[SM_NB];
-#pragma unroll
-    for (int b = 0; b < SM_NB; ++b) {
-        s1[b] = 0.0;
-        s2[b] = 0.0;
-        mn[b] = __builtin_inf();
-        mx[b] = -__builtin_inf();
-    }
-    const int64_t stride = (int64_t)nb * MOM_THREADS;
-    for (int64_t i0 = threadIdx.x; i0 < N; i0 += SM_KC * stride) {   // elements k .. k + KC - 1 of every block
-        double v[SM_KC][SM_NB];
-#pragma unroll
-        for (int k = 0; k < SM_KC; ++k) {
-#pragma unroll
-            for (int b = 0; b < SM_NB; ++b) {
-                const int64_t i = i0 + k * stride + (int64_t)b * MOM_THREADS;
-                v[k][b] = x[i < N ? i : N - 1];   // clamped, unconditional
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < SM_KC; ++k) {
-#pragma unroll
-            for (int b = 0; b < SM_NB; ++b) {
-                const int64_t i = i0 + k * stride + (int64_t)b * MOM_THREADS;
-                if (b < nb && i < N) {
-                    double u;
-                    if (WHITEN) {   // whiten_block's arithmetic
-                        const double wv = (v[k][b] - c) / den;
-                        const float wf = (float)wv;
-                        adv32[i] = wf;
-                        if (w64) w64[i] = wv;
-                        u = (double)wf;
-                        s1[b] += u;
-                        s2[b] += u * u;
-                    } else {        // mom_block's
-                        u = v[k][b];
-                        const double dv = u - c;
-                        s1[b] += dv;
-                        s2[b] += dv * dv;
-                    }
-                    mn[b] = fmin(mn[b], u);
-                    mx[b] = fmax(mx[b], u);
-                }
-            }
-        }
-    }
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-#pragma unroll
-    for (int b = 0; b < SM_NB; ++b) {
-        if (b < nb) {
-            const double a = wave_sum(s1[b]), q = wave_sum(s2[b]);
-            double lo = mn[b], hi = mx[b];
-#pragma unroll
-            for (int k = 32; k > 0; k >>= 1) {
-                lo = fmin(lo, __shfl_xor(lo, k, 64));
-                hi = fmax(hi, __shfl_xor(hi, k, 64));
-            }
-            if (l == 0) {
-                xr[b][w][0] = a;
-                xr[b][w][1] = q;
-                xr[b][w][2] = lo;
-                xr[b][w][3] = hi;
-            }
-        }
-    }
-    __syncthreads();
-    if (w == 0) {
-        // lane b < nb: block b's partial as that block's thread 0 formed it (block_sum:
-        // 0.0 + the waves' sums in order; min / max from wave 0's, then every wave's)
-        double s = 0.0, q = 0.0, lo = __builtin_inf(), hi = -__builtin_inf();
-        if (l < nb) {
-            double a = 0.0, aq = 0.0, blo = xr[l][0][2], bhi = xr[l][0][3];
-#pragma unroll
-            for (int i = 0; i < MOM_THREADS / 64; ++i) {
-                a += xr[l][i][0];
-                aq += xr[l][i][1];
-                blo = fmin(blo, xr[l][i][2]);
-                bhi = fmax(bhi, xr[l][i][3]);
-            }
-            // mom_fold: each lane's running sums from 0.0 over its blocks (one here)
-            s += a;
-            q += aq;
-            lo = fmin(lo, blo);
-            hi = fmax(hi, bhi);
-        }
-        s = wave_sum(s);
-        q = wave_sum(q);
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            lo = fmin(lo, __shfl_xor(lo, o, 64));
-            hi = fmax(hi, __shfl_xor(hi, o, 64));
-        }
-        if (l == 0) {
-            const double r[6] = {s, q, (double)N, lo, hi, -lo};
-#pragma unroll
-            for (int k = 0; k < 6; ++k) {
-                out[k] = r[k];
-                bc[k] = r[k];
-            }
-        }
-    }
-    __syncthreads();
-}
-
-__global__ void __launch_bounds__(MOM_THREADS) k_mom_whiten_small(
-    const double* __restrict__ adv, int64_t T, const double* __restrict__ pr, int64_t P, double eps,
-    float* __restrict__ adv32, double* __restrict__ w64, int nb1, int nb2, double* m1, double* pm1, double* m2,
-    double* pm2, double* ms) {
-    __shared__ double xr[SM_NB][4][4];
-    __shared__ double bc[4][6];   // m1, pm1, m2, pm2 as written
-    mom_all<false>(adv, T, 0.0, 0.0, nb1, nullptr, nullptr, xr, m1, bc[0]);
-    mom_all<false>(pr, P, 0.0, 0.0, nb2, nullptr, nullptr, xr, pm1, bc[1]);
-    mom_all<false>(adv, T, bc[0][0] / bc[0][2], 0.0, nb1, nullptr, nullptr, xr, m2, bc[2]);
-    mom_all<false>(pr, P, bc[1][0] / bc[1][2], 0.0, nb2, nullptr, nullptr, xr, pm2, bc[3]);
-    const double mean = bc[0][0] / bc[0][2];
-    const double den = sqrt(bc[2][1] / bc[0][2]) + eps;
-    mom_all<true>(adv, T, mean, den, nb1, adv32, w64, xr, ms, bc[2]);
-}
-
 // adv32 = float((adv - mean) / (std + 1e-6)) (npg_cg.py:91; .float() at batch_reinforce.py:38)
 __global__ void __launch_bounds__(256) k_whiten(const double* __restrict__ adv, int64_t T,
                                                 const double* __restrict__ m1, const double* __restrict__ m2,
@@ -1596,19 +1458,6 @@ int mjrl_whiten_moments(const double* adv, int64_t T, const double* m1, const do
     const int nb = grid_for(T, MOM_THREADS * 4, mom2_grid(T));
     hipLaunchKernelGGL(k_whiten_mom, dim3(nb), dim3(MOM_THREADS), 0, (hipStream_t)stream, adv, T, m1, m2, eps, adv32,
                        w64, rpart, out);
-    return err(hipGetLastError());
-}
-
-int mjrl_moments_whiten_small(const double* adv, int64_t T, const double* path_ret, int64_t P, double eps,
-                              float* adv32, double* w64, double* rpart, double* m1, double* pm1, double* m2,
-                              double* pm2, double* ms, void* stream) {
-    if (T < 0 || P < 0 || !adv || !path_ret || !adv32 || !rpart || !m1 || !pm1 || !m2 || !pm2 || !ms)
-        return MJRL_EINVAL;
-    const int nb1 = grid_for(T, MOM_THREADS * 4, mom2_grid(T));
-    const int nb2 = grid_for(P, MOM_THREADS * 4, mom2_grid(P));
-    if (nb1 > SM_NB || nb2 > SM_NB) return MJRL_EINVAL;   // T, P <= 65,536; rpart is not used
-    hipLaunchKernelGGL(k_mom_whiten_small, dim3(1), dim3(MOM_THREADS), 0, (hipStream_t)stream, adv, T, path_ret, P,
-                       eps, adv32, w64, nb1, nb2, m1, pm1, m2, pm2, ms);
     return err(hipGetLastError());
 }
 

@@ -611,7 +611,6 @@ class DeviceBatch:
 
 # the forward pass assembles the split rows itself where it can (UpdateEngine._fused_pack)
 FUSED_PACK = os.environ.get("MJRL_AMD_FUSED_PACK", "1") != "0"
-SMALL_MOMENTS_ROWS = 65_536   # one-workgroup moments + whitening (mjrl_moments_whiten_small) up to this many rows
 TRPO_DEVICE_TRIALS = int(os.environ.get("MJRL_AMD_TRPO_DEVICE_TRIALS", "4"))   # see UpdateEngine.trpo_device_trials
 GRAPH_AUTO_ROWS = 300_000   # UpdateEngine.graphs == "auto": replay graphs up to this many rows (125k-row shard: 2.03 -> 1.97 ms; 1M rows: eager 4 % faster)
 HIDDEN_WIDTHS = (32, 64, 128, 256)   # hidden widths the row kernels are built for
@@ -1090,25 +1089,17 @@ class UpdateEngine:
             sp_ = lambda slot: C.c_void_p(self.stats[slot:].data_ptr())
             mp2 = _lib.ptr(self.mom2_part)
             dapg = algo == "dapg" and demo_coef is not None
-            if not sharded and T <= SMALL_MOMENTS_ROWS:
-                # small batches: both passes and the whitening in one single-workgroup
-                # launch (bit-identical to the three below; launch latency dominated them)
-                _lib.check(L.mjrl_moments_whiten_small(_lib.ptr(adv64), T, _lib.ptr(w["path_ret"]), P, 1e-6,
-                                                       _lib.ptr(w["adv32"]), _lib.ptr(w["w64"]) if dapg else None,
-                                                       mp2, sp_(S_M1), sp_(S_PM1), sp_(S_M2), sp_(S_PM2), sp_(S_MS),
-                                                       st), "mjrl_moments_whiten_small")
-            else:
-                _lib.check(L.mjrl_moments2(_lib.ptr(adv64), T, None, _lib.ptr(w["path_ret"]), P, None, mp2,
-                                           sp_(S_M1), sp_(S_PM1), st), "mjrl_moments2")
-                _lib.check(L.mjrl_moments2(_lib.ptr(adv64), T, sp_(S_M1), _lib.ptr(w["path_ret"]), P, sp_(S_PM1),
-                                           mp2, sp_(S_M2), sp_(S_PM2), st), "mjrl_moments2")
-                if sharded:
-                    self._sharded_moments(S_M1, 32, 2, st)
-                # whitening + surr_before = mean(LR * adv) with LR == 1 (npg_cg.py:113) in one
-                # launch; the surr_before all-reduce rides with the first post-step evaluation's
-                _lib.check(L.mjrl_whiten_moments(_lib.ptr(adv64), T, sp_(S_M1), sp_(S_M2), 1e-6,
-                                                 _lib.ptr(w["adv32"]), _lib.ptr(w["w64"]) if dapg else None, mp2,
-                                                 sp_(S_MS), st), "mjrl_whiten_moments")
+            _lib.check(L.mjrl_moments2(_lib.ptr(adv64), T, None, _lib.ptr(w["path_ret"]), P, None, mp2,
+                                       sp_(S_M1), sp_(S_PM1), st), "mjrl_moments2")
+            _lib.check(L.mjrl_moments2(_lib.ptr(adv64), T, sp_(S_M1), _lib.ptr(w["path_ret"]), P, sp_(S_PM1),
+                                       mp2, sp_(S_M2), sp_(S_PM2), st), "mjrl_moments2")
+            if sharded:
+                self._sharded_moments(S_M1, 32, 2, st)
+            # whitening + surr_before = mean(LR * adv) with LR == 1 (npg_cg.py:113) in one
+            # launch; the surr_before all-reduce rides with the first post-step evaluation's
+            _lib.check(L.mjrl_whiten_moments(_lib.ptr(adv64), T, sp_(S_M1), sp_(S_M2), 1e-6,
+                                             _lib.ptr(w["adv32"]), _lib.ptr(w["w64"]) if dapg else None, mp2,
+                                             sp_(S_MS), st), "mjrl_whiten_moments")
             ms_pending = [True]
             if dapg:
                 _lib.check(L.mjrl_moments2(_lib.ptr(w["w64"]), T, None, None, 0, None, mp2, sp_(S_MW1), None, st),

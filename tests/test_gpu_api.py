@@ -854,40 +854,3 @@ def test_staged_batch_matches_numpy(reuse):
         np.testing.assert_array_equal(rng[1], np.nanmax(obs, axis=0))
 
 
-@pytest.mark.parametrize("T,P", [(1, 1), (777, 5), (12500, 25), (40000, 200), (65536, 64)])
-@pytest.mark.parametrize("with_w64", [False, True])
-def test_moments_whiten_small_equals_three_launches(T, P, with_w64):
-    """mjrl_moments_whiten_small (small batches: both moment passes and the
-    whitening in one single-workgroup launch) writes bit for bit what
-    mjrl_moments2 x 2 + mjrl_whiten_moments write (npg_cg.py:91, 97-102, 113)."""
-    from mjrl_amd import _lib
-    L = _lib.lib()
-    rs = np.random.RandomState(T + P)
-    dev = torch.device("cuda:0")
-    adv = torch.from_numpy(rs.randn(T) * 7 + 3).to(dev)
-    pr = torch.from_numpy(rs.randn(P) * 50 - 4).to(dev)
-    outs = []
-    for small in (True, False):
-        part = torch.zeros(_lib.MOM_SCRATCH, dtype=torch.float64, device=dev)
-        st = torch.zeros(64, dtype=torch.float64, device=dev)
-        a32 = torch.zeros(T, dtype=torch.float32, device=dev)
-        w64 = torch.zeros(T, dtype=torch.float64, device=dev) if with_w64 else None
-        p = lambda k: C.c_void_p(st[k:].data_ptr())   # noqa: E731
-        sp = _lib.stream_ptr()
-        if small:
-            rc = L.mjrl_moments_whiten_small(_lib.ptr(adv), T, _lib.ptr(pr), P, 1e-6, _lib.ptr(a32),
-                                             _lib.ptr(w64) if with_w64 else None, _lib.ptr(part), p(0), p(8), p(16),
-                                             p(24), p(32), sp)
-            assert rc == 0
-        else:
-            assert L.mjrl_moments2(_lib.ptr(adv), T, None, _lib.ptr(pr), P, None, _lib.ptr(part), p(0), p(8), sp) == 0
-            assert L.mjrl_moments2(_lib.ptr(adv), T, p(0), _lib.ptr(pr), P, p(8), _lib.ptr(part), p(16), p(24),
-                                   sp) == 0
-            assert L.mjrl_whiten_moments(_lib.ptr(adv), T, p(0), p(16), 1e-6, _lib.ptr(a32),
-                                         _lib.ptr(w64) if with_w64 else None, _lib.ptr(part), p(32), sp) == 0
-        torch.cuda.synchronize()
-        outs.append((st.cpu().numpy(), a32.cpu().numpy(), None if w64 is None else w64.cpu().numpy()))
-    (s1, a1, w1), (s0, a0, w0) = outs
-    assert np.array_equal(s1[:38], s0[:38]) and np.array_equal(a1, a0)
-    assert w1 is None or np.array_equal(w1, w0)
-    np.testing.assert_allclose(s1[0] / s1[2], adv.cpu().numpy().mean(), rtol=1e-12)

@@ -208,6 +208,27 @@ int mjrl_linear_baseline_residual_f32x2(const float* obs, const float* obs_lo, c
                                         int32_t n, const int64_t* path_off, int64_t P, const double* coeffs,
                                         double* scratch, double* out, void* stream);
 
+/* QuadraticBaseline.fit (mjrl/baselines/quadratic_baseline.py:10-65) on the device:
+ * the same augmented Gram [F y]^T [F y] with the quadratic features o = clip(obs,
+ * +-10) / 10, [o, o_i o_j (i <= j, row-major), 1, a, a^2, a^3, a^4] (a = step
+ * within the path / 1000): out is K x K, K = n + n(n+1)/2 + 6; n <= 64.  The caller
+ * keeps the reference's lstsq retry loop on the (K-1) x (K-1) system.  _residual:
+ * r_t = y_t - F_t . coeffs (fit(return_errors=True)).  _f32: f32-staged
+ * observations, obs_lo their low halves (mjrl_host_stage_lo_paths_f64) or null.
+ * Scratch sizes from mjrl_quadratic_baseline_gram_scratch. */
+int mjrl_quadratic_baseline_gram_scratch(int32_t n, int64_t T, int64_t* doubles);
+int mjrl_quadratic_baseline_gram(const double* obs, const double* returns, int64_t T, int32_t n,
+                                 const int64_t* path_off, int64_t P, double* scratch, double* out, void* stream);
+int mjrl_quadratic_baseline_gram_f32(const float* obs, const float* obs_lo, const double* returns, int64_t T,
+                                     int32_t n, const int64_t* path_off, int64_t P, double* scratch, double* out,
+                                     void* stream);
+int mjrl_quadratic_baseline_residual(const double* obs, const double* returns, int64_t T, int32_t n,
+                                     const int64_t* path_off, int64_t P, const double* coeffs, double* scratch,
+                                     double* out, void* stream);
+int mjrl_quadratic_baseline_residual_f32(const float* obs, const float* obs_lo, const double* returns, int64_t T,
+                                         int32_t n, const int64_t* path_off, int64_t P, const double* coeffs,
+                                         double* scratch, double* out, void* stream);
+
 /* ---- subsampled Fisher rows (npg_cg.py:58-62: obs[rand_idx], act[rand_idx]) ----
  * dst row i = src row idx[i] for i < n, rows of row_bytes bytes (a multiple of 4);
  * indices may repeat (np.random.choice draws with replacement).  Used to build

@@ -100,6 +100,11 @@ SIGNATURES = {
     "mjrl_linear_baseline_residual_f32": [P, P, I64, I32, P, I64, P, P, P, P],
     "mjrl_linear_baseline_gram_f32x2": [P, P, P, I64, I32, P, I64, P, P, P],
     "mjrl_linear_baseline_residual_f32x2": [P, P, P, I64, I32, P, I64, P, P, P, P],
+    "mjrl_quadratic_baseline_gram_scratch": [I32, I64, C.POINTER(I64)],
+    "mjrl_quadratic_baseline_gram": [P, P, I64, I32, P, I64, P, P, P],
+    "mjrl_quadratic_baseline_gram_f32": [P, P, P, I64, I32, P, I64, P, P, P],
+    "mjrl_quadratic_baseline_residual": [P, P, I64, I32, P, I64, P, P, P, P],
+    "mjrl_quadratic_baseline_residual_f32": [P, P, P, I64, I32, P, I64, P, P, P, P],
     "mjrl_npg_step": [SP, P, P, P, I32, F32, F32, I32, F32, P, P, P, P],
     "mjrl_trpo_trial": [SP, P, P, F32, P, P, P, P, F64, F64, I32, I32, P, P, P],
     "mjrl_policy_mean": [SP, P, I64, P, P, P, P, P, P, P],

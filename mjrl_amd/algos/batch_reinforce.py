@@ -35,6 +35,10 @@ from ..utils.logger import DataLog
 
 logging.disable(logging.CRITICAL)   # as the reference's algos do at import
 
+# QuadraticBaseline fits on the device up to this observation width (its Gram has
+# n + n(n+1)/2 + 6 columns: 2,150 at 64; mjrl_quadratic_baseline_gram's limit)
+QUADRATIC_DEVICE_MAX_N = 64
+
 
 def _check_policy(policy):
     """Rejects, at agent construction, a policy shape no device kernel covers
@@ -325,7 +329,8 @@ class BatchREINFORCE:
         return paths
 
     def _fit_baseline(self, paths, return_errors=False):
-        """baseline.fit(paths) (batch_reinforce.py:93-101).  A LinearBaseline is
+        """baseline.fit(paths) (batch_reinforce.py:93-101).  A LinearBaseline, and a
+        QuadraticBaseline of up to QUADRATIC_DEVICE_MAX_N observation columns, is
         fitted on the device from the batch still in HBM (its Gram products are
         the T x k work); other baselines fit on the host.
         Sharded (world > 1), every rank fits on the union of all ranks' paths:
@@ -337,12 +342,15 @@ class BatchREINFORCE:
         batch = getattr(self, "_last_batch", None)
         self._last_batch = None
         comm = self.comm()
-        if batch is not None and type(self.baseline).__name__ == "LinearBaseline" \
-                and hasattr(self.baseline, "_reg_coeff") and batch.T == sum(len(p["rewards"]) for p in paths):
+        kind = type(self.baseline).__name__
+        if batch is not None and kind in ("LinearBaseline", "QuadraticBaseline") \
+                and hasattr(self.baseline, "_reg_coeff") and batch.T == sum(len(p["rewards"]) for p in paths) \
+                and (kind == "LinearBaseline" or batch.obs.shape[1] <= QUADRATIC_DEVICE_MAX_N):
             # float32 rows of values that are not float32s: the fit reads their low
             # halves too (staged now from the f64 paths), i.e. the sampler's values
-            return self.engine().fit_linear_baseline(batch, self.baseline, return_errors=return_errors,
-                                                     obs_lo=batch.obs_lo(paths))
+            fit = self.engine().fit_linear_baseline if kind == "LinearBaseline" else \
+                self.engine().fit_quadratic_baseline
+            return fit(batch, self.baseline, return_errors=return_errors, obs_lo=batch.obs_lo(paths))
         if comm.world_size > 1:
             return _fit_sharded(self.baseline, paths, comm, return_errors)
         return self.baseline.fit(paths, return_errors=return_errors) if return_errors else self.baseline.fit(paths)

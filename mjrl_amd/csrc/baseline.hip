@@ -1,4 +1,5 @@
-// baseline.hip — LinearBaseline.fit on the device.
+// baseline.hip — LinearBaseline.fit and QuadraticBaseline.fit on the device (SURVEY.md
+// §8f row f1).
 //
 // Reference: mjrl/baselines/linear_baseline.py:10-44.  fit() builds the feature
 // matrix F = [clip(obs, +-10), a, a^2, a^3, 1] (a = index within the path / 1000)
@@ -20,6 +21,11 @@
 //     tiles of one row slice are mapped to the same XCD so they share its L2);
 //   - 32-row chunks double-buffered through LDS, the next chunk's loads in
 //     registers while the current one is multiplied.
+//
+// QuadraticBaseline (quadratic_baseline.py:10-65) runs the same Gram with its own
+// features, o = clip(obs, +-10) / 10: [o, o_i o_j (i <= j, row-major), 1, a, a^2,
+// a^3, a^4] (n + n(n+1)/2 + 5 columns, n <= 64): each loader thread decodes its
+// eight columns of each panel once per launch (QCol) and forms them per row.
 #include <math.h>
 
 #include "common.h"
@@ -74,6 +80,51 @@ __device__ __forceinline__ double feat(const TO* __restrict__ obs, const float* 
     }
 }
 
+// QuadraticBaseline column g (quadratic_baseline.py:10-37) as (kind, i, j); the
+// augmented Gram appends the return as column n + nq + 5
+enum QKind { Q_LIN, Q_QUAD, Q_ONE, Q_A1, Q_A2, Q_A3, Q_A4, Q_Y, Q_ZERO };
+struct QCol {
+    int kind, i, j;
+};
+__device__ __forceinline__ QCol qcol(int g, int n) {
+    const int nq = n * (n + 1) / 2;
+    if (g < n) return {Q_LIN, g, 0};
+    if (g < n + nq) {
+        int r = g - n, i = 0;
+        while (r >= n - i) {   // row i of the upper triangle holds n - i products
+            r -= n - i;
+            ++i;
+        }
+        return {Q_QUAD, i, i + r};
+    }
+    const int t = g - n - nq;
+    return {t <= 5 ? Q_ONE + t : Q_ZERO, 0, 0};
+}
+
+// o = clip(obs, +-10) / 10 (quadratic_baseline.py:12)
+template <typename TO>
+__device__ __forceinline__ double qobs(const TO* __restrict__ obs, const float* __restrict__ lo, int64_t i) {
+    const double o = obs_at(obs, lo, i);
+    return (o < -10.0 ? -10.0 : (o > 10.0 ? 10.0 : o)) / 10.0;
+}
+
+template <typename TO>
+__device__ __forceinline__ double qfeat(const TO* __restrict__ obs, const float* __restrict__ lo,
+                                        const double* __restrict__ y, const double* __restrict__ al, int64_t row,
+                                        QCol c, int n) {
+    switch (c.kind) {
+        case Q_LIN: return qobs(obs, lo, row * n + c.i);
+        case Q_QUAD: return qobs(obs, lo, row * n + c.i) * qobs(obs, lo, row * n + c.j);
+        case Q_ONE: return 1.0;
+        case Q_A1: return al[row];                          // al ** 1 (numpy: the value itself)
+        case Q_A2: return al[row] * al[row];                // al ** 2 (numpy: square)
+        case Q_A3: return pow(al[row], 3.0);                // al ** 3, al ** 4: C pow
+        case Q_A4: return pow(al[row], 4.0);
+        case Q_Y: return y[row];
+        default: return 0.0;
+    }
+}
+
 template <typename TO>
 struct GramArgs {
     const TO* obs;
@@ -85,7 +136,7 @@ struct GramArgs {
     double* slab;   // [GSLICES][npair][GT][GT]
 };
 
-template <typename TO>
+template <typename TO, bool QUAD>
 __global__ void __launch_bounds__(GTHREADS, 2) k_gram(GramArgs<TO> a) {
     __shared__ __attribute__((aligned(16))) double PI[2][GRC][GLD];
     __shared__ __attribute__((aligned(16))) double PJ[2][GRC][GLD];
@@ -107,13 +158,28 @@ __global__ void __launch_bounds__(GTHREADS, 2) k_gram(GramArgs<TO> a) {
     // loader: thread -> (row tid / 8, columns 8 (tid % 8) .. +8) of both panels
     const int lr = tid >> 3, lc = (tid & 7) * 8;
     double vi[8], vj[8];
+    QCol ci[8], cj[8];   // QUAD: this thread's columns, decoded once
+    if (QUAD) {
+        const int nf = a.n + a.n * (a.n + 1) / 2 + 5;   // the return's column
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int gi = ti * GT + lc + u, gj = tj * GT + lc + u;
+            ci[u] = gi == nf ? QCol{Q_Y, 0, 0} : (gi > nf ? QCol{Q_ZERO, 0, 0} : qcol(gi, a.n));
+            cj[u] = gj == nf ? QCol{Q_Y, 0, 0} : (gj > nf ? QCol{Q_ZERO, 0, 0} : qcol(gj, a.n));
+        }
+    }
     auto gload = [&](int64_t c0) {
         const int64_t row = c0 + lr;
         const bool in = row < r1;
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            vi[u] = in ? feat(a.obs, a.lo, a.y, a.al, row, ti * GT + lc + u, a.n) : 0.0;
-            vj[u] = in ? feat(a.obs, a.lo, a.y, a.al, row, tj * GT + lc + u, a.n) : 0.0;
+            if (QUAD) {
+                vi[u] = in ? qfeat(a.obs, a.lo, a.y, a.al, row, ci[u], a.n) : 0.0;
+                vj[u] = in ? qfeat(a.obs, a.lo, a.y, a.al, row, cj[u], a.n) : 0.0;
+            } else {
+                vi[u] = in ? feat(a.obs, a.lo, a.y, a.al, row, ti * GT + lc + u, a.n) : 0.0;
+                vj[u] = in ? feat(a.obs, a.lo, a.y, a.al, row, tj * GT + lc + u, a.n) : 0.0;
+            }
         }
     };
     auto lstore = [&](int buf) {
@@ -214,10 +280,29 @@ __global__ void __launch_bounds__(256) k_linear_residual(const TO* __restrict__ 
     }
 }
 
+// r_t = y_t - F_t . c with QuadraticBaseline's features (fit(return_errors=True))
+template <typename TO>
+__global__ void __launch_bounds__(256) k_quadratic_residual(const TO* __restrict__ obs, const float* __restrict__ lo,
+                                                            const double* __restrict__ y,
+                                                            const double* __restrict__ al, int64_t T, int n,
+                                                            const double* __restrict__ coef, double* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int nf = n + n * (n + 1) / 2 + 5;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t row = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; row < T; row += nw) {
+        double acc = 0.0;
+        for (int g = lane; g < nf; g += 64) acc += qfeat(obs, lo, y, al, row, qcol(g, n), n) * coef[g];
+        acc = wave_sum(acc);
+        if (lane == 0) out[row] = y[row] - acc;
+    }
+}
+
 inline int err(hipError_t e) { return e == hipSuccess ? MJRL_OK : (int)e; }
 
-inline void gram_dims(int n, int& K, int& ntile, int& npair) {
-    K = n + 5;
+constexpr int QMAX_N = 64;   // QuadraticBaseline: n + n(n+1)/2 + 6 <= 2,150 Gram columns
+
+inline void gram_dims(int n, int& K, int& ntile, int& npair, bool quad = false) {
+    K = quad ? n + n * (n + 1) / 2 + 6 : n + 5;
     ntile = (K + GT - 1) / GT;
     npair = ntile * (ntile + 1) / 2;
 }
@@ -235,14 +320,15 @@ int mjrl_linear_baseline_gram_scratch(int32_t n, int64_t T, int64_t* doubles) {
 }
 
 extern "C++" {
-template <typename TO>
+template <typename TO, bool QUAD = false>
 static int linear_baseline_gram(const TO* obs, const float* lo, const double* returns, int64_t T, int32_t n,
                                 const int64_t* path_off, int64_t P, double* scratch, double* out, void* stream) {
-    if (n <= 0 || T < 0 || P < 0 || !out || !scratch || (T > 0 && (!obs || !returns || !path_off)))
+    if (n <= 0 || T < 0 || P < 0 || !out || !scratch || (T > 0 && (!obs || !returns || !path_off)) ||
+        (QUAD && n > QMAX_N))
         return MJRL_EINVAL;
     hipStream_t st = (hipStream_t)stream;
     int K, ntile, npair;
-    gram_dims(n, K, ntile, npair);
+    gram_dims(n, K, ntile, npair, QUAD);
     double* slab = scratch;
     double* al = scratch + (int64_t)GSLICES * npair * GT * GT;
     if (P > 0) {
@@ -251,7 +337,7 @@ static int linear_baseline_gram(const TO* obs, const float* lo, const double* re
     }
     GramArgs<TO> ga{obs, lo, returns, al, T, n, ntile, npair, slab};
     const int groups = (GSLICES + 7) / 8;   // slices per XCD
-    hipLaunchKernelGGL(k_gram<TO>, dim3(8 * groups * npair), dim3(GTHREADS), 0, st, ga);
+    hipLaunchKernelGGL((k_gram<TO, QUAD>), dim3(8 * groups * npair), dim3(GTHREADS), 0, st, ga);
     const int64_t ne = (int64_t)npair * GT * GT;
     hipLaunchKernelGGL(k_gram_reduce, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st, slab, ntile, npair, K,
                        out);
@@ -260,24 +346,29 @@ static int linear_baseline_gram(const TO* obs, const float* lo, const double* re
 }  // extern "C++"
 
 extern "C++" {
-template <typename TO>
+template <typename TO, bool QUAD = false>
 static int linear_baseline_residual(const TO* obs, const float* lo, const double* returns, int64_t T, int32_t n,
                                     const int64_t* path_off, int64_t P, const double* coeffs, double* scratch,
                                     double* out, void* stream) {
-    if (n <= 0 || T < 0 || P < 0 || (T > 0 && (!obs || !returns || !path_off || !coeffs || !scratch || !out)))
+    if (n <= 0 || T < 0 || P < 0 || (T > 0 && (!obs || !returns || !path_off || !coeffs || !scratch || !out)) ||
+        (QUAD && n > QMAX_N))
         return MJRL_EINVAL;
     if (T == 0) return MJRL_OK;
     hipStream_t st = (hipStream_t)stream;
     int K, ntile, npair;
-    gram_dims(n, K, ntile, npair);
+    gram_dims(n, K, ntile, npair, QUAD);
     double* al = scratch + (int64_t)GSLICES * npair * GT * GT;
     if (P > 0) {
         const int64_t g = (P + 3) / 4;
         hipLaunchKernelGGL(k_path_time, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, st, path_off, P, al);
     }
     const int64_t g = (T + 3) / 4;
-    hipLaunchKernelGGL(k_linear_residual<TO>, dim3((unsigned)(g < 16384 ? g : 16384)), dim3(256), 0, st, obs, lo,
-                       returns, al, T, n, coeffs, out);
+    if (QUAD)
+        hipLaunchKernelGGL(k_quadratic_residual<TO>, dim3((unsigned)(g < 16384 ? g : 16384)), dim3(256), 0, st, obs,
+                           lo, returns, al, T, n, coeffs, out);
+    else
+        hipLaunchKernelGGL(k_linear_residual<TO>, dim3((unsigned)(g < 16384 ? g : 16384)), dim3(256), 0, st, obs,
+                           lo, returns, al, T, n, coeffs, out);
     return err(hipGetLastError());
 }
 }  // extern "C++"
@@ -318,6 +409,39 @@ int mjrl_linear_baseline_residual_f32x2(const float* obs, const float* obs_lo, c
                                         double* scratch, double* out, void* stream) {
     if (T > 0 && !obs_lo) return MJRL_EINVAL;
     return linear_baseline_residual(obs, obs_lo, returns, T, n, path_off, P, coeffs, scratch, out, stream);
+}
+
+int mjrl_quadratic_baseline_gram_scratch(int32_t n, int64_t T, int64_t* doubles) {
+    if (n <= 0 || n > QMAX_N || T < 0 || !doubles) return MJRL_EINVAL;
+    int K, ntile, npair;
+    gram_dims(n, K, ntile, npair, true);
+    *doubles = (int64_t)GSLICES * npair * GT * GT + T;
+    return MJRL_OK;
+}
+
+int mjrl_quadratic_baseline_gram(const double* obs, const double* returns, int64_t T, int32_t n,
+                                 const int64_t* path_off, int64_t P, double* scratch, double* out, void* stream) {
+    return linear_baseline_gram<double, true>(obs, nullptr, returns, T, n, path_off, P, scratch, out, stream);
+}
+
+int mjrl_quadratic_baseline_gram_f32(const float* obs, const float* obs_lo, const double* returns, int64_t T,
+                                     int32_t n, const int64_t* path_off, int64_t P, double* scratch, double* out,
+                                     void* stream) {
+    return linear_baseline_gram<float, true>(obs, obs_lo, returns, T, n, path_off, P, scratch, out, stream);
+}
+
+int mjrl_quadratic_baseline_residual(const double* obs, const double* returns, int64_t T, int32_t n,
+                                     const int64_t* path_off, int64_t P, const double* coeffs, double* scratch,
+                                     double* out, void* stream) {
+    return linear_baseline_residual<double, true>(obs, nullptr, returns, T, n, path_off, P, coeffs, scratch, out,
+                                                  stream);
+}
+
+int mjrl_quadratic_baseline_residual_f32(const float* obs, const float* obs_lo, const double* returns, int64_t T,
+                                         int32_t n, const int64_t* path_off, int64_t P, const double* coeffs,
+                                         double* scratch, double* out, void* stream) {
+    return linear_baseline_residual<float, true>(obs, obs_lo, returns, T, n, path_off, P, coeffs, scratch, out,
+                                                 stream);
 }
 
 }  // extern "C"

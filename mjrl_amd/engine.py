@@ -1447,7 +1447,16 @@ class UpdateEngine:
         return h[0].numpy().copy(), h[1].numpy().copy(), h[2].numpy().copy()
 
     @_on_device
-    def fit_linear_baseline(self, batch, baseline, returns=None, return_errors=False, obs_lo=None):
+    def fit_quadratic_baseline(self, batch, baseline, returns=None, return_errors=False, obs_lo=None):
+        """QuadraticBaseline.fit (baselines/quadratic_baseline.py:40-65) on the
+        batch's rows in HBM: the Gram of its features [o, o_i o_j (i <= j), 1, a ..
+        a^4] (o = clip(obs) / 10) with the returns on the device
+        (mjrl_quadratic_baseline_gram, n <= 64), then the reference's lstsq retry
+        loop; as fit_linear_baseline otherwise."""
+        return self.fit_linear_baseline(batch, baseline, returns, return_errors, obs_lo, quadratic=True)
+
+    @_on_device
+    def fit_linear_baseline(self, batch, baseline, returns=None, return_errors=False, obs_lo=None, quadratic=False):
         """LinearBaseline.fit (baselines/linear_baseline.py:20-44) on the batch's
         RL rows already in HBM: the Gram products [F y]^T [F y] on the device
         (mjrl_linear_baseline_gram, all-reduced when sharded), then the
@@ -1460,17 +1469,28 @@ class UpdateEngine:
         L = self.lib
         st = _lib.stream_ptr()
         n, T, P = int(batch.obs.shape[1]), batch.T, batch.P
-        k = n + 4
+        k = n + n * (n + 1) // 2 + 5 if quadratic else n + 4
         y = returns if returns is not None else self.ws["ret"][:T]
         nd = C.c_int64()
-        _lib.check(L.mjrl_linear_baseline_gram_scratch(n, T, C.byref(nd)), "mjrl_linear_baseline_gram_scratch")
+        kind = "quadratic" if quadratic else "linear"
+        _lib.check(getattr(L, "mjrl_%s_baseline_gram_scratch" % kind)(n, T, C.byref(nd)),
+                   "mjrl_%s_baseline_gram_scratch" % kind)
         f64 = dict(dtype=torch.float64, device=self.device)
         scratch = torch.empty(max(nd.value, 1), **f64)
         gram = torch.zeros((k + 1, k + 1), **f64)
         f32 = batch.obs.dtype == torch.float32
-        if f32 and obs_lo is not None:
+        if obs_lo is not None and f32:
             if obs_lo.dtype != torch.float32 or obs_lo.shape[0] < T or obs_lo.shape[1] != n:
-                raise ValueError("fit_linear_baseline: obs_lo must be float32 [T, n]")
+                raise ValueError("fit_%s_baseline: obs_lo must be float32 [T, n]" % kind)
+        if quadratic and f32:   # one f32 entry, low halves or null
+            lo = _lib.ptr(obs_lo) if obs_lo is not None else None
+            gram_fn = functools.partial(L.mjrl_quadratic_baseline_gram_f32, _lib.ptr(batch.obs))
+            res_fn = functools.partial(L.mjrl_quadratic_baseline_residual_f32, _lib.ptr(batch.obs))
+            obs_arg = lo
+        elif quadratic:
+            gram_fn, res_fn = L.mjrl_quadratic_baseline_gram, L.mjrl_quadratic_baseline_residual
+            obs_arg = _lib.ptr(batch.obs)
+        elif f32 and obs_lo is not None:
             gram_fn = functools.partial(L.mjrl_linear_baseline_gram_f32x2, _lib.ptr(batch.obs))
             res_fn = functools.partial(L.mjrl_linear_baseline_residual_f32x2, _lib.ptr(batch.obs))
             obs_arg = _lib.ptr(obs_lo)
@@ -1479,14 +1499,14 @@ class UpdateEngine:
             res_fn = L.mjrl_linear_baseline_residual_f32 if f32 else L.mjrl_linear_baseline_residual
             obs_arg = _lib.ptr(batch.obs)
         _lib.check(gram_fn(obs_arg, _lib.ptr(y), T, n, _lib.ptr(batch.path_off), P,
-                           _lib.ptr(scratch), _lib.ptr(gram), st), "mjrl_linear_baseline_gram")
+                           _lib.ptr(scratch), _lib.ptr(gram), st), "mjrl_%s_baseline_gram" % kind)
         self.comm.allreduce_sum(gram)
 
         def sse(coeffs):
             r = torch.empty(max(T, 1), **f64)
             c = torch.from_numpy(np.ascontiguousarray(coeffs, dtype=np.float64)).to(self.device)
             _lib.check(res_fn(obs_arg, _lib.ptr(y), T, n, _lib.ptr(batch.path_off), P, _lib.ptr(c),
-                              _lib.ptr(scratch), _lib.ptr(r), st), "mjrl_linear_baseline_residual")
+                              _lib.ptr(scratch), _lib.ptr(r), st), "mjrl_%s_baseline_residual" % kind)
             out = torch.zeros(8, **f64)
             part = torch.empty(4 * 256, **f64)
             _lib.check(L.mjrl_moments(_lib.ptr(r), T, None, _lib.ptr(part), _lib.ptr(out), st), "mjrl_moments")
@@ -1498,7 +1518,7 @@ class UpdateEngine:
         if return_errors:
             err_before = (sse(baseline._coeffs) if baseline._coeffs is not None else yy) / yy
         reg = baseline._reg_coeff
-        for _ in range(10):   # linear_baseline.py:31-38
+        for _ in range(10):   # linear_baseline.py:31-38, quadratic_baseline.py:51-59
             c = np.linalg.lstsq(FtF + reg * np.identity(k), Fty, rcond=None)[0]
             baseline._coeffs = c
             if not np.any(np.isnan(c)):

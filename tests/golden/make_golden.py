@@ -636,6 +636,64 @@ def f64obs_cases():
                 seed=609, col_scale=col_scale, spiky=spiky)
 
 
+def quad_case(name, n, lengths, terminated, seed, col_scale=None, gamma=0.995):
+    """QuadraticBaseline.fit (quadratic_baseline.py:10-65) on observations that
+    are NOT float32s, inputs replayed from RandomState(seed) as in f64obs_case
+    (oracle.npg_cpu.regen_f64obs; stored as their SHA-256): returns
+    (process_samples.compute_returns), then fit(return_errors=True) on the first
+    half of the paths (coeffs0, err0: no previous coefficients) and again on all
+    paths (coeffs1, err1: error_before with coeffs0), the all-path fit's spread
+    over two path permutations, and its predict() on the last path."""
+    import hashlib
+    from mjrl.baselines.quadratic_baseline import QuadraticBaseline as RefQuad
+    rs = np.random.RandomState(seed)
+    paths = []
+    for H, term in zip(lengths, terminated):
+        obs = rs.randn(H, n)
+        if col_scale is not None:
+            obs = obs * col_scale
+        paths.append(dict(observations=obs, rewards=rs.randn(H), terminated=bool(term)))
+    obs = concat(paths, "observations")
+    spec = EnvSpec(n, 1, max(lengths), 1)
+    process_samples.compute_returns(paths, gamma)
+    q = RefQuad(spec)
+    err0 = q.fit(paths[: len(paths) // 2], return_errors=True)
+    coeffs0 = q._coeffs.copy()
+    err1 = q.fit(paths, return_errors=True)
+    spread = 0.0
+    for ps in (1, 2):
+        order = np.random.RandomState(ps).permutation(len(paths))
+        alt = RefQuad(spec)
+        alt.fit([paths[i] for i in order])
+        spread = max(spread, float(np.linalg.norm(alt._coeffs - q._coeffs)))
+    sha = lambda *arrs: hashlib.sha256(b"".join(np.ascontiguousarray(a).tobytes() for a in arrs)).hexdigest()
+    out = dict(n=np.int64(n), lengths=np.array(lengths, np.int64), terminated=np.array(terminated, np.uint8),
+               gen_seed=np.int64(seed), gamma=np.float64(gamma),
+               inputs_sha256=np.array(sha(obs, concat(paths, "rewards"))), returns=concat(paths, "returns"),
+               coeffs0=coeffs0, err0=np.array(err0, np.float64), coeffs1=q._coeffs.copy(),
+               err1=np.array(err1, np.float64), coeffs1_spread=np.float64(spread),
+               predict_last=q.predict(paths[-1]))
+    if col_scale is not None:
+        out["col_scale"] = col_scale
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), **out)
+    print("%-22s T=%-6d n=%-3d k=%-4d inexact %.3f err0 %s err1 %s fit spread %.3g" % (
+        name, obs.shape[0], n, len(q._coeffs), np.mean(obs.astype(np.float32).astype(np.float64) != obs), err0, err1,
+        spread / np.linalg.norm(q._coeffs)))
+
+
+def quad_cases():
+    # point_mass width (reference tests/point_mass_test.py: 40 trajectories x 25 steps)
+    quad_case("quad_point_mass", 4, [25] * 40, [False] * 40, seed=701)
+    # Swimmer width, ragged, terminated paths, values past the +-10 clip
+    rs = np.random.RandomState(702)
+    lengths = [500] * 12 + list(rs.randint(1, 500, size=5))
+    quad_case("quad_swimmer", 8, lengths, [False] * 12 + [True, False, True, True, False], seed=703,
+              col_scale=np.array([1, 3, 12, 0.5, 8, 2, 30, 0.1]))
+    # HalfCheetah width (k = 175 features: three 64-column Gram tiles)
+    quad_case("quad_halfcheetah", 17, [1000] * 6 + [333, 1], [False] * 6 + [True, True], seed=704,
+              col_scale=10.0 ** np.random.RandomState(705).uniform(-1, 1.3, size=17))
+
+
 def bc_case():
     """Reference BC (behavior_cloning.py:11-68): MLE of expert actions by minibatch
     Adam, minibatches from np.random.choice after np.random.seed(17); the
@@ -697,7 +755,9 @@ def ppo_case():
 if __name__ == "__main__":
     if not ONLY or "f64obs" in ONLY:
         f64obs_cases()
-    if ONLY == {"f64obs"}:
+    if not ONLY or "quad" in ONLY:
+        quad_cases()
+    if ONLY and ONLY <= {"f64obs", "quad"}:
         sys.exit(0)
     main()
     if not ONLY or "baselines" in ONLY:

@@ -163,7 +163,8 @@ def test_engine_methods_run_on_their_device():
     """Every UpdateEngine entry point that launches kernels makes self.device
     current first (the kernels go to torch's current stream of that device)."""
     from mjrl_amd.engine import UpdateEngine
-    for name in ("update", "returns_advantages", "normalize_advantages", "fit_linear_baseline", "fvp",
+    for name in ("update", "returns_advantages", "normalize_advantages", "fit_linear_baseline",
+                 "fit_quadratic_baseline", "fvp",
                  "load_rows", "forward_pass", "eval_pass"):
         fn = getattr(UpdateEngine, name)
         assert getattr(fn, "__wrapped__", None) is not None, name

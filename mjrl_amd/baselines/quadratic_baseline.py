@@ -1,6 +1,8 @@
 """Quadratic-feature value baseline (API of mjrl/baselines/quadratic_baseline.py:4-70):
 [o/10 (clipped), upper-triangular o_i o_j, 1, t/1000 .. (t/1000)^4] features,
-ridge normal equations.  Host numpy, the caller's object (fit on GPU: SURVEY §8f f1)."""
+ridge normal equations.  The object and its predict are host numpy; an agent
+fits it on the device from the batch in HBM (UpdateEngine.fit_quadratic_baseline,
+n <= 64; BatchREINFORCE._fit_baseline), and fit() here is the host path."""
 import numpy as np
 
 

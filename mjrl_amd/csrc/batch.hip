@@ -537,16 +537,14 @@ __global__ void __launch_bounds__(64 * GAE_WAVES) k_gae(const double* __restrict
 // Lanes = paths (round 6): the serial recurrences of LP_PATHS paths run side by side
 // in ONE instruction stream each, one wave per chain, each lane one path — wave 0
 // the returns (discount_sum(rewards, gamma)), wave 1 the advantages (discount_sum(td,
-// gamma lambda), idle without GAE); the path-return sum (front to back) on lanes 0..7
-// of the first mover wave, which has the slack (a third chain wave beside the two
-// cost them 1.5 us at 125 x 1000, profiles/r06c/abl_gae10/gae_nofwd.txt).  A
+// gamma lambda), idle without GAE), wave 2 the path-return sum (front to back).  A
 // dependent fp64 multiply -> add costs ~11 cycles of issue per step for the whole
 // wave, however many lanes are on (profiles/r06b/gae_latency.txt), so LP_PATHS paths
 // advance for the price one did — as long as the chain wave does little else: a
 // store of its outputs costs it ~10 cycles a step to HBM and ~13 to LDS, an LDS read
 // ~2 (profiles/r06c/gae_latency.txt, the "lanes" rows).  So the chain waves only read
 // and keep one checkpoint per LP_GB-step segment (the accumulator entering it, one
-// LDS write per segment), and the four mover waves (2..5) recompute every segment
+// LDS write per segment), and the four mover waves (3..6) recompute every segment
 // from its checkpoint — the same __dmul_rn / __dadd_rn in the same order, so the
 // same values bit for bit — one segment per lane, 256 segments side by side, and
 // store them (each lane a 128-byte run).  The steps come through three LDS buffers in
@@ -563,8 +561,8 @@ constexpr int LP_W = MJRL_GAE_W;          // steps per window
 constexpr int LP_LD = LP_W + 1;           // LDS row stride (doubles): chain lanes conflict-free
 constexpr int LP_GB = 16;                 // steps per segment (chain register batch, recompute task)
 constexpr int LP_NS = LP_W / LP_GB;       // segments per window row
-constexpr int LP_CH = 2;                  // chain waves 0..1
-constexpr int LP_MVW = 4;                 // mover waves 2..5 (wave 2 also runs the path-return sum)
+constexpr int LP_CH = 3;                  // chain waves 0..2
+constexpr int LP_MVW = 4;                 // mover waves 3..6
 constexpr int LP_T = 64 * (LP_CH + LP_MVW);
 constexpr int LP_MV = 64 * LP_MVW;
 constexpr int LP_TPP = LP_MV / LP_PATHS;  // mover threads a path: runs of LP_TPP consecutive steps a load
@@ -574,17 +572,20 @@ constexpr int LP_NB = 3;                  // LDS buffers
 static_assert(LP_W % LP_TPP == 0 && LP_W % LP_GB == 0, "window split");
 static_assert(2 * LP_PATHS * LP_NS <= LP_MV, "one recompute segment per mover thread");
 
-// A chain wave's pass over one window row (its lane's path): acc = x + c * acc over
-// the whole window with no step mask (a partial window, the path's first steps,
-// holds its valid steps at the top, which the chain meets first; what it computes
-// below them is never stored and the path's chain ends there), writing the
-// accumulator entering each segment to ck[k * LP_PATHS] (segment k = batch k: u in
-// [W - (k + 1) GB, W - k GB)).  Batch k + 2's LDS reads are issued before batch k's
-// steps (the compiler barrier keeps them from all being hoisted to the top).
+// A chain wave's pass over one window row (its lane's path), batch k + 2's LDS reads
+// issued before batch k's steps (the compiler barrier keeps them from all being
+// hoisted to the top).  Forward: the path-return sum front to back, Python's
+// sum(p["rewards"]) (npg_cg.py:97; x + 1.0 * acc is x + acc exactly, k_gae's form;
+// steps past the path's end hold 0.0).  Backward: acc = x + c * acc over the whole
+// window with no step mask (a partial window, the path's first steps, holds its valid
+// steps at the top, which the chain meets first; what it computes below them is never
+// stored and the path's chain ends there), writing the accumulator entering each
+// segment to ck[k * LP_PATHS] (segment k = batch k: u in [W - (k + 1) GB, W - k GB)).
+template <bool FWD>
 __device__ __forceinline__ double lp_chain(const double* __restrict__ row, double acc, double c,
                                            double* __restrict__ ck) {
     double X[3][LP_GB];
-    auto at = [](int k) { return LP_W - (k + 1) * LP_GB; };
+    auto at = [](int k) { return FWD ? k * LP_GB : LP_W - (k + 1) * LP_GB; };
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
 #pragma unroll
@@ -597,9 +598,17 @@ __device__ __forceinline__ double lp_chain(const double* __restrict__ row, doubl
             for (int g = 0; g < LP_GB; ++g) X[(k + 2) % 3][g] = row[at(k + 2) + g];
         }
         asm volatile("" ::: "memory");
-        ck[k * LP_PATHS] = acc;
+#ifndef MJRL_GAE_ABL_NOFWD
+        if (FWD) {
 #pragma unroll
-        for (int g = LP_GB - 1; g >= 0; --g) acc = __dadd_rn(X[k % 3][g], __dmul_rn(c, acc));
+            for (int g = 0; g < LP_GB; ++g) acc = __dadd_rn(X[k % 3][g], acc);
+        }
+#endif
+        if (!FWD) {
+            ck[k * LP_PATHS] = acc;
+#pragma unroll
+            for (int g = LP_GB - 1; g >= 0; --g) acc = __dadd_rn(X[k % 3][g], __dmul_rn(c, acc));
+        }
     }
     return acc;
 }
@@ -632,7 +641,7 @@ __global__ void __launch_bounds__(LP_T) k_gae_lp(const double* __restrict__ rew,
         // ---- a chain wave: LDS reads, one checkpoint write a segment ----
         const bool chain = lane < np && (w != 1 || use_gae);
         const double c = w == 0 ? gamma : gl;
-        const double* const cw = (w == 0 ? RB : TD) + lane * LP_LD;
+        const double* const cw = (w == 0 ? RB : (w == 1 ? TD : RF)) + lane * LP_LD;
         double acc = 0.0;
         __syncthreads();   // window 0 put
         for (int i = 0; i < nwin; ++i) {
@@ -642,10 +651,16 @@ __global__ void __launch_bounds__(LP_T) k_gae_lp(const double* __restrict__ rew,
                 continue;
             }
 #endif
-            if (chain)
-                acc = lp_chain(cw + (i % LP_NB) * LP_BUF, acc, c, &CK[w][i & 1][0][lane]);
+            if (chain) {
+                const double* const row = cw + (i % LP_NB) * LP_BUF;
+                if (w == 2)
+                    acc = lp_chain<true>(row, acc, c, nullptr);
+                else
+                    acc = lp_chain<false>(row, acc, c, &CK[w][i & 1][0][lane]);
+            }
             __syncthreads();
         }
+        if (w == 2 && lane < np) path_ret[p0 + lane] = acc;
         return;
     }
     // ---- a mover: every global load, the recompute, every output store ----
@@ -739,8 +754,6 @@ __global__ void __launch_bounds__(LP_T) k_gae_lp(const double* __restrict__ rew,
     }
     if (nwin > 1) load(1);
     __syncthreads();   // window 0 put
-    const bool fsum = w == LP_CH && lane < np;   // the path-return sum's lanes
-    double facc = 0.0;
     for (int i = 0; i < nwin; ++i) {
         // the chains run window i (buffer i % 3); buffer (i - 1) % 3 holds window i - 1,
         // whose checkpoints are CK[.][(i - 1) & 1]; put(i + 1) fills the third buffer
@@ -749,33 +762,9 @@ __global__ void __launch_bounds__(LP_T) k_gae_lp(const double* __restrict__ rew,
         if (i + 1 < nwin) put(i + 1);
         if (i + 2 < nwin) load(i + 2);
 #endif
-        if (fsum) {
-            // the path-return sum front to back, Python's sum(p["rewards"]) (npg_cg.py:97;
-            // x + 1.0 * acc is x + acc exactly, k_gae's form; steps past the path's end
-            // hold 0.0, which leaves acc unchanged), eight steps a batch
-            const double* const row = RF + (i % LP_NB) * LP_BUF + lane * LP_LD;
-            double x[8], xn[8];
-#pragma unroll
-            for (int g = 0; g < 8; ++g) x[g] = row[g];
-#pragma unroll 4
-            for (int u0 = 0; u0 < LP_W; u0 += 8) {
-                if (u0 + 8 < LP_W) {
-#pragma unroll
-                    for (int g = 0; g < 8; ++g) xn[g] = row[u0 + 8 + g];
-                }
-                asm volatile("" ::: "memory");
-#ifndef MJRL_GAE_ABL_NOFWD
-#pragma unroll
-                for (int g = 0; g < 8; ++g) facc = __dadd_rn(x[g], facc);
-#endif
-#pragma unroll
-                for (int g = 0; g < 8; ++g) x[g] = xn[g];
-            }
-        }
         __syncthreads();
     }
     if (nwin > 0) recompute(nwin - 1);
-    if (fsum) path_ret[p0 + lane] = facc;
 }
 
 // Moments pass 1: per-block partials of sum(x-c), sum((x-c)^2), min, max.

@@ -15,9 +15,11 @@ sampling loop of samplers/vector_sampler.py:
     each row computed from its f64 values (the coefficients are fixed while a
     batch is sampled: baseline.fit runs after the update) and the exactness
     flag; the actions likewise (f32);
-  - when a trajectory ends, its rows are copied to HBM on the staging copy
-    stream at the trajectory's fixed position ep * H of a padded device slab,
-    while the other environments keep stepping;
+  - every FLUSH_ROWS steps of a trajectory, its completed rows are copied to HBM
+    on the staging copy stream at their fixed position (ep * H + t) of a padded
+    device slab, and the rest when it ends, while the environments keep
+    stepping (so the last lock step leaves at most FLUSH_ROWS rows a slot to
+    copy);
   - rewards and the predictions travel the same way (8 bytes a row each);
   - after sampling, batch() compacts the padded slabs into the contiguous
     layout with one device gather per slot (mjrl_gather_rows; none when every
@@ -27,8 +29,8 @@ sampling loop of samplers/vector_sampler.py:
 The DeviceBatch it returns is bit-identical to DeviceBatch.from_paths on the
 same paths (the same f32 rounding, the same per-row prediction arithmetic,
 ranges that give the same column scales): tests/test_gpu_stream_staging.py.
-What remains after the last environment step is one trajectory's copy, the
-gather, the 1-D slots and the update itself (bench.py e2e_stream).
+What remains after the last environment step is the trajectories' last rows,
+the gather, the 1-D slots and the update itself (bench.py e2e_stream).
 """
 import ctypes as C
 
@@ -51,6 +53,7 @@ class StreamSink:
     the batch is sampled); nslots: the sampler's environment slots."""
 
     NBUF = 2   # slabs per environment slot: a slot starts its next trajectory while the last one's copy runs
+    FLUSH_ROWS = 256   # a live trajectory's completed rows leave for HBM in runs of this many
 
     def __init__(self, n, m, horizon, N, device, baseline=None, nslots=64):
         self.n, self.m, self.H, self.N = int(n), int(m), int(horizon), int(N)
@@ -78,6 +81,7 @@ class StreamSink:
         self._row_ptr0 = self.obs_h.ctypes.data
         self.buf = np.zeros(S, np.int64)
         self.ep = np.full(S, -1, np.int64)
+        self.copied = np.zeros(S, np.int64)   # rows of the slot's live trajectory already sent
         self.lo = np.full(self.n, np.inf, np.float32)
         self.hi = np.full(self.n, -np.inf, np.float32)
         self.flag = np.zeros(1, np.int32)
@@ -105,6 +109,7 @@ class StreamSink:
             self._ev[slot][b] = None
         self.buf[slot] = b
         self.ep[slot] = ep
+        self.copied[slot] = 0
 
     def rows(self, slots, obs, t):
         """Observation rows obs [E, n] (f64) of environments `slots` at path
@@ -125,6 +130,11 @@ class StreamSink:
             self.flag.ctypes.data), "mjrl_host_stage_rows_f64x")
         if pred is not None:
             self.pred_h[slots, b, t] = pred
+        # row t arriving means rows < t are complete (their actions and rewards were
+        # recorded in the previous step): send full runs of them
+        due = np.nonzero(t - self.copied[slots] >= self.FLUSH_ROWS)[0]
+        for i in due.tolist():
+            self._send(int(slots[i]), int(t[i]))
 
     def actions(self, slots, act, t):
         """Action rows act [E, m] of environments `slots` at path indices t."""
@@ -140,22 +150,31 @@ class StreamSink:
         """One environment's reward at path index t (the sampler's per-step call)."""
         self.rew_h[slot, self.buf[slot], t] = r
 
+    def _send(self, slot, upto):
+        """Rows [copied, upto) of slot `slot`'s live trajectory (observations,
+        actions, rewards, baseline predictions) to their place in the padded
+        device slabs, on the copy stream."""
+        ep, b, a = int(self.ep[slot]), int(self.buf[slot]), int(self.copied[slot])
+        if upto <= a:
+            return
+        H = self.H
+        with torch.cuda.stream(self.cs):
+            self.obs_pad[ep * H + a: ep * H + upto].copy_(self._obs[slot, b, a:upto], non_blocking=True)
+            self.act_pad[ep * H + a: ep * H + upto].copy_(self._act[slot, b, a:upto], non_blocking=True)
+            self.rew_pad[ep * H + a: ep * H + upto].copy_(self._rew[slot, b, a:upto], non_blocking=True)
+            if self.pred_pad is not None:
+                self.pred_pad[ep * H + a: ep * H + upto].copy_(self._pred[slot, b, a:upto], non_blocking=True)
+        self.copied[slot] = upto
+
     def finish(self, slot, length, terminated=False):
-        """Slot `slot`'s trajectory ended after `length` rows: its rows (observations,
-        actions, rewards, baseline predictions) leave for HBM now, on the copy
-        stream, while sampling continues."""
+        """Slot `slot`'s trajectory ended after `length` rows: its rows not sent yet
+        leave for HBM now, on the copy stream, while sampling continues."""
         ep, b, Lr = int(self.ep[slot]), int(self.buf[slot]), int(length)
         self.lengths[ep] = Lr
         self.term[ep] = bool(terminated)
         if Lr:
-            H = self.H
-            with torch.cuda.stream(self.cs):
-                self.obs_pad[ep * H: ep * H + Lr].copy_(self._obs[slot, b, :Lr], non_blocking=True)
-                self.act_pad[ep * H: ep * H + Lr].copy_(self._act[slot, b, :Lr], non_blocking=True)
-                self.rew_pad[ep * H: ep * H + Lr].copy_(self._rew[slot, b, :Lr], non_blocking=True)
-                if self.pred_pad is not None:
-                    self.pred_pad[ep * H: ep * H + Lr].copy_(self._pred[slot, b, :Lr], non_blocking=True)
-            ev = torch.cuda.Event()
+            self._send(slot, Lr)
+            ev = torch.cuda.Event()   # covers the trajectory's earlier runs too (one stream, in order)
             ev.record(self.cs)
             self._ev[slot][b] = ev
         self.ep[slot] = -1

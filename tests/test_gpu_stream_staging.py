@@ -20,8 +20,9 @@ def _same_batch(a, b):
     assert a.obs_inexact == b.obs_inexact and np.array_equal(a.lengths, b.lengths)
 
 
+@pytest.mark.parametrize("flush", [256, 7])
 @pytest.mark.parametrize("fitted,ragged", [(False, True), (True, True), (True, False)])
-def test_stream_batch_equals_from_paths(fitted, ragged):
+def test_stream_batch_equals_from_paths(fitted, ragged, flush, monkeypatch):
     from mjrl_amd.baselines.linear_baseline import LinearBaseline
     from mjrl_amd.engine import DeviceBatch
     from mjrl_amd.policies.gaussian_mlp import MLP
@@ -29,6 +30,9 @@ def test_stream_batch_equals_from_paths(fitted, ragged):
     from mjrl_amd.samplers.vector_sampler import sample_paths_vectorized
     from mjrl_amd.utils.gym_env import EnvSpec
     from stub_env import StubEnv
+    # flush 7: a live trajectory's completed rows leave in runs of 7 (the 40-step
+    # horizon is otherwise shorter than one run)
+    monkeypatch.setattr(StreamSink, "FLUSH_ROWS", flush)
     dev = torch.device("cuda:0")
     spec = EnvSpec(6, 2, 40, 1)
     policy = MLP(spec, hidden_sizes=(32, 32), seed=4, init_log_std=-0.5)

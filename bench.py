@@ -450,15 +450,20 @@ def e2e_stream(paths_range, eng, th0, base, upd, device, cfg, nslots=64):
             tf += time.perf_counter() - f0
         t0 = time.perf_counter()
         b = sink.batch(paths)
+        torch.cuda.synchronize()   # the last copies and the 1-D slots (split out for the breakdown)
+        t1 = time.perf_counter()
         eng.update(b, th, **upd)
         torch.cuda.synchronize()
-        return (time.perf_counter() - t0) * 1e3, tf * 1e3
+        t2 = time.perf_counter()
+        return (t2 - t0) * 1e3, tf * 1e3, (t1 - t0) * 1e3, (t2 - t1) * 1e3
 
     one(th0.clone())
     runs = [one(th0.clone()) for _ in range(2)]
     crit = float(np.median([r[0] for r in runs]))
     feed = float(np.median([r[1] for r in runs]))
     return dict(post_sampling_ms=round(crit, 2), feed_ms=round(feed, 1), feed_us_per_row=round(feed * 1e3 / T, 3),
+                batch_ms=round(float(np.median([r[2] for r in runs])), 2),
+                update_ms=round(float(np.median([r[3] for r in runs])), 2),
                 timesteps=T, slots=nslots,
                 note="StreamSink fed per lock step as the vectorised sampler feeds it (observation rows through "
                      "mjrl_host_stage_rows_f64x into pinned per-slot slabs, each trajectory copied to HBM when it "

@@ -537,7 +537,8 @@ __global__ void __launch_bounds__(64 * GAE_WAVES) k_gae(const double* __restrict
 // Lanes = paths (round 6): the serial recurrences of LP_PATHS paths run side by side
 // in ONE instruction stream each, one wave per chain, each lane one path — wave 0
 // the returns (discount_sum(rewards, gamma)), wave 1 the advantages (discount_sum(td,
-// gamma lambda), idle without GAE), wave 2 the path-return sum (front to back).  A
+// gamma lambda), idle without GAE), wave 2 the path-return sum (front to back; on a
+// mover wave instead it measured slower, profiles/r06e/rejected/).  A
 // dependent fp64 multiply -> add costs ~11 cycles of issue per step for the whole
 // wave, however many lanes are on (profiles/r06b/gae_latency.txt), so LP_PATHS paths
 // advance for the price one did — as long as the chain wave does little else: a

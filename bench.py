@@ -466,8 +466,9 @@ def e2e_stream(paths_range, eng, th0, base, upd, device, cfg, nslots=64):
                 update_ms=round(float(np.median([r[3] for r in runs])), 2),
                 timesteps=T, slots=nslots,
                 note="StreamSink fed per lock step as the vectorised sampler feeds it (observation rows through "
-                     "mjrl_host_stage_rows_f64x into pinned per-slot slabs, each trajectory copied to HBM when it "
-                     "ends); post_sampling_ms = from the last trajectory's hand-over to the update's readback "
+                     "mjrl_host_stage_rows_f64x into pinned per-slot slabs, each trajectory copied to HBM in runs "
+                     "of StreamSink.FLUSH_ROWS rows as it is sampled and the rest when it ends); batch_ms = the "
+                     "last runs' copies and the 1-D slots, update_ms = the update after them; post_sampling_ms = from the last trajectory's hand-over to the update's readback "
                      "(the padded slabs are the batch when every path runs the full horizon, else one device "
                      "gather; offsets / flags; update); feed_ms = the sampler-side cost of the "
                      "hand-overs (spread over sampling, timed without environments); median of 2")

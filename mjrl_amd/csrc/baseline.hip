@@ -24,8 +24,9 @@
 //
 // QuadraticBaseline (quadratic_baseline.py:10-65) runs the same Gram with its own
 // features, o = clip(obs, +-10) / 10: [o, o_i o_j (i <= j, row-major), 1, a, a^2,
-// a^3, a^4] (n + n(n+1)/2 + 5 columns, n <= 64): each loader thread decodes its
-// eight columns of each panel once per launch (QCol) and forms them per row.
+// a^3, a^4] (n + n(n+1)/2 + 5 columns, n <= 64): o is formed once per value by
+// k_quad_obs (the f64 division off the Gram's loaders), each loader thread decodes
+// its eight columns of each panel once per launch (QCol) and forms them per row.
 #include <math.h>
 
 #include "common.h"
@@ -82,23 +83,24 @@ __device__ __forceinline__ double feat(const TO* __restrict__ obs, const float* 
 
 // QuadraticBaseline column g (quadratic_baseline.py:10-37) as (kind, i, j); the
 // augmented Gram appends the return as column n + nq + 5
+// (kind, i, j) packed in one int (kind << 16 | i << 8 | j; n <= 64): the loader's
+// sixteen decoded columns stay in sixteen registers
 enum QKind { Q_LIN, Q_QUAD, Q_ONE, Q_A1, Q_A2, Q_A3, Q_A4, Q_Y, Q_ZERO };
-struct QCol {
-    int kind, i, j;
-};
+typedef int QCol;
+__device__ __forceinline__ QCol qpack(int kind, int i, int j) { return kind << 16 | i << 8 | j; }
 __device__ __forceinline__ QCol qcol(int g, int n) {
     const int nq = n * (n + 1) / 2;
-    if (g < n) return {Q_LIN, g, 0};
+    if (g < n) return qpack(Q_LIN, g, 0);
     if (g < n + nq) {
         int r = g - n, i = 0;
         while (r >= n - i) {   // row i of the upper triangle holds n - i products
             r -= n - i;
             ++i;
         }
-        return {Q_QUAD, i, i + r};
+        return qpack(Q_QUAD, i, i + r);
     }
     const int t = g - n - nq;
-    return {t <= 5 ? Q_ONE + t : Q_ZERO, 0, 0};
+    return qpack(t <= 5 ? Q_ONE + t : Q_ZERO, 0, 0);
 }
 
 // o = clip(obs, +-10) / 10 (quadratic_baseline.py:12)
@@ -109,17 +111,35 @@ __device__ __forceinline__ double qobs(const TO* __restrict__ obs, const float* 
 }
 
 template <typename TO>
-__device__ __forceinline__ double qfeat(const TO* __restrict__ obs, const float* __restrict__ lo,
-                                        const double* __restrict__ y, const double* __restrict__ al, int64_t row,
-                                        QCol c, int n) {
-    switch (c.kind) {
-        case Q_LIN: return qobs(obs, lo, row * n + c.i);
-        case Q_QUAD: return qobs(obs, lo, row * n + c.i) * qobs(obs, lo, row * n + c.j);
+__global__ void __launch_bounds__(256) k_quad_obs(const TO* __restrict__ obs, const float* __restrict__ lo, int64_t N,
+                                                  double* __restrict__ o) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += stride) o[i] = qobs(obs, lo, i);
+}
+
+// the row's time features (quadratic_baseline.py:31-35): al ** 1 (numpy: the value
+// itself), al ** 2 (numpy: square), al ** 3 and al ** 4 (C pow), once per row
+struct QTime {
+    double a1, a2, a3, a4;
+};
+__device__ __forceinline__ QTime qtime(const double* __restrict__ al, int64_t row) {
+    const double a = al[row];
+    return {a, a * a, pow(a, 3.0), pow(a, 4.0)};
+}
+
+// column c of row `row` from o = clip(obs, +-10) / 10 formed beforehand (k_quad_obs:
+// the f64 divisions once per value, not once per product)
+__device__ __forceinline__ double qfeat(const double* __restrict__ o, const double* __restrict__ y,
+                                        const QTime& tm, int64_t row, QCol c, int n) {
+    const int ci = (c >> 8) & 0xff, cj = c & 0xff;
+    switch (c >> 16) {
+        case Q_LIN: return o[row * n + ci];
+        case Q_QUAD: return o[row * n + ci] * o[row * n + cj];
         case Q_ONE: return 1.0;
-        case Q_A1: return al[row];                          // al ** 1 (numpy: the value itself)
-        case Q_A2: return al[row] * al[row];                // al ** 2 (numpy: square)
-        case Q_A3: return pow(al[row], 3.0);                // al ** 3, al ** 4: C pow
-        case Q_A4: return pow(al[row], 4.0);
+        case Q_A1: return tm.a1;
+        case Q_A2: return tm.a2;
+        case Q_A3: return tm.a3;
+        case Q_A4: return tm.a4;
         case Q_Y: return y[row];
         default: return 0.0;
     }
@@ -164,22 +184,26 @@ __global__ void __launch_bounds__(GTHREADS, 2) k_gram(GramArgs<TO> a) {
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             const int gi = ti * GT + lc + u, gj = tj * GT + lc + u;
-            ci[u] = gi == nf ? QCol{Q_Y, 0, 0} : (gi > nf ? QCol{Q_ZERO, 0, 0} : qcol(gi, a.n));
-            cj[u] = gj == nf ? QCol{Q_Y, 0, 0} : (gj > nf ? QCol{Q_ZERO, 0, 0} : qcol(gj, a.n));
+            ci[u] = gi == nf ? qpack(Q_Y, 0, 0) : (gi > nf ? qpack(Q_ZERO, 0, 0) : qcol(gi, a.n));
+            cj[u] = gj == nf ? qpack(Q_Y, 0, 0) : (gj > nf ? qpack(Q_ZERO, 0, 0) : qcol(gj, a.n));
         }
     }
     auto gload = [&](int64_t c0) {
         const int64_t row = c0 + lr;
         const bool in = row < r1;
+        if (QUAD) {
+            const QTime tm = qtime(a.al, in ? row : r0);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                vi[u] = in ? qfeat((const double*)a.obs, a.y, tm, row, ci[u], a.n) : 0.0;
+                vj[u] = in ? qfeat((const double*)a.obs, a.y, tm, row, cj[u], a.n) : 0.0;
+            }
+            return;
+        }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            if (QUAD) {
-                vi[u] = in ? qfeat(a.obs, a.lo, a.y, a.al, row, ci[u], a.n) : 0.0;
-                vj[u] = in ? qfeat(a.obs, a.lo, a.y, a.al, row, cj[u], a.n) : 0.0;
-            } else {
-                vi[u] = in ? feat(a.obs, a.lo, a.y, a.al, row, ti * GT + lc + u, a.n) : 0.0;
-                vj[u] = in ? feat(a.obs, a.lo, a.y, a.al, row, tj * GT + lc + u, a.n) : 0.0;
-            }
+            vi[u] = in ? feat(a.obs, a.lo, a.y, a.al, row, ti * GT + lc + u, a.n) : 0.0;
+            vj[u] = in ? feat(a.obs, a.lo, a.y, a.al, row, tj * GT + lc + u, a.n) : 0.0;
         }
     };
     auto lstore = [&](int buf) {
@@ -281,9 +305,7 @@ __global__ void __launch_bounds__(256) k_linear_residual(const TO* __restrict__ 
 }
 
 // r_t = y_t - F_t . c with QuadraticBaseline's features (fit(return_errors=True))
-template <typename TO>
-__global__ void __launch_bounds__(256) k_quadratic_residual(const TO* __restrict__ obs, const float* __restrict__ lo,
-                                                            const double* __restrict__ y,
+__global__ void __launch_bounds__(256) k_quadratic_residual(const double* __restrict__ o, const double* __restrict__ y,
                                                             const double* __restrict__ al, int64_t T, int n,
                                                             const double* __restrict__ coef, double* __restrict__ out) {
     const int lane = threadIdx.x & 63;
@@ -291,13 +313,19 @@ __global__ void __launch_bounds__(256) k_quadratic_residual(const TO* __restrict
     const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
     for (int64_t row = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; row < T; row += nw) {
         double acc = 0.0;
-        for (int g = lane; g < nf; g += 64) acc += qfeat(obs, lo, y, al, row, qcol(g, n), n) * coef[g];
+        const QTime tm = qtime(al, row);
+        for (int g = lane; g < nf; g += 64) acc += qfeat(o, y, tm, row, qcol(g, n), n) * coef[g];
         acc = wave_sum(acc);
         if (lane == 0) out[row] = y[row] - acc;
     }
 }
 
 inline int err(hipError_t e) { return e == hipSuccess ? MJRL_OK : (int)e; }
+
+inline int grid_for(int64_t work, int per_block, int cap) {
+    int64_t g = (work + per_block - 1) / per_block;
+    return (int)(g < 1 ? 1 : (g > cap ? cap : g));
+}
 
 constexpr int QMAX_N = 64;   // QuadraticBaseline: n + n(n+1)/2 + 6 <= 2,150 Gram columns
 
@@ -335,9 +363,20 @@ static int linear_baseline_gram(const TO* obs, const float* lo, const double* re
         const int64_t g = (P + 3) / 4;
         hipLaunchKernelGGL(k_path_time, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, st, path_off, P, al);
     }
-    GramArgs<TO> ga{obs, lo, returns, al, T, n, ntile, npair, slab};
     const int groups = (GSLICES + 7) / 8;   // slices per XCD
-    hipLaunchKernelGGL((k_gram<TO, QUAD>), dim3(8 * groups * npair), dim3(GTHREADS), 0, st, ga);
+    if (QUAD) {
+        // o = clip(obs) / 10 once per value (scratch behind the path times), then the
+        // Gram over the features formed from it
+        double* o = al + T;
+        const int64_t N = T * (int64_t)n;
+        if (N > 0)
+            hipLaunchKernelGGL(k_quad_obs<TO>, dim3((unsigned)grid_for(N, 256, 8192)), dim3(256), 0, st, obs, lo, N, o);
+        GramArgs<double> ga{o, nullptr, returns, al, T, n, ntile, npair, slab};
+        hipLaunchKernelGGL((k_gram<double, true>), dim3(8 * groups * npair), dim3(GTHREADS), 0, st, ga);
+    } else {
+        GramArgs<TO> ga{obs, lo, returns, al, T, n, ntile, npair, slab};
+        hipLaunchKernelGGL((k_gram<TO, false>), dim3(8 * groups * npair), dim3(GTHREADS), 0, st, ga);
+    }
     const int64_t ne = (int64_t)npair * GT * GT;
     hipLaunchKernelGGL(k_gram_reduce, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st, slab, ntile, npair, K,
                        out);
@@ -363,10 +402,13 @@ static int linear_baseline_residual(const TO* obs, const float* lo, const double
         hipLaunchKernelGGL(k_path_time, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, st, path_off, P, al);
     }
     const int64_t g = (T + 3) / 4;
-    if (QUAD)
-        hipLaunchKernelGGL(k_quadratic_residual<TO>, dim3((unsigned)(g < 16384 ? g : 16384)), dim3(256), 0, st, obs,
-                           lo, returns, al, T, n, coeffs, out);
-    else
+    if (QUAD) {
+        double* o = al + T;
+        const int64_t N = T * (int64_t)n;
+        hipLaunchKernelGGL(k_quad_obs<TO>, dim3((unsigned)grid_for(N, 256, 8192)), dim3(256), 0, st, obs, lo, N, o);
+        hipLaunchKernelGGL(k_quadratic_residual, dim3((unsigned)(g < 16384 ? g : 16384)), dim3(256), 0, st, o, returns,
+                           al, T, n, coeffs, out);
+    } else
         hipLaunchKernelGGL(k_linear_residual<TO>, dim3((unsigned)(g < 16384 ? g : 16384)), dim3(256), 0, st, obs,
                            lo, returns, al, T, n, coeffs, out);
     return err(hipGetLastError());
@@ -415,7 +457,7 @@ int mjrl_quadratic_baseline_gram_scratch(int32_t n, int64_t T, int64_t* doubles)
     if (n <= 0 || n > QMAX_N || T < 0 || !doubles) return MJRL_EINVAL;
     int K, ntile, npair;
     gram_dims(n, K, ntile, npair, true);
-    *doubles = (int64_t)GSLICES * npair * GT * GT + T;
+    *doubles = (int64_t)GSLICES * npair * GT * GT + T + T * (int64_t)n;   // slabs, path times, o
     return MJRL_OK;
 }
 

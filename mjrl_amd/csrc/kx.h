@@ -283,11 +283,6 @@ constexpr bool KX_ABL_NOCHAIN = true;    // timing ablation only: the FVP's P2-P
 #else
 constexpr bool KX_ABL_NOCHAIN = false;
 #endif
-#ifdef MJRL_KX_EVAL_FOLD_PHASE
-constexpr bool KX_EVAL_P2FOLD = false;   // variant (A/B): EVAL folds the first layer's halves in its own phase
-#else
-constexpr bool KX_EVAL_P2FOLD = true;    // EVAL: P2 folds the halves + tanh while loading its operand (as FVP)
-#endif
 #ifdef MJRL_KX_ABL_NOCOLS
 constexpr bool KX_ABL_NOCOLS = true;     // timing ablation only: the FVP preamble's column scales not computed
 #else
@@ -699,20 +694,17 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) acc1[i][rr] *= Us[i * 16 + 4 * lq + rr] * wsc1;
         }
-        if (MODE == FVP || (MODE == EVAL && KX_EVAL_P2FOLD)) {
-            // FVP / EVAL: both observation-half partials go to LDS whole (kh = 0 -> D0,
-            // kh = 1 -> D0B) and P2 folds them while it loads its operand: no fold
-            // phase (EVAL: P2 forms tanh of the sum itself, its only reader of a0).  FVP:
-            // the cached activations of this wave's rows go into the a0 / a1 images.
+        if (MODE == FVP) {
+            // FVP: both observation-half partials go to LDS whole (kh = 0 -> D0, kh = 1 ->
+            // D0B) and P2 folds them while it loads its operand: no fold phase.  The
+            // cached activations of this wave's rows go into the a0 / a1 images.
             float* dst = kh ? D0B : D0;
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) dst[(i * 16 + 4 * lq + rr) * L::LD + cb * 16 + lr16] = acc1[i][rr];
-            if (MODE == FVP) {
-                astore4(A0i, cb * 16 + lr16, kh * 16 + 4 * lq, pa0);
-                astore4(A1i, cb * 16 + lr16, kh * 16 + 4 * lq, pa1);
-            }
+            astore4(A0i, cb * 16 + lr16, kh * 16 + 4 * lq, pa0);
+            astore4(A1i, cb * 16 + lr16, kh * 16 + 4 * lq, pa1);
             __syncthreads();
             KX_STAMP(1);
             KX_STAMP(2);
@@ -781,19 +773,7 @@ __global__ void __launch_bounds__(KT, 1) k_kx(RowArgs a, FOut o) {
 #pragma unroll
                 for (int s = 0; s < 2; ++s) {
                     half8 bh, bl, xh, xl;
-                    if (MODE == EVAL && KX_EVAL_P2FOLD) {
-                        // a0 = tanh(half 0 + half 1) of this lane's row and eight columns,
-                        // split as astore4 would store it (a * AHR: hi, lo) — the same bits
-                        // arow reads from the image the fold phase writes otherwise
-                        const int o = (kh * 16 + lr16) * L::LD + 32 * s + 8 * lq;
-                        const float8v pre = load8(D0 + o) + load8(D0B + o);
-                        float8v av;
-#pragma unroll
-                        for (int e = 0; e < 8; ++e) av[e] = tanhf(pre[e]);
-                        split8(av, AHR, xh, xl);
-                    } else {
-                        arow(A0i, kh, s, lq, lr16, xh, xl);
-                    }
+                    arow(A0i, kh, s, lq, lr16, xh, xl);
                     wrow(img, L::WIMG, j, s, lq, bh, bl);
                     acc = mfma_x3(xh, xl, bh, bl, acc);
                 }

@@ -8,7 +8,6 @@ import argparse
 import concurrent.futures as cf
 import os
 import subprocess
-import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)

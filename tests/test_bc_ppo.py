@@ -5,7 +5,6 @@ variants are in test_gpu_api.py."""
 import os
 
 import numpy as np
-import pytest
 import torch
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")

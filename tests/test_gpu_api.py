@@ -342,6 +342,46 @@ def test_gae_kernel_ragged_many_paths(use_gae, fn):
     assert np.all(pr[~keep] == 0.0)
 
 
+@pytest.mark.parametrize("seed", [0, 1, 2, 3])
+def test_gae_kernel_random_lengths(seed):
+    """mjrl_gae on random batches (P in [1, 300], lengths in [0, 1200] with exact
+    multiples of the 16-step segment and the 256-step window mixed in, random
+    termination flags, GAE on and off): bit-identical to the oracle's chains."""
+    from mjrl_amd import _lib
+    from oracle import npg_cpu as O
+    L = _lib.lib()
+    rs = np.random.RandomState(100 + seed)
+    P = int(rs.randint(1, 301))
+    lengths = rs.randint(0, 1201, size=P)
+    pick = rs.rand(P)
+    lengths[pick < 0.15] = 16 * rs.randint(0, 40, size=int((pick < 0.15).sum()))
+    lengths[pick > 0.9] = 256 * rs.randint(1, 5, size=int((pick > 0.9).sum()))
+    T = int(lengths.sum())
+    rew = rs.randn(T) * 2.0
+    base = rs.randn(T)
+    term = (rs.rand(P) < 0.5).astype(np.uint8)
+    off = np.concatenate([[0], np.cumsum(lengths)]).astype(np.int64)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()   # noqa: E731
+    keep = lengths > 0
+    m = np.repeat(keep, lengths)
+    for use_gae in (1, 0):
+        ret = torch.full((max(T, 1),), np.nan, dtype=torch.float64, device="cuda")
+        adv = torch.full((max(T, 1),), np.nan, dtype=torch.float64, device="cuda")
+        pret = torch.full((P,), np.nan, dtype=torch.float64, device="cuda")
+        gamma, lam = 0.995, 0.97
+        rc = L.mjrl_gae(_lib.ptr(t(rew)), _lib.ptr(t(base)), _lib.ptr(t(off)), _lib.ptr(t(term)), P, gamma, lam,
+                        use_gae, _lib.ptr(ret), _lib.ptr(adv), _lib.ptr(pret), _lib.stream_ptr())
+        assert rc == 0
+        torch.cuda.synchronize()
+        r_ref, a_ref = O.returns_and_advantages(rew[m], base[m], lengths[keep], term[keep].astype(bool), gamma,
+                                                lam if use_gae else None)
+        assert np.array_equal(ret.cpu().numpy()[:T], r_ref)
+        assert np.array_equal(adv.cpu().numpy()[:T], a_ref)
+        pr = pret.cpu().numpy()
+        assert np.array_equal(pr[keep], np.array([sum(r) for r in O.split(rew[m], lengths[keep])]))
+        assert np.all(pr[~keep] == 0.0)
+
+
 @pytest.mark.parametrize("use_gae", [1, 0])
 def test_gae_kernel_multiwindow_bitexact(use_gae):
     """mjrl_gae through the C-ABI on paths shorter than, equal to and longer

@@ -364,12 +364,13 @@ def test_gae_kernel_random_lengths(seed):
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()   # noqa: E731
     keep = lengths > 0
     m = np.repeat(keep, lengths)
+    d_rew, d_base, d_off, d_term = t(rew), t(base), t(off), t(term)   # alive across the launches
     for use_gae in (1, 0):
         ret = torch.full((max(T, 1),), np.nan, dtype=torch.float64, device="cuda")
         adv = torch.full((max(T, 1),), np.nan, dtype=torch.float64, device="cuda")
         pret = torch.full((P,), np.nan, dtype=torch.float64, device="cuda")
         gamma, lam = 0.995, 0.97
-        rc = L.mjrl_gae(_lib.ptr(t(rew)), _lib.ptr(t(base)), _lib.ptr(t(off)), _lib.ptr(t(term)), P, gamma, lam,
+        rc = L.mjrl_gae(_lib.ptr(d_rew), _lib.ptr(d_base), _lib.ptr(d_off), _lib.ptr(d_term), P, gamma, lam,
                         use_gae, _lib.ptr(ret), _lib.ptr(adv), _lib.ptr(pret), _lib.stream_ptr())
         assert rc == 0
         torch.cuda.synchronize()
